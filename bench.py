@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training images/sec for ViT-B/16 @224 px, bf16, on 1..8 MI355X (BASELINE.json).
+
+One process per GPU (``torch.distributed.run``), RCCL gradient all-reduce via the framework's
+bucketed DDP. Each step is a full training step of the reference recipe: forward, mean
+cross-entropy, backward, global-norm clip 1.0, Adam (wd 0.03 on weights, 0 on biases/norms) and a
+per-step LR-schedule update. Synthetic ImageNet-shaped inputs (random [B,3,224,224], 1000 classes)
+and random-init weights: there is no dataset or checkpoint access.
+
+Prints ONE JSON line (rank 0). ``value`` is whole-job images/sec = global_batch * steps / max-rank
+elapsed time, where the timed region is bracketed by barrier + device synchronize on both sides.
+
+  python bench.py                          # 1 GPU, batch 256
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+  python bench.py --impl torch             # reference-style eager PyTorch (nn modules + autocast bf16)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 256 @1 GPU, 512/GPU @>1)")
+    p.add_argument("--model", default="vit_b16")
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--num-classes", type=int, default=1000)
+    p.add_argument("--impl", choices=["fused", "torch"], default="fused")
+    p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    if args.impl == "torch":
+        os.environ["PVR_DISABLE_FUSED"] = "1"
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_vit_paper_replication_amd.models import vit
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    n = max(args.gpus, world_env)
+    rank, world, device = init_distributed()
+    per_gpu = args.batch or (256 if world == 1 else 512)
+    torch.manual_seed(1234)
+
+    model = vit(args.model, image_size=args.image_size, num_classes=args.num_classes).to(device)
+    groups = param_groups_weight_decay(model, 0.03)
+    total_steps = args.warmup + args.steps
+    if args.impl == "fused":
+        opt = FusedAdam(groups, lr=1e-3, betas=(0.9, 0.999))
+    else:
+        opt = torch.optim.Adam(groups, lr=1e-3, betas=(0.9, 0.999))
+    sched = warmup_linear_decay(opt, max(total_steps, 20), 0.05)
+    net = DistributedDataParallel(model) if world > 1 else model
+
+    g = torch.Generator(device=device).manual_seed(rank)
+    x = torch.rand(per_gpu, 3, args.image_size, args.image_size, device=device, generator=g)
+    y = torch.randint(0, args.num_classes, (per_gpu,), device=device, generator=g)
+
+    def step():
+        net.train()
+        if args.impl == "fused":
+            logits = net(x)
+            loss = cross_entropy(logits, y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step(clip_norm=1.0)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = net(x)
+                loss = torch.nn.functional.cross_entropy(logits.float(), y)
+            opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            opt.step()
+        sched.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    if args.profile_out and rank == 0:
+        from pytorch_vit_paper_replication_amd.utils.profiling import profile_steps
+
+        profile_steps(step, steps=2, out_path=args.profile_out)
+
+    global_batch = per_gpu * world
+    ips = global_batch * args.steps / elapsed
+    name = {"vit_b16": "ViT-B/16", "vit_l16": "ViT-L/16", "vit_h14": "ViT-H/14"}.get(args.model, args.model)
+    seq = (args.image_size // int(model.config["patch_size"])) ** 2 + 1
+    if rank == 0:
+        out = {
+            "metric": "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X",
+            "value": round(ips, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random [B,3,224,224] in [0,1), 1000 classes, random-init weights)",
+            "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
+                       "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl,
+                       "optimizer": "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
+                       "dropout": "0.1 (mlp, embedding)", "final_loss": round(final_loss, 4)},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+"""Loader for the in-tree gfx950 extension ``_C`` (built by :mod:`.build`).
+
+Policy: on a GPU tensor the fused HIP path is mandatory. If the extension cannot be loaded while a
+GPU is present, :func:`use_fused` raises instead of silently running PyTorch fallbacks — set
+``PVR_ALLOW_TORCH_FALLBACK=1`` to opt into the plain-PyTorch path on purpose (that is how the
+reference-style baseline is benchmarked). On CPU the PyTorch reference path always runs.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_C = None
+_ERR: BaseException | None = None
+_TRIED = False
+
+
+def load():
+    """Import the compiled extension once; returns the module or None."""
+    global _C, _ERR, _TRIED
+    if _TRIED:
+        return _C
+    _TRIED = True
+    try:
+        from . import _C as mod  # noqa: F401  (built in-tree)
+
+        _C = mod
+    except BaseException as e:  # pragma: no cover - depends on build state
+        _ERR = e
+        if os.environ.get("PVR_AUTOBUILD", "0") == "1":
+            try:
+                from .build import build_extension
+
+                build_extension()
+                from . import _C as mod2
+
+                _C = mod2
+                _ERR = None
+            except BaseException as e2:
+                _ERR = e2
+    return _C
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def ext():
+    m = load()
+    if m is None:
+        raise RuntimeError(
+            "pytorch_vit_paper_replication_amd: the gfx950 extension _C is not built or failed to load "
+            f"({_ERR!r}). Build it with `python -m pytorch_vit_paper_replication_amd.build`."
+        )
+    return m
+
+
+def fallback_allowed() -> bool:
+    return os.environ.get("PVR_ALLOW_TORCH_FALLBACK", "0") == "1"
+
+
+def fused_disabled() -> bool:
+    return os.environ.get("PVR_DISABLE_FUSED", "0") == "1"
+
+
+def use_fused(t: torch.Tensor) -> bool:
+    """True when ``t`` lives on the GPU and the HIP kernels should run on it."""
+    if not t.is_cuda:
+        return False
+    if fused_disabled():
+        return False
+    if available():
+        return True
+    if fallback_allowed():
+        return False
+    ext()  # raises with the load error
+    return False

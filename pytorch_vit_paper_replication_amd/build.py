@@ -1,0 +1,113 @@
+"""In-tree native build of the gfx950 extension (``_C``).
+
+The HIP kernels (``csrc/*.hip``) are compiled by ``hipcc --offload-arch=gfx950`` into object files
+without any torch headers; only ``csrc/bindings.cpp`` sees ATen/pybind11 and is compiled by the host
+C++ compiler. Everything is linked into ``pytorch_vit_paper_replication_amd/_C<EXT_SUFFIX>`` next to
+this file so that the built library travels with the source tree (and is what the GPU box loads).
+
+Rebuilds are incremental (per-object source/header mtime check) and the objects compile in parallel.
+Run ``python -m pytorch_vit_paper_replication_amd.build`` (or ``build_extension()``) to build.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+CSRC = PKG_DIR / "csrc"
+BUILD_DIR = PKG_DIR / "_build"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+if ARCH != "gfx950":  # this framework is written for CDNA4 only
+    ARCH = "gfx950"
+
+
+def ext_path() -> Path:
+    return PKG_DIR / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _torch_dirs():
+    import torch
+
+    tdir = Path(torch.__file__).resolve().parent
+    return tdir / "include", tdir / "lib"
+
+
+def _hipcc() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    return str(Path(rocm) / "bin" / "hipcc")
+
+
+def _newer(src_files, target: Path) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(s).stat().st_mtime > t for s in src_files)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build command failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build_extension(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
+    """Compile every HIP kernel for gfx950 and link the torch extension. Returns the .so path."""
+    BUILD_DIR.mkdir(exist_ok=True)
+    inc, lib = _torch_dirs()
+    py_inc = sysconfig.get_paths()["include"]
+    headers = list(CSRC.glob("*.h"))
+    hip_srcs = sorted(CSRC.glob("*.hip"))
+    objs = []
+    jobs_list = []
+    hip_flags = [
+        f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
+        "-munsafe-fp-atomics", "-Wno-unused-result",
+    ]
+    for src in hip_srcs:
+        obj = BUILD_DIR / (src.stem + ".o")
+        objs.append(obj)
+        if force or _newer([src, *headers], obj):
+            jobs_list.append([_hipcc(), *hip_flags, "-c", str(src), "-o", str(obj)])
+    bind_src = CSRC / "bindings.cpp"
+    bind_obj = BUILD_DIR / "bindings.o"
+    objs.append(bind_obj)
+    if force or _newer([bind_src], bind_obj):
+        cxx = os.environ.get("CXX", "g++")
+        import torch
+
+        abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+        jobs_list.append([
+            cxx, "-O2", "-std=c++17", "-fPIC", "-c", str(bind_src), "-o", str(bind_obj),
+            "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+            "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+            f"-I{inc}", f"-I{inc / 'torch' / 'csrc' / 'api' / 'include'}", "-I/opt/rocm/include", f"-I{py_inc}",
+            "-w",
+        ])
+    if jobs_list:
+        n = jobs or min(len(jobs_list), max(1, (os.cpu_count() or 4)), 16)
+        with cf.ThreadPoolExecutor(max_workers=n) as ex:
+            for out in ex.map(_run, jobs_list):
+                if verbose and out.strip():
+                    print(out)
+    so = ext_path()
+    if force or jobs_list or not so.exists():
+        link = [
+            _hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(so),
+            f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
+            f"-Wl,-rpath,{lib}",
+        ]
+        _run(link)
+        if verbose:
+            print(f"[build] linked {so}")
+    return so
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    p = build_extension(verbose=True, force=force)
+    print(p)

@@ -1,0 +1,437 @@
+// Multi-head self-attention forward/backward for ViT (no mask, head_dim 64), gfx950.
+//
+// Replaces nn.MultiheadAttention's scaled_dot_product_attention core (reference models/vit.py:86-97;
+// SURVEY.md K7). Q, K and V are read in place from the fused QKV GEMM output [tokens][3*D]
+// (row = token, head h at columns h*64, D + h*64, 2D + h*64), so there are no head transposes.
+//
+// Forward: one workgroup = 4 waves = 64 queries of one (batch, head); each wave owns 16 queries
+// and computes S^T = K . Q^T so that the query sits on the MFMA lane: the softmax row reduction
+// over keys is then in-register plus two cross-lane steps, and P^T is directly the B operand of
+// O^T = V^T . P^T (V^T read with ds_read_b64_tr_b16). K/V tiles of 64 keys are LDS-DMA staged
+// (two stages) with an online softmax, so any sequence length works (197, 257, 577 tokens...).
+// The log-sum-exp per query is saved for the backward.
+//
+// Backward: one workgroup covers up to 256 keys of one (batch, head); each wave keeps its 32
+// keys' K and V fragments in registers and accumulates dK^T, dV^T over all query blocks of 32
+// (key on the lane: S and dP accumulators are directly the B operands of the dV/dK products).
+// dS crosses LDS once for dQ = dS . K, which the waves split by output fragment, so dQ needs no
+// atomics when one workgroup holds every key (N <= 256).
+#include "common.h"
+
+namespace pvr {
+namespace {
+
+constexpr int DH = 64;
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+// XOR on the 16-B chunk index of 128-B rows: conflict-free for row reads (ds_read_b128, 16 rows x
+// one chunk), and for transposed reads of rows {4g+q, 16+4g+q} and {8g+q, 8g+4+q}.
+PVR_DEV int swz_a(int r) { return (((r >> 1) & 1) << 1) ^ (((r >> 2) & 1) << 2) ^ (((r >> 3) & 1) * 5); }
+
+PVR_DEV int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ swz_a(row)) << 4); }
+
+// DMA `rows` rows (multiple of 8) of a [row][64] bf16 operand into a swizzled 128-B-row LDS image.
+// Row r of the image comes from element offset (r * ld) of the buffer resource.
+PVR_DEV void dma_rows(__amdgpu_buffer_rsrc_t rs, char* lds, int rows, int64_t ld, int row_base, int wave, int nwaves, int lane) {
+  for (int s = wave; s < rows / 8; s += nwaves) {
+    const int row = s * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz_a(row);
+    const uint32_t voff = (uint32_t)((int64_t)(row_base + row) * ld * 2 + c * 16);
+    dma16(rs, to_lds(lds + s * 1024), voff);
+  }
+}
+
+// 16x32 operand fragment from a swizzled image, rows r0 + (l&15), k = 32ks + 8(l>>4) + j.
+PVR_DEV v8s frag_rows(const char* img, int r0, int ks, int lane) {
+  return ds_read_b128(img + lds_off(r0 + (lane & 15), ks * 4 + (lane >> 4)));
+}
+
+// Transposed fragment: lane i (of group g) gets img[row_of(g, j)][c0 + i] for j = 0..7 where rows are
+// rowA + q (j = q) and rowB + q (j = 4 + q); cols c0..c0+15 (c0 multiple of 16).
+PVR_DEV v8s frag_tr(const char* img, int rowA, int rowB, int c0, int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const int chunk = (c0 >> 3) + (p >> 1);
+  const v4s lo = ds_read_tr(img + lds_off(rowA + q, chunk) + 8 * (p & 1));
+  const v4s hi = ds_read_tr(img + lds_off(rowB + q, chunk) + 8 * (p & 1));
+  return cat44(lo, hi);
+}
+
+PVR_DEV v8s pack_p(const v4f& a, const v4f& b) {
+  v8s r;
+  const uint32_t w0 = pack2bf(a[0], a[1]), w1 = pack2bf(a[2], a[3]);
+  const uint32_t w2 = pack2bf(b[0], b[1]), w3 = pack2bf(b[2], b[3]);
+  r[0] = (short)(w0 & 0xFFFF); r[1] = (short)(w0 >> 16);
+  r[2] = (short)(w1 & 0xFFFF); r[3] = (short)(w1 >> 16);
+  r[4] = (short)(w2 & 0xFFFF); r[5] = (short)(w2 >> 16);
+  r[6] = (short)(w3 & 0xFFFF); r[7] = (short)(w3 >> 16);
+  return r;
+}
+
+PVR_DEV uint32_t clamp_bytes(int64_t b) { return b < 0 ? 0u : (b > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)b); }
+
+// ----------------------------------------------------------------------------------- forward
+__global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
+                                                        int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale) {
+  constexpr int KT = 64;                       // keys per tile
+  constexpr int TILE_BYTES = KT * DH * 2;      // 8 KiB
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [stage][K|V]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int q0 = blockIdx.x * 64 + wave * 16;
+
+  const uint16_t* base = qkv + (int64_t)b * N * ld;
+  const int64_t extent = ((int64_t)(N - 1) * ld + DH) * 2;
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(base + D + h * DH, clamp_bytes(extent));
+  const __amdgpu_buffer_rsrc_t vrs = make_rsrc(base + 2 * D + h * DH, clamp_bytes(extent));
+
+  // Q fragments (B operand): lane holds Q[q0 + li][32ks + 8g + j]
+  v8s qf[2];
+  {
+    const int q = min(q0 + li, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const v8s*)(base + (int64_t)q * ld + h * DH + ks * 32 + 8 * g);
+  }
+
+  const float c = scale * LOG2E;
+  float m_run = -INFINITY, l_run = 0.f;
+  v4f o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = (N + KT - 1) / KT;
+  dma_rows(krs, smem, KT, ld, 0, wave, 4, lane);
+  dma_rows(vrs, smem + TILE_BYTES, KT, ld, 0, wave, 4, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const char* kimg = smem + (t & 1) * 2 * TILE_BYTES;
+    const char* vimg = kimg + TILE_BYTES;
+    if (t + 1 < ntiles) {
+      char* nk = smem + ((t + 1) & 1) * 2 * TILE_BYTES;
+      dma_rows(krs, nk, KT, ld, (t + 1) * KT, wave, 4, lane);
+      dma_rows(vrs, nk + TILE_BYTES, KT, ld, (t + 1) * KT, wave, 4, lane);
+    }
+    // S^T[key][q] for 4 key fragments
+    v4f s[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      s[f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) s[f] = mfma16(frag_rows(kimg, 16 * f, ks, lane), qf[ks], s[f]);
+    }
+    const int kbase = t * KT;
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kbase + 16 * f + 4 * g + r;
+        const float v = key < N ? s[f][r] * c : -INFINITY;
+        s[f][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = exp2f(m_run - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = exp2f(s[f][r] - m_new);
+        s[f][r] = pv;
+        psum += pv;
+      }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] *= alpha;
+    // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const v8s vf = frag_tr(vimg, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane);
+        o[e] = mfma16(vf, pf, o[e]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  const int q = q0 + li;
+  if (q < N) {
+    const float inv = 1.f / l_run;
+    uint16_t* orow = out + ((int64_t)b * N + q) * ld_o + h * DH;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint2 w;
+      w.x = pack2bf(o[e][0] * inv, o[e][1] * inv);
+      w.y = pack2bf(o[e][2] * inv, o[e][3] * inv);
+      *(uint2*)(orow + 16 * e + 4 * g) = w;
+    }
+    if (g == 0) lse[(int64_t)bh * N + q] = (m_run + __log2f(l_run)) * LN2;
+  }
+}
+
+// ------------------------------------------------------------------------- backward: delta
+// delta[bh][q] = sum_d dO[q][h*64 + d] * O[q][h*64 + d]
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                              const uint16_t* __restrict__ o, int64_t ld_o,
+                                                              float* __restrict__ delta, int B, int N, int H) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= (int64_t)B * N * H) return;
+  const int h = (int)(i % H);
+  const int64_t tok = i / H;
+  const int b = (int)(tok / N), q = (int)(tok % N);
+  const uint16_t* a = dout + tok * ld_do + h * DH;
+  const uint16_t* bb = o + tok * ld_o + h * DH;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < DH / 8; ++c) {
+    const uint4 x = *(const uint4*)(a + c * 8), y = *(const uint4*)(bb + c * 8);
+    const uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      s += bf2f(xa[j] & 0xFFFF) * bf2f(ya[j] & 0xFFFF) + bf2f(xa[j] >> 16) * bf2f(ya[j] >> 16);
+  }
+  delta[((int64_t)b * H + h) * N + q] = s;
+}
+
+// ------------------------------------------------------------------------- backward: main
+// grid (nkb, B*H), block NW*64 (NW in {1,2,4,8}); workgroup keys [kb*KB, kb*KB + KB), KB = 32*NW.
+__global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                        const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                        const float* __restrict__ lse, const float* __restrict__ delta,
+                                                        uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
+                                                        int N, int H, int D, float scale) {
+  constexpr int QB = 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int NW = blockDim.x >> 6;
+  const int KB = NW * 32;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int kb0 = blockIdx.x * KB;
+  const int kw0 = kb0 + wave * 32;
+
+  // LDS carve: K image [KB][64] | Q blk [32][64] | dO blk [32][64] | dS [32][KB] | lse2[32] | delta[32]
+  char* kimg = smem;
+  char* qimg = kimg + KB * 128;
+  char* doimg = qimg + QB * 128;
+  char* dsimg = doimg + QB * 128;
+  float* s_lse = (float*)(dsimg + QB * KB * 2);
+  float* s_del = s_lse + QB;
+  const int ds_cpr = KB / 8;  // 16-B chunks per dS row (power of two)
+
+  const uint16_t* base = qkv + (int64_t)b * N * ld;
+  const int64_t extent = ((int64_t)(N - 1) * ld + DH) * 2;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(base + h * DH, clamp_bytes(extent));
+  const __amdgpu_buffer_rsrc_t krs = make_rsrc(base + D + h * DH, clamp_bytes(extent));
+  const uint16_t* dobase = dout + (int64_t)b * N * ld_do;
+  const __amdgpu_buffer_rsrc_t dors = make_rsrc(dobase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2));
+
+  // own keys' K and V fragments (B operands): lane holds X[kw0 + 16f + li][32ks + 8g + j]
+  v8s kf[2][2], vf[2][2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int key = kw0 + 16 * f + li;
+    const bool ok = key < N;
+    const int kc = ok ? key : 0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v8s kk = *(const v8s*)(base + (int64_t)kc * ld + D + h * DH + ks * 32 + 8 * g);
+      v8s vv = *(const v8s*)(base + (int64_t)kc * ld + 2 * D + h * DH + ks * 32 + 8 * g);
+      if (!ok) { kk = v8s{0, 0, 0, 0, 0, 0, 0, 0}; vv = kk; }
+      kf[f][ks] = kk;
+      vf[f][ks] = vv;
+    }
+  }
+  // whole key block's K image for the dQ product
+  dma_rows(krs, kimg, KB, ld, kb0, wave, NW, lane);
+
+  v4f dk[4][2], dv[4][2];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int f = 0; f < 2; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const float c = scale * LOG2E;
+  const int nqb = (N + QB - 1) / QB;
+  for (int qb = 0; qb < nqb; ++qb) {
+    const int q0 = qb * QB;
+    dma_rows(qrs, qimg, QB, ld, q0, wave, NW, lane);
+    dma_rows(dors, doimg, QB, ld_do, q0, wave, NW, lane);
+    if (threadIdx.x < QB) {
+      const int q = q0 + threadIdx.x;
+      s_lse[threadIdx.x] = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
+      s_del[threadIdx.x] = q < N ? delta[(int64_t)bh * N + q] : 0.f;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]
+    v4f s[2][2], dp[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) s[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const v8s qa = frag_rows(qimg, 16 * a, ks, lane);
+        const v8s da = frag_rows(doimg, 16 * a, ks, lane);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          s[a][f] = mfma16(qa, kf[f][ks], s[a][f]);
+          dp[a][f] = mfma16(da, vf[f][ks], dp[a][f]);
+        }
+      }
+    }
+    // P and dS
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * a + 4 * g + r;
+        const float l2 = s_lse[ql], dl = s_del[ql];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const float pv = exp2f(s[a][f][r] * c - l2);
+          s[a][f][r] = pv;
+          dp[a][f][r] = pv * (dp[a][f][r] - dl);
+        }
+      }
+    // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const v8s pf = pack_p(s[0][f], s[1][f]);
+      const v8s sf = pack_p(dp[0][f], dp[1][f]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const v8s dot = frag_tr(doimg, 4 * g, 16 + 4 * g, 16 * e, lane);
+        const v8s qt = frag_tr(qimg, 4 * g, 16 + 4 * g, 16 * e, lane);
+        dv[e][f] = mfma16(dot, pf, dv[e][f]);
+        dk[e][f] = mfma16(qt, sf, dk[e][f]);
+      }
+    }
+    // dS -> LDS (bf16) [q][key_local], chunk-swizzled by row for the dQ row reads
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * a + 4 * g + r;
+          const int kl = wave * 32 + 16 * f + li;
+          const int chunk = (kl >> 3) ^ (ql & (ds_cpr - 1) & 15);
+          *(uint16_t*)(dsimg + ql * KB * 2 + chunk * 16 + (kl & 7) * 2) = f2bf(dp[a][f][r]);
+        }
+    __syncthreads();
+    // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 8 output fragments split over the waves
+    for (int fr = wave; fr < 8; fr += NW) {
+      const int a = fr >> 2, e = fr & 3;
+      v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < KB / 32; ++ks) {
+        const int ql = 16 * a + li;
+        const int chunk = (ks * 4 + g) ^ (ql & (ds_cpr - 1) & 15);
+        const v8s af = ds_read_b128(dsimg + ql * KB * 2 + chunk * 16);
+        const v8s bf = frag_tr(kimg, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane);
+        acc = mfma16(af, bf, acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + 16 * a + 4 * g + r;
+        if (q < N) {
+          const float val = acc[r] * scale;
+          if (dq_acc)
+            atomicAdd(dq_acc + ((int64_t)b * N + q) * D + h * DH + 16 * e + li, val);
+          else
+            dqkv[((int64_t)b * N + q) * ld_dq + h * DH + 16 * e + li] = f2bf(val);
+        }
+      }
+    }
+  }
+  // dK, dV stores: lane holds X^T[d = 16e + 4g + r][key = kw0 + 16f + li]
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int key = kw0 + 16 * f + li;
+    if (key >= N) continue;
+    uint16_t* row = dqkv + ((int64_t)b * N + key) * ld_dq;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint2 wk, wv;
+      wk.x = pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale);
+      wk.y = pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale);
+      wv.x = pack2bf(dv[e][f][0], dv[e][f][1]);
+      wv.y = pack2bf(dv[e][f][2], dv[e][f][3]);
+      *(uint2*)(row + D + h * DH + 16 * e + 4 * g) = wk;
+      *(uint2*)(row + 2 * D + h * DH + 16 * e + 4 * g) = wv;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
+                                                          int64_t rows, int D) {
+  const int64_t n = rows * D;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / D;
+    const int d = (int)(i % D);
+    dqkv[r * ld_dq + d] = f2bf(acc[i]);
+  }
+}
+
+}  // namespace
+}  // namespace pvr
+
+extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
+                                   int H, int D, float scale, hipStream_t s) {
+  using namespace pvr;
+  if (D != H * DH || B <= 0 || N <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((N + 63) / 64, B * H), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
+  return hipGetLastError();
+}
+
+extern "C" int pvr_attn_bwd_waves(int N) {
+  const int need = (N + 31) / 32;
+  return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
+}
+
+// dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
+extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                   int B, int N, int H, int D, float scale, hipStream_t s) {
+  using namespace pvr;
+  if (D != H * DH || B <= 0 || N <= 0) return hipErrorInvalidValue;
+  const int64_t nrows = (int64_t)B * N * H;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, dout, ld_do, out, ld_o, delta, B, N, H);
+  const int NW = pvr_attn_bwd_waves(N);
+  const int KB = NW * 32;
+  const int nkb = (N + KB - 1) / KB;
+  if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
+  const size_t smem = (size_t)KB * 128 + 2 * 32 * 128 + 32 * KB * 2 + 2 * 32 * 4;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(nkb, B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
+                     nkb > 1 ? dq_acc : nullptr, N, H, D, scale);
+  if (nkb > 1) {
+    const int64_t rows = (int64_t)B * N;
+    int64_t blocks = (rows * D + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dq_acc, dqkv, ld_dq, rows, D);
+  }
+  return hipGetLastError();
+}

@@ -1,0 +1,300 @@
+// pybind11 / ATen bindings for the gfx950 kernels. Every entry point launches on PyTorch's current
+// HIP stream (so it composes with torch streams, events and hipGraph capture) and validates dtypes,
+// shapes and strides before touching device memory.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+namespace pvr {
+struct GemmParams {
+  int M, N, K;
+  const uint16_t* A; int64_t lda; int a_kcontig;
+  const uint16_t* B; int64_t ldb; int b_kcontig;
+  void* C; int64_t ldc;
+  const float* bias;
+  const uint16_t* resid; int64_t ld_resid;
+  const float* addend; int addend_period;
+  uint16_t* aux; int64_t ld_aux;
+  int row_group, row_stride_group, row_offset;
+  const uint64_t* seed_ptr; uint64_t seed_offset; uint32_t drop_thr; float drop_scale;
+  int k_split_len;
+  int epi;
+  int tile_cfg;
+};
+struct AdamGroup {
+  float lr, beta1, beta2, eps, weight_decay;
+  float bc1, bc2_sqrt;
+  int decoupled;
+};
+}  // namespace pvr
+
+extern "C" {
+hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
+hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
+hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, hipStream_t);
+hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
+hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
+hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+hipError_t pvr_xent(const float*, int64_t, const int64_t*, int, int, float*, float*, int*, float, hipStream_t);
+int pvr_norm_partial_blocks();
+hipError_t pvr_grad_norm(const float*, int64_t, float, float*, float*, hipStream_t);
+hipError_t pvr_adam(float*, const float*, float*, float*, uint16_t*, int64_t, const int64_t*, const int*, int, const pvr::AdamGroup*, const float*, int, hipStream_t);
+hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
+hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "pvr kernel '", what, "' failed: ", hipGetErrorString(e));
+}
+
+const uint16_t* bf(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+uint16_t* bf_mut(torch::Tensor& t, const char* name) { return const_cast<uint16_t*>(bf(t, name)); }
+const float* f32(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32, got ", t.scalar_type());
+  return t.data_ptr<float>();
+}
+float* f32_mut(torch::Tensor& t, const char* name) { return const_cast<float*>(f32(t, name)); }
+
+template <class T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// 2-D row-major view check: last-dim contiguous, returns leading dimension (elements)
+int64_t ld_of(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have unit stride in its last dim");
+  TORCH_CHECK(t.stride(0) % 8 == 0 || t.size(0) == 1, name, " leading dimension must be a multiple of 8 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+  return t.size(0) == 1 ? t.size(1) : t.stride(0);
+}
+
+// C = A . B^T with the given operand layouts; see csrc/gemm.hip for the epilogue contract.
+void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torch::Tensor C, int64_t M, int64_t N, int64_t K,
+          int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> addend,
+          int64_t addend_period, c10::optional<torch::Tensor> aux, int64_t row_group, int64_t row_stride_group,
+          int64_t row_offset, c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, int64_t k_split,
+          int64_t tile_cfg) {
+  pvr::GemmParams p{};
+  p.M = (int)M; p.N = (int)N; p.K = (int)K;
+  p.A = bf(A, "A"); p.lda = ld_of(A, "A"); p.a_kcontig = a_kcontig;
+  p.B = bf(B, "B"); p.ldb = ld_of(B, "B"); p.b_kcontig = b_kcontig;
+  TORCH_CHECK(N % 8 == 0, "gemm: N must be a multiple of 8");
+  if (a_kcontig) TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64 for a k-contiguous A");
+  if (b_kcontig) TORCH_CHECK(K % 64 == 0, "gemm: K must be a multiple of 64 for a k-contiguous B");
+  if (a_kcontig) {
+    TORCH_CHECK(A.size(0) >= M && A.size(1) >= K, "gemm: A too small");
+  } else {
+    TORCH_CHECK(A.size(0) >= K && A.size(1) >= M, "gemm: A too small");
+  }
+  if (b_kcontig) {
+    TORCH_CHECK(B.size(0) >= N && B.size(1) >= K, "gemm: B too small");
+  } else {
+    TORCH_CHECK(B.size(0) >= K && B.size(1) >= N, "gemm: B too small");
+  }
+  const bool f32out = epi >= 3;
+  TORCH_CHECK(C.is_cuda() && C.scalar_type() == (f32out ? torch::kFloat32 : torch::kBFloat16), "gemm: C dtype mismatch for epilogue");
+  p.C = C.data_ptr(); p.ldc = ld_of(C, "C");
+  if (bias.has_value() && bias->defined()) { TORCH_CHECK(bias->numel() >= N && bias->is_contiguous(), "bias"); p.bias = f32(*bias, "bias"); }
+  if (resid.has_value() && resid->defined()) { p.resid = bf(*resid, "resid"); p.ld_resid = ld_of(*resid, "resid"); }
+  if (addend.has_value() && addend->defined()) { p.addend = f32(*addend, "addend"); p.addend_period = (int)addend_period; TORCH_CHECK(addend_period > 0, "addend_period"); }
+  if (aux.has_value() && aux->defined()) { p.aux = const_cast<uint16_t*>(bf(*aux, "aux")); p.ld_aux = ld_of(*aux, "aux"); }
+  if (epi == 1 || epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm: GELU epilogues need aux");
+  p.row_group = (int)row_group; p.row_stride_group = (int)row_stride_group; p.row_offset = (int)row_offset;
+  if (drop_p > 0.0) {
+    TORCH_CHECK(seed.has_value() && seed->defined() && seed->scalar_type() == torch::kInt64, "dropout needs an int64 seed tensor");
+    p.seed_ptr = reinterpret_cast<const uint64_t*>(seed->data_ptr());
+    p.seed_offset = (uint64_t)seed_offset;
+    uint32_t thr = (uint32_t)llround(drop_p * 65536.0);
+    if (thr > 65535) thr = 65535;
+    p.drop_thr = thr;
+    p.drop_scale = (float)(65536.0 / (65536.0 - thr));
+  }
+  p.k_split_len = k_split > 0 ? (int)(((k_split + 63) / 64) * 64) : (int)(((K + 63) / 64) * 64);
+  p.epi = (int)epi;
+  p.tile_cfg = (int)tile_cfg;
+  check(pvr_gemm(&p, stream()), "gemm");
+}
+
+std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps, int64_t rows,
+                                         int64_t x_row_stride) {
+  const int64_t D = w.numel();
+  auto y = torch::empty({rows, D}, x.options());
+  auto mean = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  auto rstd = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  TORCH_CHECK(x.stride(-1) == 1, "layernorm: x last dim must be contiguous");
+  check(pvr_layernorm_fwd(bf(x, "x"), x_row_stride, f32(w, "w"), f32(b, "b"), bf_mut(y, "y"), D, f32_mut(mean, "mean"),
+                          f32_mut(rstd, "rstd"), (int)rows, (int)D, (float)eps, stream()),
+        "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t x_stride, torch::Tensor mean, torch::Tensor rstd,
+                   torch::Tensor w, c10::optional<torch::Tensor> dres, int64_t dres_stride, torch::Tensor dx, int64_t dx_stride,
+                   c10::optional<torch::Tensor> dw, c10::optional<torch::Tensor> db, int64_t rows) {
+  const int64_t D = w.numel();
+  check(pvr_layernorm_bwd(bf(dy, "dy"), dy_stride, bf(x, "x"), x_stride, f32(mean, "mean"), f32(rstd, "rstd"), f32(w, "w"),
+                          opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
+                          opt_ptr<float>(db), (int)rows, (int)D, stream()),
+        "layernorm_bwd");
+}
+
+void cast_f32_bf16(torch::Tensor in, torch::Tensor out) {
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "cast: shape/contiguity");
+  check(pvr_cast_f32_bf16(f32(in, "in"), bf_mut(out, "out"), in.numel(), stream()), "cast_f32_bf16");
+}
+
+void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tensor> db, c10::optional<torch::Tensor> dz,
+            c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p) {
+  uint32_t thr = 0;
+  float scale = 1.f;
+  const uint64_t* sp = nullptr;
+  if (drop_p > 0.0) {
+    TORCH_CHECK(seed.has_value() && seed->defined(), "colsum: dropout needs a seed");
+    sp = reinterpret_cast<const uint64_t*>(seed->data_ptr());
+    thr = (uint32_t)llround(drop_p * 65536.0);
+    if (thr > 65535) thr = 65535;
+    scale = (float)(65536.0 / (65536.0 - thr));
+  }
+  int64_t ldz = 0;
+  uint16_t* dzp = nullptr;
+  if (dz.has_value() && dz->defined()) { dzp = const_cast<uint16_t*>(bf(*dz, "dz")); ldz = ld_of(*dz, "dz"); }
+  check(pvr_colsum(bf(dy, "dy"), ld_of(dy, "dy"), (int)rows, (int)N, opt_ptr<float>(db), dzp, ldz, sp, (uint64_t)seed_offset, thr,
+                   scale, stream()),
+        "colsum");
+}
+
+void im2col(torch::Tensor img, torch::Tensor out, int64_t P, int64_t Kp) {
+  TORCH_CHECK(img.is_contiguous() && img.dim() == 4, "im2col: img must be contiguous NCHW");
+  check(pvr_im2col(f32(img, "img"), bf_mut(out, "out"), (int)img.size(0), (int)img.size(1), (int)img.size(2), (int)img.size(3),
+                   (int)P, (int)Kp, stream()),
+        "im2col");
+}
+
+void cls_rows(torch::Tensor cls, torch::Tensor pos, torch::Tensor out, int64_t B, int64_t D, int64_t row_stride,
+              c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p) {
+  uint32_t thr = 0;
+  float scale = 1.f;
+  const uint64_t* sp = nullptr;
+  if (drop_p > 0.0) {
+    sp = reinterpret_cast<const uint64_t*>(seed->data_ptr());
+    thr = (uint32_t)llround(drop_p * 65536.0);
+    if (thr > 65535) thr = 65535;
+    scale = (float)(65536.0 / (65536.0 - thr));
+  }
+  check(pvr_cls_rows(f32(cls, "cls"), f32(pos, "pos"), bf_mut(out, "out"), (int)B, (int)D, row_stride, sp, (uint64_t)seed_offset,
+                     thr, scale, stream()),
+        "cls_rows");
+}
+
+void patch_bwd(torch::Tensor dE, int64_t B, int64_t ntok, int64_t D, c10::optional<torch::Tensor> dpos, c10::optional<torch::Tensor> dcls,
+               c10::optional<torch::Tensor> dconv, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> seed,
+               int64_t seed_offset, double drop_p) {
+  uint32_t thr = 0;
+  float scale = 1.f;
+  const uint64_t* sp = nullptr;
+  if (drop_p > 0.0) {
+    sp = reinterpret_cast<const uint64_t*>(seed->data_ptr());
+    thr = (uint32_t)llround(drop_p * 65536.0);
+    if (thr > 65535) thr = 65535;
+    scale = (float)(65536.0 / (65536.0 - thr));
+  }
+  check(pvr_patch_bwd(bf(dE, "dE"), (int)B, (int)ntok, (int)D, opt_ptr<float>(dpos), opt_ptr<float>(dcls), opt_ptr<uint16_t>(dconv),
+                      opt_ptr<float>(dbias), sp, (uint64_t)seed_offset, thr, scale, stream()),
+        "patch_bwd");
+}
+
+// returns per-row losses; writes dlogits (if given) and increments correct[0]
+torch::Tensor xent(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> dlogits, c10::optional<torch::Tensor> correct,
+                   double grad_scale) {
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits must be [B, C] row-major");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous(), "xent: labels must be contiguous int64");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  auto loss = torch::empty({B}, logits.options().dtype(torch::kFloat32));
+  check(pvr_xent(f32(logits, "logits"), logits.stride(0), labels.data_ptr<int64_t>(), (int)B, (int)C, loss.data_ptr<float>(),
+                 opt_ptr<float>(dlogits), opt_ptr<int>(correct), (float)grad_scale, stream()),
+        "xent");
+  return loss;
+}
+
+void grad_norm(torch::Tensor g, double max_norm, torch::Tensor workspace, torch::Tensor out) {
+  TORCH_CHECK(g.is_contiguous(), "grad_norm: flat grad must be contiguous");
+  TORCH_CHECK(workspace.numel() >= pvr_norm_partial_blocks(), "grad_norm: workspace too small");
+  check(pvr_grad_norm(f32(g, "g"), g.numel(), (float)max_norm, f32_mut(workspace, "ws"), f32_mut(out, "out"), stream()), "grad_norm");
+}
+
+void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow, torch::Tensor seg_start,
+          torch::Tensor seg_group, torch::Tensor groups, c10::optional<torch::Tensor> clip, bool skip_nonfinite) {
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam: size mismatch");
+  TORCH_CHECK(groups.scalar_type() == torch::kFloat32 && groups.size(-1) == 8, "adam: groups must be float32 [G, 8]");
+  TORCH_CHECK(seg_start.scalar_type() == torch::kInt64 && seg_group.scalar_type() == torch::kInt32, "adam: segment table dtypes");
+  uint16_t* sh = nullptr;
+  if (shadow.has_value() && shadow->defined()) sh = const_cast<uint16_t*>(bf(*shadow, "shadow"));
+  check(pvr_adam(f32_mut(p, "p"), f32(g, "g"), f32_mut(m, "m"), f32_mut(v, "v"), sh, p.numel(), seg_start.data_ptr<int64_t>(),
+                 seg_group.data_ptr<int>(), (int)seg_start.numel(), reinterpret_cast<const pvr::AdamGroup*>(groups.data_ptr<float>()),
+                 opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0, stream()),
+        "adam");
+}
+
+void scale_by_clip(torch::Tensor g, torch::Tensor clip) {
+  check(pvr_scale_by_clip(f32_mut(g, "g"), g.numel(), f32(clip, "clip"), stream()), "scale_by_clip");
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int64_t H, double scale) {
+  const int64_t D = qkv.size(1) / 3;
+  auto out = torch::empty({B * N, D}, qkv.options());
+  auto lse = torch::empty({B * H, N}, qkv.options().dtype(torch::kFloat32));
+  TORCH_CHECK(qkv.size(0) == B * N, "attn_fwd: qkv rows != B*N");
+  check(pvr_attn_fwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf_mut(out, "out"), D, f32_mut(lse, "lse"), (int)B, (int)N, (int)H, (int)D,
+                     (float)scale, stream()),
+        "attn_fwd");
+  return {out, lse};
+}
+
+torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
+                       double scale) {
+  const int64_t D = qkv.size(1) / 3;
+  auto dqkv = torch::empty_like(qkv);
+  auto delta = torch::empty_like(lse);
+  torch::Tensor dq_acc;
+  if (N > 256) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
+  check(pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"), ld_of(dout, "dout"),
+                     f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"), ld_of(dqkv, "dqkv"),
+                     dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D, (float)scale, stream()),
+        "attn_bwd");
+  return dqkv;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
+  m.def("gemm", &gemm);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("colsum", &colsum);
+  m.def("im2col", &im2col);
+  m.def("cls_rows", &cls_rows);
+  m.def("patch_bwd", &patch_bwd);
+  m.def("xent", &xent);
+  m.def("grad_norm", &grad_norm);
+  m.def("norm_partial_blocks", []() { return pvr_norm_partial_blocks(); });
+  m.def("adam", &adam);
+  m.def("scale_by_clip", &scale_by_clip);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("arch", []() { return std::string("gfx950"); });
+}

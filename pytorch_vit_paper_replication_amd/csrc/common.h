@@ -1,0 +1,112 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels of this package.
+//
+// Everything here is written for 64-lane wavefronts, MFMA bf16 16x16x32 fragments and
+// LDS-DMA (buffer_load ... lds) staging. No CUDA/HIP dual paths: this is CDNA4 code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PVR_DEV __device__ __forceinline__
+
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+namespace pvr {
+
+PVR_DEV float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+// Round-to-nearest-even f32->bf16 (NaN stays NaN through the plain cast path).
+PVR_DEV uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+PVR_DEV uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// 16x16x32 bf16 MFMA: D = A(16x32) * B(32x16) + C.
+// lane l holds A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15], D[row 4(l>>4)+r][col l&15].
+PVR_DEV v4f mfma16(v8s a, v8s b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, a),
+                                                  __builtin_bit_cast(v8bf, b), c, 0, 0, 0);
+}
+
+// Buffer resource: hardware range check returns 0 for every byte past `bytes`.
+PVR_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// LDS-DMA: 16 bytes per lane, LDS destination = lds_base (wave-uniform) + lane*16.
+PVR_DEV void dma16(__amdgpu_buffer_rsrc_t r, lds_void* lds_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_base, 16, voff, 0, 0, 0);
+}
+
+PVR_DEV lds_void* to_lds(void* p) { return (lds_void*)p; }
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, cols 4p..4p+3 of a 4x16
+// block; lane i receives column i of the 4 rows (row q in element q).
+PVR_DEV v4s ds_read_tr(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)lds_ptr);
+}
+
+PVR_DEV v8s ds_read_b128(const void* lds_ptr) {
+  return *(const __attribute__((address_space(3))) v8s*)lds_ptr;
+}
+
+PVR_DEV v8s cat44(v4s a, v4s b) {
+  v8s r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// Counter-based dropout RNG: murmur3-style finaliser over (seed, element index).
+// Shared by every kernel that recomputes a mask in backward, so forward and backward agree bit
+// for bit without storing the mask.
+PVR_DEV uint32_t rng_hash(uint64_t seed, uint64_t idx) {
+  uint32_t h = (uint32_t)idx * 0x9E3779B1u ^ (uint32_t)seed;
+  h ^= (uint32_t)(idx >> 32) * 0x7FEB352Du;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+// keep iff (hash & 0xFFFF) >= threshold, threshold = round(p * 65536).
+PVR_DEV bool rng_keep(uint64_t seed, uint64_t idx, uint32_t thr16) {
+  return (rng_hash(seed, idx) & 0xFFFFu) >= thr16;
+}
+
+PVR_DEV float gelu_erf(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
+PVR_DEV float gelu_erf_grad(float u) {
+  const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * u * u);
+  return cdf + u * pdf;
+}
+
+PVR_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+PVR_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap: blocks dealt round-robin over 8 XCDs (b, b+8 share one) are given
+// contiguous logical tile ranges so neighbouring tiles share the XCD's L2.
+PVR_DEV int xcd_remap(int bid, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+}  // namespace pvr

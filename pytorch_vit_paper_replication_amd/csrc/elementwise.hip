@@ -1,0 +1,188 @@
+// Memory-bound helper kernels (16-B vector accesses throughout, SURVEY.md K1-K4, K11 bias-grad):
+//   * flat fp32 -> bf16 shadow cast of the parameter store
+//   * bias-gradient column sums, optionally fused with the dropout-mask backward
+//   * patch embedding: im2col gather (fp32 image -> bf16 patch rows), CLS rows, and the backward
+//     reduction of the embedding-dropout / position-embedding / CLS gradients.
+#include "common.h"
+
+namespace pvr {
+namespace {
+
+__global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restrict__ in, uint16_t* __restrict__ out, int64_t n) {
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = ((const float4*)in)[i];
+    uint2 o;
+    o.x = pack2bf(v.x, v.y);
+    o.y = pack2bf(v.z, v.w);
+    ((uint2*)out)[i] = o;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = n4 * 4 + threadIdx.x;
+    out[i] = f2bf(in[i]);
+  }
+}
+
+// dY [rows][N] (row stride ld) -> db[N] += column sums of (mask * dY); if dz != null also writes
+// the masked gradient dz (= dropout backward) with row stride ld_dz.
+__global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict__ dy, int64_t ld, int rows, int N,
+                                                      float* __restrict__ db, uint16_t* __restrict__ dz, int64_t ld_dz,
+                                                      const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale) {
+  __shared__ float red[4][64 * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;  // 8-column chunk
+  const bool act = c * 8 < N;
+  const uint64_t seed = thr ? (*seed_ptr + seed_off) : 0ull;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (act) {
+    for (int r = blockIdx.y * 4 + wave; r < rows; r += gridDim.y * 4) {
+      const uint4 q = *(const uint4*)(dy + (int64_t)r * ld + c * 8);
+      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = bf2f(u[j] & 0xFFFF);
+        v[2 * j + 1] = bf2f(u[j] >> 16);
+      }
+      if (thr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = rng_keep(seed, (uint64_t)r * N + c * 8 + j, thr) ? v[j] * scale : 0.f;
+      }
+      if (dz) {
+        uint4 o;
+        o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+        o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+        *(uint4*)(dz + (int64_t)r * ld_dz + c * 8) = o;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+    const int col = blockIdx.x * 64 * 8 + i;
+    if (col < N && db) atomicAdd(db + col, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  }
+}
+
+// img [B][C][H][W] fp32 -> patches [B*np][Kp] bf16, k = (c*P + ph)*P + pw, zero padded to Kp.
+__global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ img, uint16_t* __restrict__ out,
+                                                      int B, int C, int H, int W, int P, int Kp) {
+  const int gw = W / P, np = (H / P) * gw;
+  const int64_t total = (int64_t)B * np * Kp;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i % Kp);
+    const int64_t rowi = i / Kp;
+    const int pidx = (int)(rowi % np);
+    const int b = (int)(rowi / np);
+    float v = 0.f;
+    if (k < C * P * P) {
+      const int c = k / (P * P), rem = k % (P * P), ph = rem / P, pw = rem % P;
+      const int y = (pidx / gw) * P + ph, x = (pidx % gw) * P + pw;
+      v = img[(((int64_t)b * C + c) * H + y) * W + x];
+    }
+    out[i] = f2bf(v);
+  }
+}
+
+// out[b][0][:] = dropout(cls + pos[0])   (row b*(np+1) of the token tensor)
+__global__ void __launch_bounds__(256) cls_rows_kernel(const float* __restrict__ cls, const float* __restrict__ pos,
+                                                        uint16_t* __restrict__ out, int B, int D, int64_t row_stride,
+                                                        const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
+                                                        int64_t ncols_total) {
+  const uint64_t seed = thr ? (*seed_ptr + seed_off) : 0ull;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < B * D; i += gridDim.x * 256) {
+    const int b = i / D, d = i % D;
+    float v = cls[d] + pos[d];
+    // dropout index uses the logical [B*(np+1), D] element index (row b*(np+1))
+    if (thr) v = rng_keep(seed, (uint64_t)(b * (row_stride / D)) * D + d, thr) ? v * scale : 0.f;
+    out[(int64_t)b * row_stride + d] = f2bf(v);
+  }
+}
+
+// Backward of  E = dropout(concat(cls, conv) + pos):  dE [B][np+1][D] bf16 ->
+//   dpre = dE * mask;  dpos[n][d] += sum_b dpre;  dcls[d] += sum_b dpre[b][0][d];
+//   dconv[b*np + n-1][d] = dpre (bf16, n >= 1);  dbias[d] += sum_{b, n>=1} dpre.
+// One thread per (n, d) column, looping over the batch: deterministic, no atomics on dpos/dcls.
+__global__ void __launch_bounds__(256) patch_bwd_kernel(const uint16_t* __restrict__ dE, int B, int ntok, int D,
+                                                         float* __restrict__ dpos, float* __restrict__ dcls,
+                                                         uint16_t* __restrict__ dconv, float* __restrict__ dbias,
+                                                         const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale) {
+  const uint64_t seed = thr ? (*seed_ptr + seed_off) : 0ull;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= ntok * D) return;
+  const int n = i / D, d = i % D;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const int64_t row = (int64_t)b * ntok + n;
+    float v = bf2f(dE[row * D + d]);
+    if (thr) v = rng_keep(seed, (uint64_t)row * D + d, thr) ? v * scale : 0.f;
+    s += v;
+    if (n > 0 && dconv) dconv[((int64_t)b * (ntok - 1) + n - 1) * D + d] = f2bf(v);
+  }
+  if (dpos) dpos[i] += s;
+  if (n == 0) {
+    if (dcls) dcls[d] += s;
+  } else if (dbias) {
+    atomicAdd(dbias + d, s);
+  }
+}
+
+}  // namespace
+}  // namespace pvr
+
+extern "C" hipError_t pvr_cast_f32_bf16(const float* in, uint16_t* out, int64_t n, hipStream_t s) {
+  using namespace pvr;
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, out, n);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_colsum(const uint16_t* dy, int64_t ld, int rows, int N, float* db, uint16_t* dz, int64_t ld_dz,
+                                 const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale, hipStream_t s) {
+  using namespace pvr;
+  if (rows <= 0) return hipSuccess;
+  if (N % 8 != 0) return hipErrorInvalidValue;
+  const int gx = (N / 8 + 63) / 64;
+  int gy = (rows + 63) / 64;
+  if (gy > 256) gy = 256;
+  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, s, dy, ld, rows, N, db, dz, ld_dz, seed_ptr, seed_off, thr, scale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_im2col(const float* img, uint16_t* out, int B, int C, int H, int W, int P, int Kp, hipStream_t s) {
+  using namespace pvr;
+  const int64_t total = (int64_t)B * (H / P) * (W / P) * Kp;
+  if (total <= 0) return hipSuccess;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)blocks), dim3(256), 0, s, img, out, B, C, H, W, P, Kp);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_cls_rows(const float* cls, const float* pos, uint16_t* out, int B, int D, int64_t row_stride,
+                                   const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale, hipStream_t s) {
+  using namespace pvr;
+  if (B * D <= 0) return hipSuccess;
+  int blocks = (B * D + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(cls_rows_kernel, dim3(blocks), dim3(256), 0, s, cls, pos, out, B, D, row_stride, seed_ptr, seed_off, thr, scale, (int64_t)0);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_patch_bwd(const uint16_t* dE, int B, int ntok, int D, float* dpos, float* dcls, uint16_t* dconv,
+                                    float* dbias, const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
+                                    hipStream_t s) {
+  using namespace pvr;
+  const int n = ntok * D;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(patch_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dE, B, ntok, D, dpos, dcls, dconv, dbias,
+                     seed_ptr, seed_off, thr, scale);
+  return hipGetLastError();
+}

@@ -1,0 +1,210 @@
+// LayerNorm forward/backward for the pre-LN ViT blocks (reference models/vit.py:83, :115, :216;
+// SURVEY.md K5). One wave per token row, bf16 I/O with 16-B vector accesses, fp32 statistics.
+// The backward fuses the residual-branch gradient add (dx = dres + LN'(dy)) and reduces
+// d(gamma)/d(beta) per block in LDS before one f32 atomic per column per block.
+#include "common.h"
+
+namespace pvr {
+namespace {
+
+template <int MAXCH>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const uint16_t* __restrict__ x, int64_t x_stride,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      uint16_t* __restrict__ y, int64_t y_stride,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = D >> 3;
+  const uint16_t* xr = x + (int64_t)row * x_stride;
+  float v[MAXCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      const uint4 q = *(const uint4*)(xr + c * 8);
+      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[i][2 * j] = bf2f(u[j] & 0xFFFF);
+        v[i][2 * j + 1] = bf2f(u[j] >> 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+  uint16_t* yr = y + (int64_t)row * y_stride;
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
+      const float4 b0 = *(const float4*)(b + c * 8), b1 = *(const float4*)(b + c * 8 + 4);
+      const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * ww[j] + bb[j];
+      uint4 q;
+      q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
+      q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
+      *(uint4*)(yr + c * 8) = q;
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+PVR_DEV void load8(const uint16_t* p, float* o) {
+  const uint4 q = *(const uint4*)p;
+  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[2 * j] = bf2f(u[j] & 0xFFFF);
+    o[2 * j + 1] = bf2f(u[j] >> 16);
+  }
+}
+
+// Grid-stride over rows: each wave keeps its lanes' dgamma/dbeta partials in registers.
+template <int MAXCH>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict__ dy, int64_t dy_stride,
+                                                      const uint16_t* __restrict__ x, int64_t x_stride,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      const float* __restrict__ w,
+                                                      const uint16_t* __restrict__ dres, int64_t dres_stride,
+                                                      uint16_t* __restrict__ dx, int64_t dx_stride,
+                                                      float* __restrict__ dw, float* __restrict__ db, int rows, int D) {
+  __shared__ float red[4][2][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = D >> 3;
+  float gw[MAXCH][8], gb[MAXCH][8];
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gw[i][j] = gb[i][j] = 0.f;
+
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXCH][8], g[MAXCH][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float xv[8], dv[8];
+        load8(x + (int64_t)row * x_stride + c * 8, xv);
+        load8(dy + (int64_t)row * dy_stride + c * 8, dv);
+        const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
+        const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] = (xv[j] - mu) * rs;
+          g[i][j] = dv[j] * ww[j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+          gw[i][j] += dv[j] * xh[i][j];
+          gb[i][j] += dv[j];
+        }
+      }
+    }
+    const float c1 = wave_sum(s1) / D, c2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (g[i][j] - c1 - xh[i][j] * c2) * rs;
+        if (dres) {
+          float r[8];
+          load8(dres + (int64_t)row * dres_stride + c * 8, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        uint4 q;
+        q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
+        q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
+        *(uint4*)(dx + (int64_t)row * dx_stride + c * 8) = q;
+      }
+    }
+  }
+  // block reduction of dgamma/dbeta partials, then one atomic per column per block
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wave][0][c * 8 + j] = gw[i][j];
+        red[wave][1][c * 8 + j] = gb[i][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += 256) {
+    const float a = red[0][0][col] + red[1][0][col] + red[2][0][col] + red[3][0][col];
+    const float bsum = red[0][1][col] + red[1][1][col] + red[2][1][col] + red[3][1][col];
+    if (dw) atomicAdd(dw + col, a);
+    if (db) atomicAdd(db + col, bsum);
+  }
+}
+
+}  // namespace
+}  // namespace pvr
+
+extern "C" hipError_t pvr_layernorm_fwd(const uint16_t* x, int64_t x_stride, const float* w, const float* b,
+                                        uint16_t* y, int64_t y_stride, float* mean, float* rstd, int rows, int D,
+                                        float eps, hipStream_t s) {
+  using namespace pvr;
+  if (rows <= 0) return hipSuccess;
+  if (D % 8 != 0 || D > 2048) return hipErrorInvalidValue;
+  const dim3 grid((rows + 3) / 4), block(256);
+  const int maxch = (D / 8 + 63) / 64;
+  switch (maxch) {
+    case 1: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
+    case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
+    default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, const uint16_t* x, int64_t x_stride,
+                                        const float* mean, const float* rstd, const float* w, const uint16_t* dres,
+                                        int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
+                                        int rows, int D, hipStream_t s) {
+  using namespace pvr;
+  if (rows <= 0) return hipSuccess;
+  if (D % 8 != 0 || D > 1280) return hipErrorInvalidValue;
+  int nblk = (rows + 3) / 4;
+  if (nblk > 1024) nblk = 1024;
+  const dim3 grid(nblk), block(256);
+  const int maxch = (D / 8 + 63) / 64;
+  switch (maxch) {
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, rows, D); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, rows, D); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, rows, D); break;
+  }
+  return hipGetLastError();
+}

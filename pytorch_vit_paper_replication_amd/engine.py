@@ -1,0 +1,146 @@
+"""Training / evaluation engine with the reference API (GM/engine.py:9-211).
+
+``train(model, train_dataloader, test_dataloader, optimizer, loss_fn, lr_scheduler, epochs, device)``
+returns ``{"train_loss": [...], "train_acc": [...], "test_loss": [...], "test_acc": [...]}`` and prints
+``Epoch: n | train_loss: .. | train_acc: .. | test_loss: .. | test_acc: ..`` per epoch, exactly like
+the reference. Preserved semantics:
+  * the scheduler steps once per batch, gradients are clipped to global norm 1.0 before the step;
+  * metrics are the mean over batches of per-batch means (a partial last batch weighs like a full one);
+  * the train accuracy uses argmax(softmax(logits)) (== argmax(logits)), test uses argmax(logits).
+
+MI355X-oriented differences (no behaviour change):
+  * per-batch loss/accuracy accumulate on the device; the host syncs once per epoch instead of
+    twice per batch (the reference's ``.item()`` calls, GM/engine.py:54,74,121,125);
+  * with :class:`~..optim.FusedAdam` the clip runs inside the optimizer (device-side coefficient,
+    no sync) and ``nn.CrossEntropyLoss()`` is executed by the fused softmax-xent kernel;
+  * under ``torch.distributed`` metrics are all-reduced across ranks and only rank 0 prints.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+from torch import nn
+
+try:
+    from tqdm.auto import tqdm
+except Exception:  # pragma: no cover
+    def tqdm(x, **_):
+        return x
+
+from .ops.fused_vit import cross_entropy
+
+
+def _is_dist() -> bool:
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
+def _rank0() -> bool:
+    return not _is_dist() or torch.distributed.get_rank() == 0
+
+
+def _fused_loss(loss_fn):
+    """Use the fused kernel for a default nn.CrossEntropyLoss (same math and reduction)."""
+    if isinstance(loss_fn, nn.CrossEntropyLoss) and loss_fn.weight is None and loss_fn.reduction == "mean" \
+            and loss_fn.label_smoothing == 0.0 and loss_fn.ignore_index == -100:
+        return cross_entropy
+    return loss_fn
+
+
+def _clip_and_step(model, optimizer, max_norm: Optional[float]):
+    from .optim.adam import FusedAdam
+
+    if isinstance(optimizer, FusedAdam):
+        optimizer.step(clip_norm=max_norm)
+        return
+    if max_norm is not None:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+    optimizer.step()
+
+
+def _reduce_means(sums: torch.Tensor, count: int, device) -> Tuple[float, ...]:
+    """sums: per-metric sums of per-batch means; returns global mean-of-batch-means."""
+    vals = torch.cat([sums.double().reshape(-1), torch.tensor([float(count)], dtype=torch.float64, device=sums.device)])
+    if _is_dist():
+        if vals.device.type == "cpu" and torch.distributed.get_backend() == "nccl":
+            vals = vals.to(device)
+        torch.distributed.all_reduce(vals)
+    vals = vals.cpu()
+    n = max(vals[-1].item(), 1.0)
+    return tuple((vals[:-1] / n).tolist())
+
+
+def train_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, optimizer: torch.optim.Optimizer,
+               lr_scheduler, device, *, max_grad_norm: Optional[float] = 1.0) -> Tuple[float, float]:
+    """One training epoch (reference GM/engine.py:9-79). Returns (train_loss, train_acc)."""
+    model.train()
+    lf = _fused_loss(loss_fn)
+    sums = torch.zeros(2, dtype=torch.float32, device=device)
+    nb = 0
+    for X, y in dataloader:
+        X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
+        y_pred = model(X)
+        loss = lf(y_pred, y)
+        optimizer.zero_grad()
+        loss.backward()
+        _clip_and_step(model, optimizer, max_grad_norm)
+        lr_scheduler.step()
+        with torch.no_grad():
+            acc = (y_pred.argmax(dim=1) == y).sum().float() / y_pred.shape[0]
+            sums += torch.stack([loss.detach().float(), acc])
+        nb += 1
+    loss_m, acc_m = _reduce_means(sums, nb, device)
+    return loss_m, acc_m
+
+
+def test_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, device) -> Tuple[float, float]:
+    """One evaluation epoch (reference GM/engine.py:81-130). Returns (test_loss, test_acc)."""
+    model.eval()
+    lf = _fused_loss(loss_fn)
+    sums = torch.zeros(2, dtype=torch.float32, device=device)
+    nb = 0
+    with torch.inference_mode():
+        for X, y in dataloader:
+            X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
+            logits = model(X)
+            loss = lf(logits, y)
+            acc = (logits.argmax(dim=1) == y).sum().float() / logits.shape[0]
+            sums += torch.stack([loss.float(), acc])
+            nb += 1
+    loss_m, acc_m = _reduce_means(sums, nb, device)
+    return loss_m, acc_m
+
+
+def train(model: torch.nn.Module, train_dataloader, test_dataloader, optimizer: torch.optim.Optimizer,
+          loss_fn: torch.nn.Module, lr_scheduler, epochs: int, device, *, max_grad_norm: Optional[float] = 1.0,
+          checkpoint_dir: Optional[str] = None, metrics_path: Optional[str] = None) -> Dict[str, List]:
+    """Train and test for ``epochs`` epochs (reference GM/engine.py:132-211)."""
+    results = {"train_loss": [], "train_acc": [], "test_loss": [], "test_acc": []}
+    model.to(device)
+    it = tqdm(range(epochs)) if _rank0() else range(epochs)
+    for epoch in it:
+        train_loss, train_acc = train_step(model=model, dataloader=train_dataloader, loss_fn=loss_fn,
+                                           optimizer=optimizer, lr_scheduler=lr_scheduler, device=device,
+                                           max_grad_norm=max_grad_norm)
+        test_loss, test_acc = test_step(model=model, dataloader=test_dataloader, loss_fn=loss_fn, device=device)
+        if _rank0():
+            print(f"Epoch: {epoch + 1} | "
+                  f"train_loss: {train_loss:.4f} | "
+                  f"train_acc: {train_acc:.4f} | "
+                  f"test_loss: {test_loss:.4f} | "
+                  f"test_acc: {test_acc:.4f}")
+        results["train_loss"].append(train_loss)
+        results["train_acc"].append(train_acc)
+        results["test_loss"].append(test_loss)
+        results["test_acc"].append(test_acc)
+        if metrics_path and _rank0():
+            from .utils.metrics import append_jsonl
+
+            append_jsonl(metrics_path, {"epoch": epoch + 1, "train_loss": train_loss, "train_acc": train_acc,
+                                        "test_loss": test_loss, "test_acc": test_acc})
+        if checkpoint_dir:
+            from .utils.checkpoint import save_checkpoint
+
+            save_checkpoint(checkpoint_dir, model=model, optimizer=optimizer, lr_scheduler=lr_scheduler,
+                            epoch=epoch + 1, results=results)
+    return results

@@ -1,0 +1,270 @@
+"""Vision Transformer (Dosovitskiy et al., 2020) with the reference's public surface.
+
+API parity with the reference ``models/vit.py``:
+  * ``ViT(image_size=224, patch_size=16, num_transformer_layer=12, num_heads=12, embedding_dim=768,
+    mlp_size=3072, attn_dropout=0, mlp_dropout=0.1, embedding_dropout=0.1, num_classes=1000)``
+    (reference models/vit.py:173-183) and ``forward(x [B,3,H,W]) -> logits [B, num_classes]``;
+  * sub-blocks ``PatchEmbedding`` (:5-67), ``MultiHeadSelfAttentionBlock`` (:69-98),
+    ``MLPBlock`` (:100-131), ``TransformerEncoderBlock`` (:133-169) with the same constructor
+    signatures and submodule names, hence the same 152-key ``state_dict``;
+  * the same initialisation, in the same RNG order (CLS/pos ``torch.rand``, Conv/Linear kaiming,
+    in_proj xavier, zero MHA biases), so a seeded model is bit-identical to the reference's.
+
+Execution: on CPU (or with ``PVR_DISABLE_FUSED=1``) every module runs plain PyTorch fp32 math
+equivalent to the reference. On an MI355X the top-level ``ViT.forward`` runs the fused path: flat
+parameter store with a bf16 shadow, hand-written gfx950 kernels for patch embedding, LayerNorm,
+MFMA GEMMs with fused bias/GELU/dropout/residual epilogues, flash-style attention and a fused
+classifier head (``ops.fused_vit``), with hand-written backward passes.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .. import _ext
+
+
+class PatchEmbedding(nn.Module):
+    """Image -> [B, N+1, D] patch + CLS + position embeddings (reference models/vit.py:5-67)."""
+
+    def __init__(self, image_size: int, color_channels: int = 3, patch_size: int = 16,
+                 embedding_dropout: float = 0.1, embedding_dim: int = 768):
+        super().__init__()
+        self.patch_size = patch_size
+        assert image_size % self.patch_size == 0, (
+            f"Input image size must be divisible by patch size, image size: {image_size}, patch_size: {patch_size}")
+        self.number_of_patches = int((image_size ** 2) / (patch_size ** 2))
+        self.patch_and_flatten = nn.Sequential(
+            nn.Conv2d(in_channels=color_channels, out_channels=embedding_dim, kernel_size=patch_size, stride=patch_size),
+            nn.Flatten(start_dim=2, end_dim=3),
+        )
+        self.class_token = nn.Parameter(torch.rand(1, 1, embedding_dim), requires_grad=True)
+        self.position_embedding = nn.Parameter(torch.rand(1, self.number_of_patches + 1, embedding_dim),
+                                               requires_grad=True)
+        self.dropout = nn.Dropout(p=embedding_dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        b = x.shape[0]
+        cls = self.class_token.expand(b, -1, -1)
+        x = self.patch_and_flatten(x).permute(0, 2, 1)
+        x = torch.cat((cls, x), dim=1) + self.position_embedding
+        return self.dropout(x)
+
+
+class SelfAttention(nn.Module):
+    """Multi-head attention with ``nn.MultiheadAttention``'s parameter layout and init.
+
+    Parameters ``in_proj_weight [3D, D]`` (rows q;k;v), ``in_proj_bias [3D]``, ``out_proj.{weight,bias}``,
+    so checkpoints interchange with the reference's ``nn.MultiheadAttention(batch_first=True)``.
+    """
+
+    def __init__(self, embed_dim: int, num_heads: int, dropout: float = 0.0, batch_first: bool = True):
+        super().__init__()
+        assert embed_dim % num_heads == 0, "embed_dim must be divisible by num_heads"
+        self.embed_dim = embed_dim
+        self.num_heads = num_heads
+        self.head_dim = embed_dim // num_heads
+        self.dropout = dropout
+        self.batch_first = batch_first
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
+        self.in_proj_bias = nn.Parameter(torch.empty(3 * embed_dim))
+        # created (and default-initialised) before in_proj, exactly like nn.MultiheadAttention
+        self.out_proj = nn.Linear(embed_dim, embed_dim, bias=True)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.constant_(self.in_proj_bias, 0.0)
+        nn.init.constant_(self.out_proj.bias, 0.0)
+
+    def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, need_weights: bool = False,
+                attn_mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        if not self.batch_first:
+            query, key, value = (t.transpose(0, 1) for t in (query, key, value))
+        B, Nq, D = query.shape
+        Nk = key.shape[1]
+        H, dh = self.num_heads, self.head_dim
+        w_q, w_k, w_v = self.in_proj_weight.chunk(3)
+        b_q, b_k, b_v = self.in_proj_bias.chunk(3)
+        if query is key and key is value:
+            q, k, v = F.linear(query, self.in_proj_weight, self.in_proj_bias).chunk(3, dim=-1)
+        else:
+            q, k, v = F.linear(query, w_q, b_q), F.linear(key, w_k, b_k), F.linear(value, w_v, b_v)
+        q = q.view(B, Nq, H, dh).transpose(1, 2)
+        k = k.view(B, Nk, H, dh).transpose(1, 2)
+        v = v.view(B, Nk, H, dh).transpose(1, 2)
+        p = self.dropout if self.training else 0.0
+        weights = None
+        if need_weights:
+            s = (q @ k.transpose(-2, -1)) / math.sqrt(dh)
+            if attn_mask is not None:
+                s = s + attn_mask
+            a = torch.softmax(s, dim=-1)
+            weights = a.mean(dim=1)
+            a = F.dropout(a, p=p, training=p > 0)
+            o = a @ v
+        else:
+            o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=p)
+        o = o.transpose(1, 2).reshape(B, Nq, D)
+        o = self.out_proj(o)
+        if not self.batch_first:
+            o = o.transpose(0, 1)
+        return o, weights
+
+
+class MultiHeadSelfAttentionBlock(nn.Module):
+    """LN -> MSA (reference models/vit.py:69-98); the residual is added by the caller."""
+
+    def __init__(self, embedding_dim: int = 768, num_heads: int = 12, attn_dropout: float = 0):
+        super().__init__()
+        self.layer_norm = nn.LayerNorm(normalized_shape=embedding_dim)
+        self.multi_head_attention = SelfAttention(embed_dim=embedding_dim, num_heads=num_heads,
+                                                  dropout=attn_dropout, batch_first=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        normalized_x = self.layer_norm(x)
+        attn_output, _ = self.multi_head_attention(query=normalized_x, key=normalized_x, value=normalized_x,
+                                                   need_weights=False)
+        return attn_output
+
+
+class MLPBlock(nn.Module):
+    """LN -> Linear -> GELU -> Dropout -> Linear -> Dropout (reference models/vit.py:100-131)."""
+
+    def __init__(self, embedding_dim: int = 768, mlp_size: int = 3072, dropout: float = 0.1):
+        super().__init__()
+        self.layer_norm = nn.LayerNorm(normalized_shape=embedding_dim)
+        self.mlp = nn.Sequential(
+            nn.Linear(in_features=embedding_dim, out_features=mlp_size),
+            nn.GELU(),
+            nn.Dropout(p=dropout),
+            nn.Linear(in_features=mlp_size, out_features=embedding_dim),
+            nn.Dropout(p=dropout),
+        )
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.mlp(self.layer_norm(x))
+
+
+class TransformerEncoderBlock(nn.Module):
+    """x = MSA(x) + x ; x = MLP(x) + x (reference models/vit.py:133-169)."""
+
+    def __init__(self, embedding_dim: int = 768, num_heads: int = 12, attn_dropout: float = 0,
+                 mlp_size: int = 3072, mlp_dropout: float = 0.1):
+        super().__init__()
+        self.msa_block = MultiHeadSelfAttentionBlock(embedding_dim=embedding_dim, num_heads=num_heads,
+                                                     attn_dropout=attn_dropout)
+        self.mlp_block = MLPBlock(embedding_dim=embedding_dim, mlp_size=mlp_size, dropout=mlp_dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.msa_block(x) + x
+        x = self.mlp_block(x) + x
+        return x
+
+    # fused-path helpers ---------------------------------------------------------------
+    def fused_params(self):
+        m, p = self.msa_block, self.mlp_block
+        a = m.multi_head_attention
+        return (m.layer_norm.weight, m.layer_norm.bias, a.in_proj_weight, a.in_proj_bias,
+                a.out_proj.weight, a.out_proj.bias, p.layer_norm.weight, p.layer_norm.bias,
+                p.mlp[0].weight, p.mlp[0].bias, p.mlp[3].weight, p.mlp[3].bias)
+
+
+class ViT(nn.Module):
+    """ViT-Base/16 by default (reference models/vit.py:172-236)."""
+
+    def __init__(self, image_size: int = 224, patch_size: int = 16, num_transformer_layer: int = 12,
+                 num_heads: int = 12, embedding_dim: int = 768, mlp_size: int = 3072, attn_dropout: float = 0,
+                 mlp_dropout: float = 0.1, embedding_dropout: float = 0.1, num_classes: int = 1000):
+        super().__init__()
+        self.patch_embedding_block = PatchEmbedding(image_size=image_size, patch_size=patch_size,
+                                                    embedding_dim=embedding_dim, embedding_dropout=embedding_dropout)
+        self.transformer_encoder = nn.Sequential(*[
+            TransformerEncoderBlock(embedding_dim=embedding_dim, num_heads=num_heads, attn_dropout=attn_dropout,
+                                    mlp_size=mlp_size, mlp_dropout=mlp_dropout)
+            for _ in range(num_transformer_layer)])
+        self.layer_norm = nn.LayerNorm(normalized_shape=embedding_dim)
+        self.classifier = nn.Sequential(nn.Linear(in_features=embedding_dim, out_features=num_classes))
+        self.config = dict(image_size=image_size, patch_size=patch_size, num_transformer_layer=num_transformer_layer,
+                           num_heads=num_heads, embedding_dim=embedding_dim, mlp_size=mlp_size,
+                           attn_dropout=attn_dropout, mlp_dropout=mlp_dropout, embedding_dropout=embedding_dropout,
+                           num_classes=num_classes)
+
+    # ------------------------------------------------------------------ reference path
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.patch_embedding_block(x)
+        x = self.transformer_encoder(x)
+        return self.layer_norm(x)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _ext.use_fused(x) and self._fused_supported(x):
+            return self._forward_fused(x)
+        x = self.forward_features(x)
+        return self.classifier(x[:, 0])
+
+    # ------------------------------------------------------------------ fused path
+    def _fused_supported(self, x: torch.Tensor) -> bool:
+        c = self.config
+        D, H = c["embedding_dim"], c["num_heads"]
+        if x.dim() != 4 or x.shape[1] != 3 or D % H != 0 or D // H != 64 or D % 64 != 0:
+            return False
+        if c["mlp_size"] % 64 != 0:
+            return False
+        if self.training and c["attn_dropout"] > 0:
+            return False  # attention-probability dropout only on the PyTorch path
+        P = c["patch_size"]
+        return x.shape[2] == x.shape[3] == c["image_size"] and x.shape[2] % P == 0
+
+    def _dropout_seed(self, device) -> torch.Tensor:
+        rng = getattr(self, "_pvr_rng", None)
+        if rng is None or rng.device != device:
+            with torch.inference_mode(False):
+                base = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+                rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
+                rng = torch.tensor([base * 2654435761 + rank * 40503], dtype=torch.int64, device=device)
+            object.__setattr__(self, "_pvr_rng", rng)
+        seed = rng.clone()
+        rng.add_(1)
+        return seed
+
+    def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops.fused_vit import EncoderBlockFn, HeadFn, PatchEmbedFn, site_drop
+        from ..runtime.param_store import get_store
+
+        c = self.config
+        dev = x.device
+        for p in self.parameters():
+            if p.device != dev:
+                raise RuntimeError(f"input is on {dev} but model parameters are on {p.device}")
+        store = get_store(self, dev)
+        store.refresh_shadow()
+        training = self.training
+        grad = torch.is_grad_enabled()
+        if grad:
+            store.prepare_grads()
+        need_seed = training and (c["mlp_dropout"] > 0 or c["embedding_dropout"] > 0)
+        seed = self._dropout_seed(dev) if need_seed else None
+        pe = self.patch_embedding_block
+        conv = pe.patch_and_flatten[0]
+        tokens = PatchEmbedFn.apply(x, c["patch_size"], store, seed, pe.dropout.p, training,
+                                    conv.weight, conv.bias, pe.class_token, pe.position_embedding)
+        B = x.shape[0]
+        N = pe.number_of_patches + 1
+        for i, blk in enumerate(self.transformer_encoder):
+            ln1 = blk.msa_block.layer_norm
+            ln2 = blk.mlp_block.layer_norm
+            p1 = blk.mlp_block.mlp[2].p
+            p2 = blk.mlp_block.mlp[4].p
+            tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads, ln1.eps, ln2.eps,
+                                          store, site_drop(seed, 1 + 2 * i, p1, training),
+                                          site_drop(seed, 2 + 2 * i, p2, training), *blk.fused_params())
+        head = self.classifier[0]
+        return HeadFn.apply(tokens, B, N, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias,
+                            head.weight, head.bias)
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())

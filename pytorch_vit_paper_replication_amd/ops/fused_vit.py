@@ -1,0 +1,241 @@
+"""Fused GPU autograd Functions for the ViT hot path (bf16 activations, fp32 accumulation).
+
+Token tensors are 2-D ``[B*N, D]`` bf16 row-major (token-major), the layout every kernel reads and
+writes in place. Each Function writes its parameter gradients straight into the flat fp32
+gradient store (``runtime.param_store``) and returns ``None`` for them, then signals the store so
+the data-parallel bucketer can launch all-reduces while the rest of backward runs.
+
+Reference semantics (models/vit.py):
+  PatchEmbedding  :45-67   conv(P, stride P) -> flatten -> cat(CLS) -> +pos -> dropout
+  TransformerEncoderBlock :166-169  x = MSA(LN(x)) + x ;  x = MLP(LN(x)) + x
+  MLPBlock        :118-126 Linear -> GELU(erf) -> Dropout -> Linear -> Dropout
+  ViT head        :232-235 LayerNorm on all tokens, classifier on token 0 (here: LN of token 0 only,
+                           identical output since LayerNorm is per token)
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import _ext
+from . import gemm
+
+SITE_SHIFT = 32
+
+
+def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
+    if seed is None or not training or p <= 0.0:
+        return None
+    return (seed, site << SITE_SHIFT, float(p))
+
+
+class PatchEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, patch, store, seed, p_drop, training, conv_w, conv_b, cls, pos):
+        ext = _ext.ext()
+        img = img.float().contiguous()
+        B, C, H, W = img.shape
+        D = conv_w.shape[0]
+        n_p = (H // patch) * (W // patch)
+        ntok = n_p + 1
+        kc = C * patch * patch
+        kp = (kc + 63) // 64 * 64
+        patches = torch.empty(B * n_p, kp, dtype=torch.bfloat16, device=img.device)
+        ext.im2col(img, patches, patch, kp)
+        w16 = store.bf16(conv_w).reshape(D, kc)
+        if kp != kc:
+            w16 = F.pad(w16, (0, kp - kc))
+        tokens = torch.empty(B * ntok, D, dtype=torch.bfloat16, device=img.device)
+        drop = site_drop(seed, 0, p_drop, training)
+        gemm.linear_fwd(patches, w16, conv_b, addend=pos.reshape(ntok, D), addend_period=ntok,
+                        row_remap=(n_p, ntok, 1), drop=drop, out=tokens)
+        dseed, doff, dp = gemm._drop_args(drop)
+        ext.cls_rows(cls.reshape(D), pos.reshape(ntok, D)[0].contiguous(), tokens, B, D, ntok * D, dseed, doff, dp)
+        ctx.save_for_backward(patches)
+        ctx.meta = (store, drop, B, ntok, D, kc, kp, conv_w, conv_b, cls, pos)
+        return tokens
+
+    @staticmethod
+    def backward(ctx, dtokens):
+        ext = _ext.ext()
+        (patches,) = ctx.saved_tensors
+        store, drop, B, ntok, D, kc, kp, conv_w, conv_b, cls, pos = ctx.meta
+        dtokens = dtokens.contiguous()
+        gpos = store.grad_dest(pos)
+        gcls = store.grad_dest(cls)
+        gb = store.grad_dest(conv_b)
+        gw = store.grad_dest(conv_w)
+        dconv = torch.empty(B * (ntok - 1), D, dtype=torch.bfloat16, device=dtokens.device) if gw is not None else None
+        dseed, doff, dp = gemm._drop_args(drop)
+        ext.patch_bwd(dtokens, B, ntok, D, None if gpos is None else gpos.view(-1),
+                      None if gcls is None else gcls.view(-1), dconv, gb, dseed, doff, dp)
+        if gw is not None:
+            if kp == kc:
+                gemm.linear_wgrad(dconv, patches, gw.view(D, kc))
+            else:
+                tmp = torch.zeros(D, kp, dtype=torch.float32, device=dtokens.device)
+                gemm.linear_wgrad(dconv, patches, tmp)
+                gw.view(D, kc).add_(tmp[:, :kc])
+        store.grad_ready([conv_w, conv_b, cls, pos])
+        return (None,) * 10
+
+
+class EncoderBlockFn(torch.autograd.Function):
+    """One pre-LN transformer encoder block, forward and hand-written backward."""
+
+    @staticmethod
+    def forward(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, *params):
+        ext = _ext.ext()
+        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
+        T, D = x.shape
+        M = w1.shape[0]
+        scale = 1.0 / math.sqrt(D // H)
+        xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
+        qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
+        o, lse = ext.attn_fwd(qkv, B, N, H, scale)
+        x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=x)
+        xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
+        u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)
+        h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=drop1)
+        x2 = gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=drop2)
+        ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
+        ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        ext = _ext.ext()
+        x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = ctx.saved_tensors
+        B, N, H, scale, store, drop1, drop2, params = ctx.meta
+        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
+        g = store.grad_dest
+        dx2 = dx2.contiguous()
+        T, D = dx2.shape
+        # ---- MLP branch: x2 = x1 + drop2(h . W2^T + b2),  h = drop1(gelu(u)),  u = xn2 . W1^T + b1
+        if drop2 is not None:
+            dz2 = torch.empty_like(dx2)
+            gemm.bias_grad(dx2, g(b2), drop=drop2, dz=dz2)
+        else:
+            dz2 = dx2
+            if b2.requires_grad:
+                gemm.bias_grad(dx2, g(b2))
+        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, drop=drop1)
+        gw2 = g(w2)
+        if gw2 is not None:
+            gemm.linear_wgrad(dz2, h, gw2)
+        gw1 = g(w1)
+        if gw1 is not None:
+            gemm.linear_wgrad(du, xn2, gw1)
+        if b1.requires_grad:
+            gemm.bias_grad(du, g(b1))
+        dxn2 = gemm.linear_dgrad(du, store.bf16(w1))
+        dx1 = torch.empty_like(dx2)
+        ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T)
+        store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
+        # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
+        if bo.requires_grad:
+            gemm.bias_grad(dx1, g(bo))
+        do = gemm.linear_dgrad(dx1, store.bf16(wo))
+        gwo = g(wo)
+        if gwo is not None:
+            gemm.linear_wgrad(dx1, o, gwo)
+        dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
+        if bqkv.requires_grad:
+            gemm.bias_grad(dqkv, g(bqkv))
+        gwqkv = g(wqkv)
+        if gwqkv is not None:
+            gemm.linear_wgrad(dqkv, xn1, gwqkv)
+        dxn1 = gemm.linear_dgrad(dqkv, store.bf16(wqkv))
+        dx = torch.empty_like(dx2)
+        ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
+        store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])
+        return (dx,) + (None,) * (8 + len(params))
+
+
+class HeadFn(torch.autograd.Function):
+    """Final LayerNorm (token 0 only) + classifier Linear in fp32."""
+
+    @staticmethod
+    def forward(ctx, tokens, B, N, eps, store, ln_w, ln_b, head_w, head_b):
+        ext = _ext.ext()
+        T, D = tokens.shape
+        xc, mean, rstd = ext.layernorm_fwd(tokens, ln_w, ln_b, eps, B, N * D)
+        xcf = xc.float()
+        logits = F.linear(xcf, head_w, head_b)
+        ctx.save_for_backward(tokens, xcf, mean, rstd)
+        ctx.meta = (B, N, store, ln_w, ln_b, head_w, head_b)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        ext = _ext.ext()
+        tokens, xcf, mean, rstd = ctx.saved_tensors
+        B, N, store, ln_w, ln_b, head_w, head_b = ctx.meta
+        D = tokens.shape[1]
+        dlogits = dlogits.float().contiguous()
+        gw = store.grad_dest(head_w)
+        if gw is not None:
+            gw.addmm_(dlogits.t(), xcf)
+        gb = store.grad_dest(head_b)
+        if gb is not None:
+            gb.add_(dlogits.sum(0))
+        dxc = (dlogits @ head_w).to(torch.bfloat16).contiguous()
+        dtokens = torch.zeros_like(tokens)
+        ext.layernorm_bwd(dxc, D, tokens, N * D, mean, rstd, ln_w, None, 0, dtokens, N * D,
+                          store.grad_dest(ln_w), store.grad_dest(ln_b), B)
+        store.grad_ready([head_w, head_b, ln_w, ln_b])
+        return (dtokens,) + (None,) * 8
+
+
+class CrossEntropyFn(torch.autograd.Function):
+    """Mean softmax cross-entropy with the gradient produced in the same kernel pass."""
+
+    @staticmethod
+    def forward(ctx, logits, target):
+        ext = _ext.ext()
+        lf = logits.float().contiguous()
+        B = lf.shape[0]
+        dl = torch.empty_like(lf) if logits.requires_grad else None
+        rows = ext.xent(lf, target.long().contiguous(), dl, None, 1.0 / B)
+        ctx.save_for_backward(dl) if dl is not None else None
+        ctx.in_dtype = logits.dtype
+        return rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return (dl * g).to(ctx.in_dtype), None
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    if _ext.use_fused(logits) and logits.dim() == 2 and target.dim() == 1:
+        return CrossEntropyFn.apply(logits, target)
+    return F.cross_entropy(logits, target)
+
+
+class TokenLayerNormFn(torch.autograd.Function):
+    """LayerNorm over every row of a bf16 token matrix [T, D] (used by the classifier-free ViT)."""
+
+    @staticmethod
+    def forward(ctx, tokens, eps, store, w, b):
+        ext = _ext.ext()
+        T, D = tokens.shape
+        y, mean, rstd = ext.layernorm_fwd(tokens, w, b, eps, T, D)
+        ctx.save_for_backward(tokens, mean, rstd)
+        ctx.meta = (store, w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ext = _ext.ext()
+        tokens, mean, rstd = ctx.saved_tensors
+        store, w, b = ctx.meta
+        T, D = tokens.shape
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(tokens)
+        ext.layernorm_bwd(dy, D, tokens, D, mean, rstd, w, None, 0, dx, D, store.grad_dest(w), store.grad_dest(b), T)
+        store.grad_ready([w, b])
+        return dx, None, None, None, None

@@ -1,0 +1,93 @@
+"""Python front-end of the MFMA GEMM (csrc/gemm.hip): forward / dgrad / wgrad of a Linear layer.
+
+Shapes follow nn.Linear: ``x [T, K]``, ``w [N, K]`` (bf16 shadow of the fp32 master weight),
+``y = x . w^T [T, N]``. All three products run on the same hand-written kernel template with
+different operand layouts (k-contiguous or mn-contiguous LDS staging) — there are no transposed
+copies of activations or weights anywhere.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _ext
+
+EPI_BF16, EPI_GELU, EPI_DGELU, EPI_F32_ATOMIC, EPI_F32_STORE = range(5)
+
+# tile configs: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves), 2 = 128x256 (8 waves)
+_FORCE_TILE = os.environ.get("PVR_GEMM_TILE")
+
+Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
+
+
+def _tile(M: int, N: int, K: int, kind: str) -> int:
+    if _FORCE_TILE is not None:
+        return int(_FORCE_TILE)
+    return 0
+
+
+def _drop_args(drop: Drop):
+    if drop is None or drop[2] <= 0.0:
+        return None, 0, 0.0
+    return drop[0], int(drop[1]), float(drop[2])
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+               resid: Optional[torch.Tensor] = None, drop: Drop = None, gelu_aux: Optional[torch.Tensor] = None,
+               addend: Optional[torch.Tensor] = None, addend_period: int = 0,
+               row_remap: Tuple[int, int, int] = (0, 0, 0), out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = resid + dropout(x.w^T + bias + addend[row % period])  (or the GELU variant with aux)."""
+    T, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(T, N, dtype=torch.bfloat16, device=x.device)
+    seed, soff, p = _drop_args(drop)
+    epi = EPI_GELU if gelu_aux is not None else EPI_BF16
+    _ext.ext().gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
+                    row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, _tile(T, N, K, "fwd"))
+    return out
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch.Tensor] = None,
+                 drop: Drop = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dy . w ; optionally fused with the GELU + dropout backward of the producing layer:
+    dx = (dy . w) * mask * gelu'(aux)."""
+    T, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(T, K, dtype=torch.bfloat16, device=dy.device)
+    seed, soff, p = _drop_args(drop)
+    epi = EPI_DGELU if dgelu_aux is not None else EPI_BF16
+    _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
+                    seed, soff, p, 0, _tile(T, K, N, "dgrad"))
+    return out
+
+
+def wgrad_splits(T: int, N: int, K: int) -> int:
+    tiles = math.ceil(N / 128) * math.ceil(K / 128)
+    target = 1024
+    s = max(1, round(target / tiles))
+    s = min(s, max(1, T // 512))
+    return s
+
+
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[N, K] += dy^T . x   (fp32, split over tokens with f32 atomics)."""
+    T, N = dy.shape
+    K = x.shape[1]
+    splits = wgrad_splits(T, N, K)
+    ksplit = math.ceil(math.ceil(T / splits) / 64) * 64
+    _ext.ext().gemm(dy, False, x, False, out, N, K, T, EPI_F32_ATOMIC, None, None, None, 0, None, 0, 0, 0,
+                    None, 0, 0.0, ksplit, _tile(N, K, T, "wgrad"))
+    return out
+
+
+def bias_grad(dy: torch.Tensor, db: Optional[torch.Tensor], *, drop: Drop = None,
+              dz: Optional[torch.Tensor] = None) -> None:
+    """db += column sums of (mask * dy); writes the masked gradient to dz when given."""
+    T, N = dy.shape
+    seed, soff, p = _drop_args(drop)
+    _ext.ext().colsum(dy, T, N, db, dz, seed, soff, p)

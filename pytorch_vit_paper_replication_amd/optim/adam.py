@@ -1,0 +1,203 @@
+"""FusedAdam: torch.optim.Adam semantics, one HIP pass over the flat parameter store.
+
+Drop-in for the reference recipe (MAIN.ipynb:2818-2824: two param groups, wd 0.03 / 0.0, coupled L2
+weight decay, betas (0.9, 0.999), eps 1e-8) and for AdamW (``decoupled_weight_decay=True``).
+
+On the fused GPU path all parameters live in one ``ParamStore``; a step is
+  [optional] global-norm clip:  two deterministic reduction kernels -> {norm, coef, nonfinite} on device
+  Adam:                          one kernel: g*coef (+wd*p) -> m, v -> p -> bf16 shadow
+so clip_grad_norm_ + optimizer.step() (SURVEY.md K14+K15, ~1000 small launches) become 3 launches
+with no host synchronisation. Elsewhere (CPU, or parameters outside a store) it falls back to the
+exact torch.optim.Adam single-tensor math.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, Optional
+
+import numpy as np
+import torch
+
+from .. import _ext
+
+
+def _store_of(params):
+    st = None
+    for p in params:
+        s = getattr(p, "_pvr_store_ref", None)
+        s = s() if s is not None else None
+        if s is None:
+            return None
+        if st is None:
+            st = s
+        elif s is not st:
+            return None
+    return st
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 decoupled_weight_decay: bool = False, skip_nonfinite: bool = True, amsgrad: bool = False,
+                 maximize: bool = False):
+        if amsgrad or maximize:
+            raise NotImplementedError("FusedAdam supports neither amsgrad nor maximize")
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                        decoupled_weight_decay=decoupled_weight_decay)
+        super().__init__(params, defaults)
+        self.skip_nonfinite = skip_nonfinite
+        self._fused = None  # (store, m, v, seg_start, seg_group, ws, clip)
+        self.last_grad_norm: Optional[torch.Tensor] = None
+        self.step_count = 0
+
+    # ------------------------------------------------------------------ helpers
+    def _all_params(self):
+        return [p for g in self.param_groups for p in g["params"]]
+
+    def _setup_fused(self):
+        params = self._all_params()
+        if not params or not params[0].is_cuda or not _ext.available():
+            return None
+        from ..runtime.param_store import lookup_store
+
+        store = lookup_store(params[0])
+        if store is None or any(lookup_store(p) is not store for p in params):
+            return None
+        if not all(store.covers_param(p) for p in params):
+            return None
+        fz = self._fused
+        if fz is not None and fz[0] is store:
+            return fz
+        dev = store.device
+        group_of = {}
+        for gi, g in enumerate(self.param_groups):
+            for p in g["params"]:
+                group_of[id(p)] = gi
+        starts, groups = [], []
+        for p, off in zip(store.params, store.offsets):
+            starts.append(off)
+            groups.append(group_of.get(id(p), -1) if p.requires_grad else -1)
+        seg_start = torch.tensor(starts, dtype=torch.int64, device=dev)
+        seg_group = torch.tensor(groups, dtype=torch.int32, device=dev)
+        m = torch.zeros(store.numel, dtype=torch.float32, device=dev)
+        v = torch.zeros(store.numel, dtype=torch.float32, device=dev)
+        # carry over any existing per-tensor state (e.g. loaded from a checkpoint)
+        for p, off in zip(store.params, store.offsets):
+            st = self.state.get(p)
+            if st and "exp_avg" in st:
+                m[off:off + p.numel()].copy_(st["exp_avg"].reshape(-1))
+                v[off:off + p.numel()].copy_(st["exp_avg_sq"].reshape(-1))
+                self.step_count = max(self.step_count, int(st.get("step", 0)))
+        for p, off in zip(store.params, store.offsets):
+            if id(p) in group_of:
+                self.state[p] = {
+                    "step": torch.tensor(float(self.step_count)),
+                    "exp_avg": m[off:off + p.numel()].view(p.shape),
+                    "exp_avg_sq": v[off:off + p.numel()].view(p.shape),
+                }
+        ws = torch.empty(_ext.ext().norm_partial_blocks(), dtype=torch.float32, device=dev)
+        clip = torch.zeros(3, dtype=torch.float32, device=dev)
+        self._fused = (store, m, v, seg_start, seg_group, ws, clip)
+        return self._fused
+
+    def _group_table(self, step: int, device) -> torch.Tensor:
+        G = len(self.param_groups)
+        arr = np.zeros((G, 8), dtype=np.float32)
+        for i, g in enumerate(self.param_groups):
+            b1, b2 = g["betas"]
+            arr[i, 0] = float(g["lr"])
+            arr[i, 1] = b1
+            arr[i, 2] = b2
+            arr[i, 3] = g["eps"]
+            arr[i, 4] = g["weight_decay"]
+            arr[i, 5] = 1.0 - b1 ** step
+            arr[i, 6] = math.sqrt(1.0 - b2 ** step)
+        arr.view(np.int32)[:, 7] = [int(bool(g["decoupled_weight_decay"])) for g in self.param_groups]
+        return torch.from_numpy(arr).to(device, non_blocking=True)
+
+    # ------------------------------------------------------------------ public
+    def zero_grad(self, set_to_none: bool = True):
+        fz = self._setup_fused()
+        if fz is not None:
+            fz[0].zero_grad()  # one memset, gradient views stay attached
+            return
+        super().zero_grad(set_to_none=set_to_none)
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Global-norm clip of every gradient (after any DP all-reduce). Returns the norm (device)."""
+        fz = self._setup_fused()
+        if fz is None:
+            params = [p for p in self._all_params() if p.grad is not None]
+            n = torch.nn.utils.clip_grad_norm_(params, max_norm)
+            self.last_grad_norm = n
+            return n
+        store, m, v, seg_start, seg_group, ws, clip = fz
+        _ext.ext().grad_norm(store.grad_flat, float(max_norm), ws, clip)
+        self._pending_clip = True
+        self.last_grad_norm = clip[0]
+        return clip[0]
+
+    @torch.no_grad()
+    def step(self, closure=None, clip_norm: Optional[float] = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        fz = self._setup_fused()
+        self.step_count += 1
+        step = self.step_count
+        if fz is not None:
+            store, m, v, seg_start, seg_group, ws, clip = fz
+            use_clip = getattr(self, "_pending_clip", False)
+            if clip_norm is not None:
+                _ext.ext().grad_norm(store.grad_flat, float(clip_norm), ws, clip)
+                self.last_grad_norm = clip[0]
+                use_clip = True
+            elif not use_clip and self.skip_nonfinite:
+                _ext.ext().grad_norm(store.grad_flat, 0.0, ws, clip)  # max_norm 0 -> coef 1, flag only
+                use_clip = True
+            table = self._group_table(step, store.device)
+            _ext.ext().adam(store.flat, store.grad_flat, m, v, store.shadow, seg_start, seg_group, table,
+                            clip if use_clip else None, self.skip_nonfinite)
+            store.mark_shadow_fresh()
+            self._pending_clip = False
+            for st in self.state.values():
+                if "step" in st:
+                    st["step"] = torch.tensor(float(step))
+            return loss
+        # ---------------- reference math (torch.optim.Adam, single-tensor, maximize=False)
+        if clip_norm is not None:
+            self.clip_grad_norm_(clip_norm)
+        for g in self.param_groups:
+            b1, b2 = g["betas"]
+            lr, eps, wd = g["lr"], g["eps"], g["weight_decay"]
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                grad = p.grad
+                st = self.state[p]
+                if len(st) == 0 or "exp_avg" not in st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                t = float(st["step"])
+                if g["decoupled_weight_decay"]:
+                    p.mul_(1 - lr * wd)
+                elif wd != 0:
+                    grad = grad.add(p, alpha=wd)
+                st["exp_avg"].lerp_(grad, 1 - b1)
+                st["exp_avg_sq"].mul_(b2).addcmul_(grad, grad.conj(), value=1 - b2)
+                bc1 = 1 - b1 ** t
+                bc2 = 1 - b2 ** t
+                step_size = lr / bc1
+                denom = (st["exp_avg_sq"].sqrt() / math.sqrt(bc2)).add_(eps)
+                p.addcdiv_(st["exp_avg"], denom, value=-step_size)
+        return loss
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        fz = self._fused
+        self._fused = None
+        if fz is not None:
+            self._setup_fused()

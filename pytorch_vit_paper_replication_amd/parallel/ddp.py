@@ -1,0 +1,171 @@
+"""Data parallelism over RCCL/xGMI with gradient buckets overlapped with backward.
+
+Design, MI355X-first rather than a copy of torch DDP:
+  * the model's parameters live in one flat fp32 ``ParamStore``; its gradient buffer IS the bucket
+    storage — buckets are contiguous slices, so there is no flatten/unflatten copy and every
+    collective is one large message (xGMI links are point-to-point: few, big transfers);
+  * parameters are broadcast from rank 0 with ONE collective over the flat master buffer (C1);
+  * buckets are formed in reverse registration order (= backward order, last encoder block first),
+    ``bucket_cap_mb`` each (default ≈ one ViT-B encoder block: 28 MB of fp32 gradients);
+  * the fused backward Functions (or autograd hooks on the PyTorch path) report parameters as final;
+    a full bucket is all-reduced immediately with ``async_op=True`` — RCCL runs it on its own stream
+    ordered after the gradient kernels already queued, so it overlaps the remaining backward;
+  * buckets launch strictly in index order on every rank (no collective-order mismatch), and an
+    autograd end-of-backward callback flushes the rest and joins the stream before the optimizer
+    (the global-norm clip therefore sees averaged gradients, C3).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from ..runtime.param_store import ParamStore, get_store
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 28.0,
+                 broadcast_parameters: bool = True, comm_dtype: Optional[torch.dtype] = None):
+        super().__init__()
+        if not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("DistributedDataParallel needs an initialised torch.distributed process group")
+        self.module = module
+        self.process_group = process_group
+        self.world = dist.get_world_size(process_group)
+        self.bucket_cap = int(bucket_cap_mb * (1 << 20))
+        self.broadcast_parameters = broadcast_parameters
+        self.comm_dtype = comm_dtype
+        self.require_backward_grad_sync = True
+        self._store: Optional[ParamStore] = None
+        self._buckets: List[tuple] = []          # (start, end, [param indices])
+        self._bucket_of: Dict[int, int] = {}
+        self._pending: List[int] = []
+        self._ready_ids = set()
+        self._next_launch = 0
+        self._works: List = []
+        self._callback_queued = False
+        self._hooks = []
+        self._avg = dist.get_backend(process_group) == "nccl"
+
+    # ------------------------------------------------------------------ setup
+    def _setup(self, device):
+        store = get_store(self.module, device)
+        if store is self._store:
+            return store
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if self._store is not None:
+            self._store.remove_listener(self._on_ready)
+        self._store = store
+        if self.broadcast_parameters:
+            with torch.no_grad():
+                src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+                dist.broadcast(store.flat, src=src, group=self.process_group)
+                for b in self.module.buffers():
+                    dist.broadcast(b, src=src, group=self.process_group)
+            store.refresh_shadow(force=True)
+        # buckets: reverse parameter order, contiguous flat ranges of about bucket_cap bytes
+        buckets = []
+        cur: List[int] = []
+        cur_bytes = 0
+        for i in reversed(range(len(store.params))):
+            cur.append(i)
+            cur_bytes += store.params[i].numel() * 4
+            if cur_bytes >= self.bucket_cap:
+                buckets.append(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            buckets.append(cur)
+        self._buckets = []
+        self._bucket_of = {}
+        for bi, idxs in enumerate(buckets):
+            lo = min(store.offsets[i] for i in idxs)
+            hi_i = max(idxs)
+            hi = store.offsets[hi_i + 1] if hi_i + 1 < len(store.params) else store.numel
+            self._buckets.append((lo, hi, idxs))
+            for i in idxs:
+                self._bucket_of[id(store.params[i])] = bi
+        store.add_listener(self._on_ready)
+        for p in store.params:
+            if p.requires_grad:
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda t: self._on_ready([t])))
+        return store
+
+    def _reset(self):
+        st = self._store
+        self._pending = [sum(1 for i in idxs if st.params[i].requires_grad) for (_, _, idxs) in self._buckets]
+        self._ready_ids = set()
+        self._next_launch = 0
+        self._works = []
+        self._callback_queued = False
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, *args, **kwargs):
+        dev = next(self.module.parameters()).device
+        store = self._setup(dev)
+        if torch.is_grad_enabled():
+            store.prepare_grads()
+        self._reset()
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    # ------------------------------------------------------------------ backward hooks
+    def _on_ready(self, params):
+        if not self.require_backward_grad_sync or self._store is None:
+            return
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        for p in params:
+            b = self._bucket_of.get(id(p))
+            if b is None or id(p) in self._ready_ids or not p.requires_grad:
+                continue
+            self._ready_ids.add(id(p))
+            self._pending[b] -= 1
+        while self._next_launch < len(self._buckets) and self._pending[self._next_launch] <= 0:
+            self._launch(self._next_launch)
+            self._next_launch += 1
+
+    def _launch(self, b: int):
+        lo, hi, _ = self._buckets[b]
+        buf = self._store.grad_flat[lo:hi]
+        if self.comm_dtype is not None and self.comm_dtype != buf.dtype:
+            tmp = buf.to(self.comm_dtype)
+            op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+            w = dist.all_reduce(tmp, op=op, group=self.process_group, async_op=True)
+            self._works.append((w, buf, tmp))
+        else:
+            op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+            w = dist.all_reduce(buf, op=op, group=self.process_group, async_op=True)
+            self._works.append((w, buf, None))
+
+    def _finalize(self):
+        while self._next_launch < len(self._buckets):
+            self._launch(self._next_launch)
+            self._next_launch += 1
+        for w, buf, tmp in self._works:
+            w.wait()
+            if tmp is not None:
+                buf.copy_(tmp)
+            if not self._avg:
+                buf.div_(self.world)
+        self._works = []
+
+    # convenience passthroughs
+    def state_dict(self, *a, **k):
+        return self.module.state_dict(*a, **k)
+
+    def load_state_dict(self, *a, **k):
+        return self.module.load_state_dict(*a, **k)

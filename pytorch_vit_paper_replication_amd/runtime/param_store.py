@@ -1,0 +1,194 @@
+"""Flat parameter / gradient / bf16-shadow store for the fused GPU path.
+
+On the first fused forward on a device, every parameter of the model is re-pointed (``p.data``)
+into one contiguous fp32 master buffer, and ``p.grad`` into one contiguous fp32 gradient buffer
+(the same Parameter objects survive, so an optimizer built before ``model.to(device)`` keeps
+working — SURVEY.md §3.4). A bf16 shadow of the master buffer feeds the MFMA GEMMs; it is
+refreshed by one cast kernel whenever a parameter changed outside the fused optimizer (detected
+from the per-parameter autograd version counters), and written directly by
+:class:`~pytorch_vit_paper_replication_amd.optim.FusedAdam` otherwise.
+
+The fused autograd Functions write weight gradients straight into the gradient views (split-K
+wgrad GEMMs accumulate with f32 atomics, bias/LN gradients are reduced in-kernel), so the
+gradient buffer doubles as the data-parallel all-reduce buckets (``parallel.ddp``): no copy into
+bucket storage and no per-tensor collectives. ``grad_ready`` notifies listeners (the DDP
+bucketer) as soon as a group of parameters has its final gradient.
+"""
+from __future__ import annotations
+
+import weakref
+from typing import Callable, Dict, Iterable, List, Optional
+
+import torch
+
+from .. import _ext
+
+ALIGN = 64  # elements; keeps every parameter 256-B aligned and 4-element vectorisable
+
+
+def _norm_device(device) -> torch.device:
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+class ParamStore:
+    def __init__(self, module: torch.nn.Module, device: torch.device):
+        seen = set()
+        params: List[torch.nn.Parameter] = []
+        names: List[str] = []
+        for n, p in module.named_parameters():
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            params.append(p)
+            names.append(n)
+        self.device = _norm_device(device)
+        self.params = params
+        self.names = names
+        self.offsets: List[int] = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = max(off, ALIGN)
+        self._index: Dict[int, int] = {id(p): i for i, p in enumerate(params)}
+        with torch.inference_mode(False), torch.no_grad():
+            self.flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            self.grad_flat = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            self.shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            self._views = []
+            self._gviews = []
+            self._sviews = []
+            for p, o in zip(params, self.offsets):
+                n = p.numel()
+                v = self.flat[o:o + n].view(p.shape)
+                v.copy_(p.data.to(self.device, torch.float32).reshape(p.shape))
+                old_grad = p.grad
+                p.data = v
+                gv = self.grad_flat[o:o + n].view(p.shape)
+                if old_grad is not None:
+                    gv.copy_(old_grad.to(self.device, torch.float32).reshape(p.shape))
+                self._views.append(v)
+                self._gviews.append(gv)
+                self._sviews.append(self.shadow[o:o + n].view(p.shape))
+                if p.requires_grad:
+                    p.grad = gv
+                p._pvr_store_ref = weakref.ref(self)
+        self._shadow_key: Optional[int] = None
+        self._listeners: List[Callable[[List[torch.nn.Parameter]], None]] = []
+        self.refresh_shadow(force=True)
+
+    # ------------------------------------------------------------------ validity
+    def covers(self, module: torch.nn.Module) -> bool:
+        """True if every parameter of ``module`` still lives in this store's buffers."""
+        for p in module.parameters():
+            i = self._index.get(id(p))
+            if i is None or p.data.data_ptr() != self._views[i].data_ptr() or p.device != self.device:
+                return False
+        return True
+
+    def covers_param(self, p: torch.nn.Parameter) -> bool:
+        i = self._index.get(id(p))
+        return i is not None and p.device == self.device and p.data.data_ptr() == self._views[i].data_ptr()
+
+    # ------------------------------------------------------------------ shadow
+    def _version_key(self) -> int:
+        return sum(p._version for p in self.params)
+
+    def refresh_shadow(self, force: bool = False) -> None:
+        key = self._version_key()
+        if force or key != self._shadow_key:
+            with torch.inference_mode(False), torch.no_grad():
+                if self.flat.is_cuda and _ext.available():
+                    _ext.ext().cast_f32_bf16(self.flat, self.shadow)
+                else:
+                    self.shadow.copy_(self.flat)
+            self._shadow_key = key
+
+    def mark_shadow_fresh(self) -> None:
+        """Called by the fused optimizer after it rewrote master + shadow in one pass."""
+        self._shadow_key = self._version_key()
+
+    def bf16(self, p: torch.nn.Parameter) -> torch.Tensor:
+        return self._sviews[self._index[id(p)]]
+
+    def offset(self, p: torch.nn.Parameter) -> int:
+        return self.offsets[self._index[id(p)]]
+
+    def contains(self, p: torch.nn.Parameter) -> bool:
+        return id(p) in self._index
+
+    # ------------------------------------------------------------------ gradients
+    def prepare_grads(self) -> None:
+        """Make every trainable parameter's .grad a view of the flat gradient buffer.
+
+        ``zero_grad(set_to_none=True)`` leaves ``p.grad is None``, which means "zero": the region is
+        cleared and the view re-attached. A foreign tensor a user assigned is copied in.
+        """
+        with torch.inference_mode(False), torch.no_grad():
+            for i, p in enumerate(self.params):
+                if not p.requires_grad:
+                    continue
+                gv = self._gviews[i]
+                g = p.grad
+                if g is None:
+                    gv.zero_()
+                    p.grad = gv
+                elif g.data_ptr() != gv.data_ptr():
+                    gv.copy_(g)
+                    p.grad = gv
+
+    def grad_dest(self, p: torch.nn.Parameter) -> Optional[torch.Tensor]:
+        """fp32 gradient view to accumulate into, or None if the parameter is frozen."""
+        if not p.requires_grad:
+            return None
+        i = self._index[id(p)]
+        gv = self._gviews[i]
+        g = p.grad
+        if g is None:
+            gv.zero_()
+            p.grad = gv
+        elif g.data_ptr() != gv.data_ptr():
+            gv.copy_(g)
+            p.grad = gv
+        return gv
+
+    def zero_grad(self) -> None:
+        self.grad_flat.zero_()
+        for i, p in enumerate(self.params):
+            if p.requires_grad:
+                p.grad = self._gviews[i]
+
+    def add_listener(self, fn: Callable[[List[torch.nn.Parameter]], None]) -> None:
+        self._listeners.append(fn)
+
+    def remove_listener(self, fn) -> None:
+        if fn in self._listeners:
+            self._listeners.remove(fn)
+
+    def grad_ready(self, params: Iterable[torch.nn.Parameter]) -> None:
+        if self._listeners:
+            ps = [p for p in params if p is not None]
+            for fn in self._listeners:
+                fn(ps)
+
+
+def lookup_store(p: torch.nn.Parameter) -> Optional[ParamStore]:
+    """The live store that owns ``p`` (None if the parameter moved out of it)."""
+    r = getattr(p, "_pvr_store_ref", None)
+    st = r() if r is not None else None
+    if st is None or not st.covers_param(p):
+        return None
+    return st
+
+
+def get_store(module: torch.nn.Module, device: torch.device) -> ParamStore:
+    """Return the module's store for ``device``, (re)building it if parameters moved."""
+    st: Optional[ParamStore] = getattr(module, "_pvr_store", None)
+    if st is not None and st.device == _norm_device(device) and st.covers(module):
+        return st
+    st = ParamStore(module, device)
+    object.__setattr__(module, "_pvr_store", st)
+    return st

@@ -1,0 +1,305 @@
+"""Numerics checks of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Each check returns (name, err, tol) where err is max|out - ref| / max(1, max|ref|) (a scale-relative
+max error). Used by tests/test_gpu_kernels.py (pytest -m gpu) and runnable standalone
+(`python tests/kernel_checks.py`) to print all errors in one GPU session.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+from typing import Callable, List, Tuple
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
+from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel_err(out: torch.Tensor, ref: torch.Tensor) -> float:
+    out = out.float()
+    ref = ref.float()
+    scale = max(1.0, ref.abs().max().item())
+    return (out - ref).abs().max().item() / scale
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale)
+
+
+# ----------------------------------------------------------------------------- GEMM
+def check_gemm_fwd(M, N, K, tile=0, bias=True, resid=False) -> Tuple[str, float, float]:
+    x, w = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05))
+    b = rnd(N) if bias else None
+    r = bf(rnd(M, N)) if resid else None
+    old = G._FORCE_TILE
+    G._FORCE_TILE = str(tile)
+    try:
+        y = G.linear_fwd(x, w, b, resid=r)
+    finally:
+        G._FORCE_TILE = old
+    ref = x.float() @ w.float().t()
+    if b is not None:
+        ref = ref + b
+    if r is not None:
+        ref = ref + r.float()
+    return (f"gemm_fwd M{M} N{N} K{K} t{tile} b{int(bias)} r{int(resid)}", rel_err(y, ref), 2e-2)
+
+
+def check_gemm_gelu(M, N, K, tile=0):
+    x, w, b = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05)), rnd(N)
+    u = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    old = G._FORCE_TILE
+    G._FORCE_TILE = str(tile)
+    try:
+        h = G.linear_fwd(x, w, b, gelu_aux=u)
+    finally:
+        G._FORCE_TILE = old
+    uref = x.float() @ w.float().t() + b
+    e1 = rel_err(u, uref)
+    e2 = rel_err(h, F.gelu(uref))
+    return (f"gemm_gelu M{M} N{N} K{K} t{tile}", max(e1, e2), 2e-2)
+
+
+def check_gemm_dgrad(M, N, K, tile=0):
+    dy, w = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05))
+    old = G._FORCE_TILE
+    G._FORCE_TILE = str(tile)
+    try:
+        dx = G.linear_dgrad(dy, w)
+    finally:
+        G._FORCE_TILE = old
+    return (f"gemm_dgrad M{M} N{N} K{K} t{tile}", rel_err(dx, dy.float() @ w.float()), 2e-2)
+
+
+def check_gemm_dgelu(M, N, K):
+    dy, w, u = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05)), bf(rnd(M, K))
+    dx = G.linear_dgrad(dy, w, dgelu_aux=u)
+    uf = u.float().requires_grad_(True)
+    g = torch.autograd.grad(F.gelu(uf), uf, torch.ones_like(uf))[0]
+    ref = (dy.float() @ w.float()) * g
+    return (f"gemm_dgelu M{M} N{N} K{K}", rel_err(dx, ref), 2e-2)
+
+
+def check_gemm_wgrad(T, N, K, tile=0):
+    dy, x = bf(rnd(T, N)), bf(rnd(T, K))
+    out = torch.zeros(N, K, device=DEV)
+    old = G._FORCE_TILE
+    G._FORCE_TILE = str(tile)
+    try:
+        G.linear_wgrad(dy, x, out)
+        G.linear_wgrad(dy, x, out)  # accumulates
+    finally:
+        G._FORCE_TILE = old
+    ref = 2 * (dy.float().t() @ x.float())
+    return (f"gemm_wgrad T{T} N{N} K{K} t{tile}", rel_err(out, ref), 5e-3)
+
+
+def check_gemm_dropout(M=512, N=256, K=128, p=0.1):
+    x, w = bf(torch.ones(M, K, device=DEV)), bf(torch.full((N, K), 1.0 / K, device=DEV))
+    seed = torch.tensor([12345], dtype=torch.int64, device=DEV)
+    y = G.linear_fwd(x, w, None, drop=(seed, 7 << 32, p))
+    keep = (y.float() != 0)
+    rate = 1 - keep.float().mean().item()
+    scale_ok = abs(y.float()[keep].mean().item() - 1.0 / (1 - p)) < 1e-2
+    # backward mask (colsum kernel) must zero exactly the same elements
+    dz = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    G.bias_grad(bf(torch.ones(M, N, device=DEV)), db, drop=(seed, 7 << 32, p), dz=dz)
+    same = torch.equal(dz.float() != 0, keep)
+    err = abs(rate - p) + (0 if scale_ok else 1) + (0 if same else 1)
+    return ("dropout rate/scale/fwd-bwd mask", err, 1e-2)
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+def check_layernorm(T, D):
+    ext = _ext.ext()
+    x = bf(rnd(T, D) * 2 + 0.5)
+    w, b = rnd(D) * 0.5 + 1, rnd(D) * 0.1
+    y, mean, rstd = ext.layernorm_fwd(x, w, b, 1e-5, T, D)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (D,), wr, br, 1e-5)
+    e1 = rel_err(y, ref)
+    dy = bf(rnd(T, D))
+    dres = bf(rnd(T, D))
+    ref.backward(dy.float())
+    dx = torch.empty_like(x)
+    dw = torch.zeros(D, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    ext.layernorm_bwd(dy, D, x, D, mean, rstd, w, dres, D, dx, D, dw, db, T)
+    e2 = rel_err(dx, xr.grad + dres.float())
+    e3 = rel_err(dw, wr.grad)
+    e4 = rel_err(db, br.grad)
+    return (f"layernorm T{T} D{D}", max(e1, e2, e3 / 10, e4 / 10), 2e-2)
+
+
+# ----------------------------------------------------------------------------- attention
+def _attn_ref(qkv, B, N, H):
+    D = qkv.shape[1] // 3
+    dh = D // H
+    q, k, v = qkv.float().view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    lse = torch.logsumexp(s, -1)
+    o = torch.softmax(s, -1) @ v
+    return o.transpose(1, 2).reshape(B * N, D), lse.reshape(B * H, N)
+
+
+def check_attn_fwd(B, N, H):
+    ext = _ext.ext()
+    D = H * 64
+    qkv = bf(rnd(B * N, 3 * D))
+    o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / 8.0)
+    oref, lref = _attn_ref(qkv, B, N, H)
+    return (f"attn_fwd B{B} N{N} H{H}", max(rel_err(o, oref), rel_err(lse, lref) / 5), 2e-2)
+
+
+def check_attn_bwd(B, N, H):
+    ext = _ext.ext()
+    D = H * 64
+    qkv = bf(rnd(B * N, 3 * D))
+    o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / 8.0)
+    do = bf(rnd(B * N, D))
+    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / 8.0)
+    qr = qkv.float().requires_grad_(True)
+    oref, _ = _attn_ref(qr, B, N, H)
+    oref.backward(do.float())
+    return (f"attn_bwd B{B} N{N} H{H}", rel_err(dqkv, qr.grad), 3e-2)
+
+
+# ----------------------------------------------------------------------------- misc
+def check_xent(B, C):
+    ext = _ext.ext()
+    logits = rnd(B, C) * 3
+    y = torch.randint(0, C, (B,), device=DEV)
+    dl = torch.empty_like(logits)
+    corr = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rows = ext.xent(logits, y, dl, corr, 1.0 / B)
+    lr = logits.clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, y)
+    ref.backward()
+    e = max(rel_err(rows.mean(), ref), rel_err(dl, lr.grad) * 10)
+    ok_acc = corr.item() == (logits.argmax(1) == y).sum().item()
+    return (f"xent B{B} C{C}", e + (0 if ok_acc else 1), 1e-4)
+
+
+def check_adam():
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay
+    from pytorch_vit_paper_replication_amd.runtime.param_store import get_store
+
+    torch.manual_seed(0)
+    m1 = ViT(image_size=32, patch_size=16, num_transformer_layer=1, num_heads=2, embedding_dim=128, mlp_size=256,
+             num_classes=10).to(DEV)
+    m2 = ViT(image_size=32, patch_size=16, num_transformer_layer=1, num_heads=2, embedding_dim=128, mlp_size=256,
+             num_classes=10).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    st = get_store(m1, torch.device(DEV))
+    o1 = FusedAdam(param_groups_weight_decay(m1, 0.03), lr=1e-2)
+    o2 = torch.optim.Adam(param_groups_weight_decay(m2, 0.03), lr=1e-2)
+    for it in range(3):
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            g = torch.randn_like(p1) * (it + 1)
+            p1.grad.copy_(g)
+            p2.grad = g.clone()
+        o1.step(clip_norm=1.0)
+        torch.nn.utils.clip_grad_norm_(m2.parameters(), 1.0)
+        o2.step()
+    err = max(rel_err(p1, p2) for p1, p2 in zip(m1.parameters(), m2.parameters()))
+    sh = max(rel_err(st.bf16(p1), p1) for p1 in m1.parameters())
+    return ("fused adam+clip vs torch.optim.Adam", err + (0 if sh < 1e-2 else 1), 1e-5)
+
+
+def check_vit_fused_vs_reference(B=4, train=False):
+    """Whole-model forward logits and parameter gradients, fused bf16 vs PyTorch fp32 (dropout 0)."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+
+    torch.manual_seed(0)
+    cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=128, mlp_size=256,
+               num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0)
+    mf = ViT(**cfg).to(DEV)
+    mr = ViT(**cfg).to(DEV)
+    mr.load_state_dict(mf.state_dict())
+    x = torch.rand(B, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B,), device=DEV)
+    mf.train(train)
+    mr.train(train)
+    lf = mf(x)
+    os.environ["PVR_DISABLE_FUSED"] = "1"
+    try:
+        lr = mr(x)
+    finally:
+        os.environ["PVR_DISABLE_FUSED"] = "0"
+    e_fwd = rel_err(lf, lr)
+    F.cross_entropy(lf, y).backward()
+    F.cross_entropy(lr, y).backward()
+    e_g = 0.0
+    worst = ""
+    for (n, p1), p2 in zip(mf.named_parameters(), mr.parameters()):
+        gs = max(p2.grad.abs().max().item(), 1e-6)
+        e = (p1.grad - p2.grad).abs().max().item() / gs
+        if e > e_g:
+            e_g, worst = e, n
+    return (f"vit fused vs fp32 ref (fwd {e_fwd:.2e}, worst grad {worst})", max(e_fwd, e_g / 3), 5e-2)
+
+
+def all_checks() -> List[Callable]:
+    c = []
+    for tile in (0, 1, 2):
+        c.append(lambda t=tile: check_gemm_fwd(50432 // 16, 768, 768, t))
+        c.append(lambda t=tile: check_gemm_fwd(197 * 3, 2304, 768, t, True, True))
+        c.append(lambda t=tile: check_gemm_gelu(197 * 2, 3072, 768, t))
+        c.append(lambda t=tile: check_gemm_dgrad(197 * 2, 3072, 768, t))
+        c.append(lambda t=tile: check_gemm_wgrad(197 * 5, 768, 3072, t))
+    c += [
+        lambda: check_gemm_fwd(100, 64, 128, 0, True, True),
+        lambda: check_gemm_dgelu(394, 768, 3072),
+        lambda: check_gemm_wgrad(17, 64, 128),
+        lambda: check_gemm_dropout(),
+        lambda: check_layernorm(394, 768),
+        lambda: check_layernorm(100, 1024),
+        lambda: check_layernorm(33, 1280),
+        lambda: check_attn_fwd(2, 197, 3),
+        lambda: check_attn_fwd(1, 17, 2),
+        lambda: check_attn_fwd(1, 577, 2),
+        lambda: check_attn_bwd(2, 197, 3),
+        lambda: check_attn_bwd(1, 17, 2),
+        lambda: check_attn_bwd(1, 64, 1),
+        lambda: check_attn_bwd(1, 257, 2),
+        lambda: check_attn_bwd(1, 577, 2),
+        lambda: check_xent(8, 1000),
+        lambda: check_xent(3, 3),
+        lambda: check_adam(),
+        lambda: check_vit_fused_vs_reference(4, False),
+        lambda: check_vit_fused_vs_reference(3, True),
+    ]
+    return c
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    bad = 0
+    for fn in all_checks():
+        try:
+            name, err, tol = fn()
+            torch.cuda.synchronize()
+            ok = err <= tol
+            bad += not ok
+            print(f"{'OK  ' if ok else 'FAIL'} {name:70s} err={err:.3e} tol={tol:.1e}", flush=True)
+        except Exception as e:  # keep going: report every kernel in one GPU session
+            bad += 1
+            print(f"ERR  {getattr(fn, '__name__', fn)}: {type(e).__name__}: {e}", flush=True)
+            if "HIP error" in str(e) or "hipError" in str(e) or "illegal" in str(e).lower():
+                break
+    print(f"{bad} failing checks")
+    sys.exit(1 if bad else 0)
