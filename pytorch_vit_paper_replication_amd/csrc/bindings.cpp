@@ -20,6 +20,7 @@ struct GemmParams {
   int k_split_len;
   int epi;
   int tile_cfg;
+  uint64_t* dbg;
 };
 struct AdamGroup {
   float lr, beta1, beta2, eps, weight_decay;
@@ -33,6 +34,7 @@ hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
+hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
 hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
@@ -86,8 +88,10 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
           int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> addend,
           int64_t addend_period, c10::optional<torch::Tensor> aux, int64_t row_group, int64_t row_stride_group,
           int64_t row_offset, c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, int64_t k_split,
-          int64_t tile_cfg) {
+          int64_t tile_cfg, c10::optional<torch::Tensor> dbg) {
   pvr::GemmParams p{};
+  if (dbg.has_value() && dbg->defined()) p.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr());
+  p.drop_scale = 1.f;
   p.M = (int)M; p.N = (int)N; p.K = (int)K;
   p.A = bf(A, "A"); p.lda = ld_of(A, "A"); p.a_kcontig = a_kcontig;
   p.B = bf(B, "B"); p.ldb = ld_of(B, "B"); p.b_kcontig = b_kcontig;
@@ -154,6 +158,13 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
 void cast_f32_bf16(torch::Tensor in, torch::Tensor out) {
   TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "cast: shape/contiguity");
   check(pvr_cast_f32_bf16(f32(in, "in"), bf_mut(out, "out"), in.numel(), stream()), "cast_f32_bf16");
+}
+
+void transpose_batched(torch::Tensor src, torch::Tensor dst, torch::Tensor meta, int64_t total_tiles) {
+  TORCH_CHECK(meta.scalar_type() == torch::kInt64 && meta.is_cuda() && meta.dim() == 2 && meta.size(1) == 5, "meta");
+  check(pvr_transpose_batched(bf(src, "src"), bf_mut(dst, "dst"), meta.data_ptr<int64_t>(), (int)meta.size(0), (int)total_tiles,
+                              stream()),
+        "transpose_batched");
 }
 
 void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tensor> db, c10::optional<torch::Tensor> dz,
@@ -281,10 +292,15 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
+        py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),
+        py::arg("addend_period"), py::arg("aux"), py::arg("row_group"), py::arg("row_stride_group"),
+        py::arg("row_offset"), py::arg("seed"), py::arg("seed_offset"), py::arg("drop_p"), py::arg("k_split"),
+        py::arg("tile_cfg"), py::arg("dbg") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("transpose_batched", &transpose_batched);
   m.def("colsum", &colsum);
   m.def("im2col", &im2col);
   m.def("cls_rows", &cls_rows);

@@ -79,9 +79,16 @@ PVR_DEV uint32_t rng_hash(uint64_t seed, uint64_t idx) {
   h ^= h >> 16;
   return h;
 }
-// keep iff (hash & 0xFFFF) >= threshold, threshold = round(p * 65536).
+// Element idx is kept iff its 16-bit half of hash(seed, idx >> 1) is >= thr16 = round(p * 65536):
+// one hash serves two neighbouring elements.
 PVR_DEV bool rng_keep(uint64_t seed, uint64_t idx, uint32_t thr16) {
-  return (rng_hash(seed, idx) & 0xFFFFu) >= thr16;
+  return ((rng_hash(seed, idx >> 1) >> ((idx & 1) * 16)) & 0xFFFFu) >= thr16;
+}
+// Pair form for an even idx: keep decisions of idx and idx + 1 from one hash.
+PVR_DEV void rng_keep2(uint64_t seed, uint64_t idx_even, uint32_t thr16, bool& k0, bool& k1) {
+  const uint32_t h = rng_hash(seed, idx_even >> 1);
+  k0 = (h & 0xFFFFu) >= thr16;
+  k1 = (h >> 16) >= thr16;
 }
 
 PVR_DEV float gelu_erf(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }

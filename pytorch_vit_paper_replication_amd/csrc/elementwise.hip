@@ -131,8 +131,41 @@ __global__ void __launch_bounds__(256) patch_bwd_kernel(const uint16_t* __restri
   }
 }
 
+// Batched bf16 transpose: matrix t (rows R_t, cols C_t) at src + soff[t] -> dst + doff[t] as [C_t][R_t].
+// 64x64 tiles through LDS (padded rows: conflict-free column reads); tile_start[t] = prefix tile count.
+__global__ void __launch_bounds__(256) transpose_batched_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                                 const int64_t* __restrict__ meta, int nmat) {
+  __shared__ uint16_t tile[64][66];
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < nmat && meta[(t + 1) * 5 + 4] <= b) ++t;
+  const int64_t soff = meta[t * 5 + 0], doff = meta[t * 5 + 1];
+  const int R = (int)meta[t * 5 + 2], C = (int)meta[t * 5 + 3];
+  const int local = b - (int)meta[t * 5 + 4];
+  const int tc = (C + 63) / 64;
+  const int r0 = (local / tc) * 64, c0 = (local % tc) * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int rr = i / 64, cc = i % 64;
+    if (r0 + rr < R && c0 + cc < C) tile[rr][cc] = src[soff + (int64_t)(r0 + rr) * C + c0 + cc];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int cc = i / 64, rr = i % 64;
+    if (r0 + rr < R && c0 + cc < C) dst[doff + (int64_t)(c0 + cc) * R + r0 + rr] = tile[rr][cc];
+  }
+}
+
 }  // namespace
 }  // namespace pvr
+
+// meta: int64 [nmat][5] = {src_off, dst_off, rows, cols, tile_prefix}; total_tiles = sum of tiles
+extern "C" hipError_t pvr_transpose_batched(const uint16_t* src, uint16_t* dst, const int64_t* meta, int nmat, int total_tiles,
+                                            hipStream_t s) {
+  using namespace pvr;
+  if (total_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(transpose_batched_kernel, dim3(total_tiles), dim3(256), 0, s, src, dst, meta, nmat);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pvr_cast_f32_bf16(const float* in, uint16_t* out, int64_t n, hipStream_t s) {
   using namespace pvr;

@@ -18,6 +18,7 @@
 // ds_read_b64_tr_b16 hardware transpose for mn-contig). Two LDS stages: the DMA for tile t+1 is in
 // flight while the MFMAs of tile t run.
 #include "common.h"
+#include <type_traits>
 
 namespace pvr {
 
@@ -43,9 +44,17 @@ struct GemmParams {
   int k_split_len;
   int epi;
   int tile_cfg;
+  uint64_t* dbg;  // diagnostic s_memtime stamps [block][4] (null in normal runs)
 };
 
 namespace {
+
+PVR_DEV void stamp(const GemmParams& p, int slot) {
+  if (p.dbg && threadIdx.x == 0) {
+    const int b = blockIdx.x + gridDim.x * blockIdx.z;
+    p.dbg[(int64_t)b * 4 + slot] = __builtin_amdgcn_s_memtime();
+  }
+}
 
 constexpr int TK = 64;  // K depth of one LDS stage
 
@@ -108,6 +117,139 @@ PVR_DEV uint32_t rsrc_bytes(int64_t extent_elems, int64_t base_elems) {
   return (uint32_t)b;
 }
 
+// Shared epilogue: acc[i][j] is the 16x16 fragment at rows mb + 16i, cols nb + 16j.
+// SWAP layout (bf16 / fp32-store outputs): bias is loaded once, and the per-row inputs (residual,
+// GELU pre-activation, position addend) of fragment row i+1 are issued BEFORE the stores of row i:
+// vmcnt counts stores too, so a load issued after a store would wait for that store's completion.
+template <int FN, int EPI>
+struct RowIn {
+  uint2 r[FN];   // residual (EPI_BF16) or aux pre-activation (EPI_DGELU), 4 bf16
+  float4 a[FN];  // addend (EPI_BF16)
+};
+
+template <int FN, int EPI>
+PVR_DEV void load_row(const GemmParams& p, int m, int64_t orow, int nb, int g, RowIn<FN, EPI>& in) {
+  if (m >= p.M) return;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nb + 16 * j + 4 * g;
+    if (n >= p.N) continue;
+    if constexpr (EPI == EPI_BF16) {
+      if (p.resid) in.r[j] = *(const uint2*)(p.resid + (int64_t)m * p.ld_resid + n);
+      if (p.addend) in.a[j] = *(const float4*)(p.addend + (orow % p.addend_period) * p.N + n);
+    } else if constexpr (EPI == EPI_DGELU) {
+      in.r[j] = *(const uint2*)(p.aux + (int64_t)m * p.ld_aux + n);
+    }
+  }
+}
+
+PVR_DEV int64_t out_row(const GemmParams& p, int m) {
+  return p.row_group ? (int64_t)(m / p.row_group) * p.row_stride_group + p.row_offset + m % p.row_group : (int64_t)m;
+}
+
+template <int FM, int FN, bool SWAP, int EPI>
+PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  if constexpr (SWAP) {
+    // lane holds C[m = mb + 16i + li][n = nb + 16j + 4g + r], r = 0..3 (4 consecutive columns)
+    const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
+    float4 bias[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bias[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+        const int n = nb + 16 * j + 4 * g;
+        if (p.bias && n < p.N) bias[j] = *(const float4*)(p.bias + n);
+      }
+    }
+    RowIn<FN, EPI> cur, nxt;
+    load_row<FN, EPI>(p, mb + li, out_row(p, mb + li), nb, g, cur);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mb + 16 * i + li;
+      const int64_t orow = out_row(p, m);
+      if (i + 1 < FM) load_row<FN, EPI>(p, m + 16, out_row(p, m + 16), nb, g, nxt);
+      if (m < p.M) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = nb + 16 * j + 4 * g;
+          if (n >= p.N) continue;
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          bool keep[4] = {true, true, true, true};
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU) {
+            if (p.drop_thr) {
+              const uint64_t idx = (uint64_t)orow * p.N + n;
+              rng_keep2(seed, idx, p.drop_thr, keep[0], keep[1]);
+              rng_keep2(seed, idx + 2, p.drop_thr, keep[2], keep[3]);
+            }
+          }
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+            v[0] += bias[j].x; v[1] += bias[j].y; v[2] += bias[j].z; v[3] += bias[j].w;
+          }
+          if constexpr (EPI == EPI_BF16) {
+            if (p.addend) {
+              v[0] += cur.a[j].x; v[1] += cur.a[j].y; v[2] += cur.a[j].z; v[3] += cur.a[j].w;
+            }
+            if (p.drop_thr) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = keep[r] ? v[r] * p.drop_scale : 0.f;
+            }
+            if (p.resid) {
+              const uint2 rr = cur.r[j];
+              v[0] += bf2f(rr.x & 0xFFFF); v[1] += bf2f(rr.x >> 16);
+              v[2] += bf2f(rr.y & 0xFFFF); v[3] += bf2f(rr.y >> 16);
+            }
+            uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+            *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
+          } else if constexpr (EPI == EPI_GELU) {
+            uint2 u; u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]);
+            *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float h = gelu_erf(v[r]);
+              v[r] = keep[r] ? h * p.drop_scale : 0.f;
+            }
+            uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+            *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
+          } else if constexpr (EPI == EPI_DGELU) {
+            const uint2 uu = cur.r[j];
+            const float u[4] = {bf2f(uu.x & 0xFFFF), bf2f(uu.x >> 16), bf2f(uu.y & 0xFFFF), bf2f(uu.y >> 16)};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = keep[r] ? v[r] * p.drop_scale * gelu_erf_grad(u[r]) : 0.f;
+            uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+            *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
+          } else if constexpr (EPI == EPI_F32_STORE) {
+            *(float4*)((float*)p.C + orow * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd((float*)p.C + orow * p.ldc + n + r, v[r]);
+          }
+        }
+      }
+      cur = nxt;
+    }
+  } else {
+    // lane holds C[m = mb + 16i + 4g + r][n = nb + 16j + li]; f32 outputs (64-B row segments per instruction)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nb + 16 * j + li;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = mb + 16 * i + 4 * g + r;
+          if (m >= p.M) continue;
+          float* dst = (float*)p.C + (int64_t)m * p.ldc + n;
+          if constexpr (EPI == EPI_F32_ATOMIC)
+            atomicAdd(dst, acc[i][j][r]);
+          else
+            *dst = acc[i][j][r];
+        }
+      }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP, int EPI>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_kernel(GemmParams p) {
   constexpr int NW = WM * WN;
@@ -157,12 +299,14 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
+  stamp(p, 0);
   if (nk > 0) {
     stage_tile<BM, AK, NW>(ars, smem, p.lda, 0, wave, lane);
     stage_tile<BN, BKC, NW>(brs, smem + A_BYTES, p.ldb, 0, wave, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  stamp(p, 1);
   for (int kt = 0; kt < nk; ++kt) {
     char* cur = smem + (kt & 1) * STAGE;
     if (kt + 1 < nk) {
@@ -191,95 +335,10 @@ __global__ void __launch_bounds__(WM* WN * 64) gemm_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  // ------------------------------------------------------------------ epilogue
-  const int g = lane >> 4, li = lane & 15;
-  if constexpr (SWAP) {
-    // lane holds C[m = .. + li][n = .. + 4g + r], r = 0..3 (4 consecutive columns)
-    const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * WTM + 16 * i + li;
-      if (m >= p.M) continue;
-      int64_t orow = m;
-      if (p.row_group) orow = (int64_t)(m / p.row_group) * p.row_stride_group + p.row_offset + m % p.row_group;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * WTN + 16 * j + 4 * g;
-        if (n >= p.N) continue;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
-          if (p.bias) {
-            const float4 bb = *(const float4*)(p.bias + n);
-            v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-          }
-        }
-        if constexpr (EPI == EPI_BF16) {
-          if (p.addend) {
-            const float4 ad = *(const float4*)(p.addend + (orow % p.addend_period) * p.N + n);
-            v[0] += ad.x; v[1] += ad.y; v[2] += ad.z; v[3] += ad.w;
-          }
-          if (p.drop_thr) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              v[r] = rng_keep(seed, (uint64_t)orow * p.N + n + r, p.drop_thr) ? v[r] * p.drop_scale : 0.f;
-          }
-          if (p.resid) {
-            const uint2 rr = *(const uint2*)(p.resid + (int64_t)m * p.ld_resid + n);
-            v[0] += bf2f(rr.x & 0xFFFF); v[1] += bf2f(rr.x >> 16);
-            v[2] += bf2f(rr.y & 0xFFFF); v[3] += bf2f(rr.y >> 16);
-          }
-          uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-          *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
-        } else if constexpr (EPI == EPI_GELU) {
-          uint2 u; u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]);
-          *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = u;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float h = gelu_erf(v[r]);
-            if (p.drop_thr) h = rng_keep(seed, (uint64_t)orow * p.N + n + r, p.drop_thr) ? h * p.drop_scale : 0.f;
-            v[r] = h;
-          }
-          uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-          *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
-        } else if constexpr (EPI == EPI_DGELU) {
-          const uint2 uu = *(const uint2*)(p.aux + (int64_t)m * p.ld_aux + n);
-          const float u[4] = {bf2f(uu.x & 0xFFFF), bf2f(uu.x >> 16), bf2f(uu.y & 0xFFFF), bf2f(uu.y >> 16)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float d = v[r];
-            if (p.drop_thr) d = rng_keep(seed, (uint64_t)orow * p.N + n + r, p.drop_thr) ? d * p.drop_scale : 0.f;
-            v[r] = d * gelu_erf_grad(u[r]);
-          }
-          uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-          *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
-        } else if constexpr (EPI == EPI_F32_STORE) {
-          *(float4*)((float*)p.C + orow * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) atomicAdd((float*)p.C + orow * p.ldc + n + r, v[r]);
-        }
-      }
-    }
-  } else {
-    // lane holds C[m = .. + 4g + r][n = .. + li]; used for f32 outputs (64-B row segments per instruction)
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * WTN + 16 * j + li;
-        if (n >= p.N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WTM + 16 * i + 4 * g + r;
-          if (m >= p.M) continue;
-          float* dst = (float*)p.C + (int64_t)m * p.ldc + n;
-          if constexpr (EPI == EPI_F32_ATOMIC)
-            atomicAdd(dst, acc[i][j][r]);
-          else
-            *dst = acc[i][j][r];
-        }
-      }
-  }
+  stamp(p, 2);
+  epilogue<FM, FN, SWAP, EPI>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(p, 3);
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP, int EPI>
@@ -299,11 +358,384 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ===================================================================================== multistage
+// 4-stage LDS ring, BK = 32, counted vmcnt (LDS-DMA for up to STAGES-2 future stages stays in flight
+// across the barrier), one raw s_barrier per stage, 8 waves. 256-row tiles halve the L2->LDS bytes
+// per MFMA against 128x128 (which needs ~64 B/clk/CU at peak MFMA rate, the whole L2 bandwidth).
+constexpr int BK32 = 32;
+
+PVR_DEV int swz_k32(int row) { return (row >> 1) & 3; }  // 64-B rows: conflict-free ds_read_b128
+
+template <int R, bool KC, int NW>
+PVR_DEV void stage32(__amdgpu_buffer_rsrc_t rs, char* lds, int64_t ld, int k0, int wave, int lane) {
+  if constexpr (KC) {
+    constexpr int NI = R / 16;  // image [R][4 chunks], one wave-instruction = 16 rows
+#pragma unroll
+    for (int i = 0; i < NI / NW; ++i) {
+      const int s = wave + NW * i;
+      const int row = s * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ swz_k32(row);
+      const uint32_t voff = (uint32_t)(row * ld * 2 + (int64_t)(k0 + c * 8) * 2);
+      dma16(rs, to_lds(lds + s * 1024), voff);
+    }
+  } else {
+    constexpr int CPR = R / 8, RPI = 64 / CPR, NI = BK32 / RPI;  // image [32 k-rows][R/8 chunks]
+#pragma unroll
+    for (int i = 0; i < NI / NW; ++i) {
+      const int s = wave + NW * i;
+      const int row = s * RPI + lane / CPR;
+      const int pc = lane % CPR;
+      const int c = (pc & ~15) | ((pc & 15) ^ swz_mn(row));
+      const uint32_t voff = (uint32_t)((int64_t)(k0 + row) * ld * 2 + c * 16);
+      dma16(rs, to_lds(lds + s * 1024), voff);
+    }
+  }
+}
+
+template <int R, bool KC>
+PVR_DEV v8s frag32(const char* lds, int r0, int lane) {
+  if constexpr (KC) {
+    const int row = r0 + (lane & 15);
+    return ds_read_b128(lds + row * 64 + (((lane >> 4) ^ swz_k32(row)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int c = (r0 >> 3) + (p >> 1);
+    const int kr0 = 8 * g + q, kr1 = kr0 + 4;
+    const int pc0 = (c & ~15) | ((c & 15) ^ swz_mn(kr0));
+    const int pc1 = (c & ~15) | ((c & 15) ^ swz_mn(kr1));
+    return cat44(ds_read_tr(lds + kr0 * (R * 2) + pc0 * 16 + 8 * (p & 1)),
+                 ds_read_tr(lds + kr1 * (R * 2) + pc1 * 16 + 8 * (p & 1)));
+  }
+}
+
+// Wait until at most N of this wave's vector-memory ops (LDS-DMA) are outstanding, then barrier.
+// The asm "memory" clobbers keep the compiler from moving LDS accesses across the barrier.
+template <int N>
+PVR_DEV void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// Same, and also retire this wave's outstanding LDS reads (their slot is refilled after the barrier).
+template <int N>
+PVR_DEV void wait_barrier_lds() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool AK, bool BKC, bool SWAP, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64) gemm_ms_kernel(GemmParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int A_BYTES = BM * BK32 * 2, B_BYTES = BN * BK32 * 2, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int LPS = (A_BYTES / 1024 + B_BYTES / 1024) / NW;  // LDS-DMA instructions per wave per stage
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = t / ntn, tn = t % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * p.k_split_len;
+  const int kend = min(p.K, kbeg + p.k_split_len);
+  const int nk = (kend - kbeg + BK32 - 1) / BK32;
+
+  const uint16_t* abase;
+  uint32_t abytes;
+  if constexpr (AK) {
+    abase = p.A + (int64_t)m0 * p.lda + kbeg;
+    abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg);
+  } else {
+    abase = p.A + (int64_t)kbeg * p.lda + m0;
+    abytes = rsrc_bytes((int64_t)(p.K - 1) * p.lda + p.M, (int64_t)kbeg * p.lda + m0);
+  }
+  const uint16_t* bbase;
+  uint32_t bbytes;
+  if constexpr (BKC) {
+    bbase = p.B + (int64_t)n0 * p.ldb + kbeg;
+    bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg);
+  } else {
+    bbase = p.B + (int64_t)kbeg * p.ldb + n0;
+    bbytes = rsrc_bytes((int64_t)(p.K - 1) * p.ldb + p.N, (int64_t)kbeg * p.ldb + n0);
+  }
+  const __amdgpu_buffer_rsrc_t ars = make_rsrc(abase, abytes);
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bbase, bbytes);
+
+  v4f acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: stages 0 .. STAGES-2
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      char* dst = smem + s * STAGE_BYTES;
+      stage32<BM, AK, NW>(ars, dst, p.lda, s * BK32, wave, lane);
+      stage32<BN, BKC, NW>(brs, dst + A_BYTES, p.ldb, s * BK32, wave, lane);
+    }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + STAGES - 2 < nk)
+      wait_barrier<(STAGES - 2) * LPS>();  // steady state: STAGES-2 future stages stay in flight
+    else
+      wait_barrier<0>();
+    const int ks = kt + STAGES - 1;
+    if (ks < nk) {
+      char* dst = smem + (ks % STAGES) * STAGE_BYTES;
+      stage32<BM, AK, NW>(ars, dst, p.lda, ks * BK32, wave, lane);
+      stage32<BN, BKC, NW>(brs, dst + A_BYTES, p.ldb, ks * BK32, wave, lane);
+    }
+    const char* cur = smem + (kt % STAGES) * STAGE_BYTES;
+    v8s af[FM], bf[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = frag32<BM, AK>(cur, wm * WTM + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bf[j] = frag32<BN, BKC>(cur + A_BYTES, wn * WTN + 16 * j, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (SWAP)
+          acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+        else
+          acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  epilogue<FM, FN, SWAP, EPI>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane);
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool AK, bool BKC, bool SWAP, int EPI>
+hipError_t launch_ms(const GemmParams& p, hipStream_t s) {
+  constexpr int SMEM = STAGES * (BM + BN) * BK32 * 2;
+  auto kern = gemm_ms_kernel<BM, BN, WM, WN, STAGES, AK, BKC, SWAP, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int nsplit = (p.K + p.k_split_len - 1) / p.k_split_len;
+  hipLaunchKernelGGL(kern, dim3(ntm * ntn, 1, nsplit), dim3(WM * WN * 64), SMEM, s, p);
+  return hipGetLastError();
+}
+
+// ===================================================================================== v3
+// 4 waves (2x2) per workgroup, wave tile (BM/2)x(BN/2) (128x128 at 256x256: 256 fp32 accumulators
+// per lane in the AGPR half of the unified register file, one wave per SIMD), BK = 32, 4-stage
+// LDS-DMA ring. Fragments are register double-buffered: the ds_reads of stage k+1 are issued while
+// the MFMAs of stage k run, so LDS latency is hidden behind the matrix pipe instead of exposed after
+// every barrier. The barrier ending stage k waits (counted vmcnt) for stage k+2 to land, so stage
+// k+1 is already visible when its fragments are read; one DMA stage stays in flight across it.
+template <int FM, int FN, int BM, int BN, bool AK, bool BKC>
+PVR_DEV void load_frags(const char* stage, int wm, int wn, int lane, v8s (&af)[FM], v8s (&bf)[FN]) {
+  constexpr int A_BYTES = BM * BK32 * 2;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) af[i] = frag32<BM, AK>(stage, wm * (16 * FM) + 16 * i, lane);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bf[j] = frag32<BN, BKC>(stage + A_BYTES, wn * (16 * FN) + 16 * j, lane);
+}
+
+template <int FM, int FN, bool SWAP>
+PVR_DEV void mfma_block(v4f (&acc)[FM][FN], const v8s (&af)[FM], const v8s (&bf)[FN]) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (SWAP)
+        acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+      else
+        acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    }
+}
+
+// One LDS-DMA wave-instruction (the idx-th of this wave) of a BK=32 operand tile.
+template <int R, bool KC, int NW>
+PVR_DEV void dma_one(__amdgpu_buffer_rsrc_t rs, char* lds, int64_t ld, int k0, int wave, int lane, int idx) {
+  const int s = wave + NW * idx;
+  if constexpr (KC) {
+    const int row = s * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ swz_k32(row);
+    dma16(rs, to_lds(lds + s * 1024), (uint32_t)(row * ld * 2 + (int64_t)(k0 + c * 8) * 2));
+  } else {
+    constexpr int CPR = R / 8, RPI = 64 / CPR;
+    const int row = s * RPI + lane / CPR;
+    const int pc = lane % CPR;
+    const int c = (pc & ~15) | ((pc & 15) ^ swz_mn(row));
+    dma16(rs, to_lds(lds + s * 1024), (uint32_t)((int64_t)(k0 + row) * ld * 2 + c * 16));
+  }
+}
+
+PVR_DEV __amdgpu_buffer_rsrc_t pick_rsrc(bool live, __amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t dead) {
+  return live ? r : dead;
+}
+
+template <int I, int N, class F>
+PVR_DEV void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// One pipeline stage: 16x16x32 MFMAs of fragment set (ac, bc) into acc, interleaved with (a) this
+// wave's LDS-DMA instructions for the stage `ds` (into LDS `dst`) and (b) the ds_reads of the next
+// stage's fragments (from `nxt`) into (an, bn). Branch-free, so the whole stage is one scheduling
+// region and sched_group_barrier pins the interleave: per fragment row, {DMA, ds_reads, MFMAs}.
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP>
+PVR_DEV void v3_stage(v4f (&acc)[BM / WM / 16][BN / WN / 16], const v8s (&ac)[BM / WM / 16], const v8s (&bc)[BN / WN / 16],
+                      v8s (&an)[BM / WM / 16], v8s (&bn)[BN / WN / 16], const char* nxt, char* dst,
+                      __amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, int64_t lda, int64_t ldb, int dk0,
+                      int wave, int lane, int wm, int wn) {
+  constexpr int NW = WM * WN, FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int A_BYTES = BM * BK32 * 2;
+  constexpr int NIA = (BM * BK32 * 2 / 1024) / NW, NIB = (BN * BK32 * 2 / 1024) / NW, ND = NIA + NIB;
+  static_for<0, FM>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    constexpr int d0 = i * ND / FM, d1 = (i + 1) * ND / FM;
+    constexpr int j0 = i * FN / FM, j1 = (i + 1) * FN / FM;
+#pragma unroll
+    for (int d = d0; d < d1; ++d) {
+      if (d < NIA)
+        dma_one<BM, AK, NW>(ars, dst, lda, dk0, wave, lane, d);
+      else
+        dma_one<BN, BKC, NW>(brs, dst + A_BYTES, ldb, dk0, wave, lane, d - NIA);
+    }
+    an[i] = frag32<BM, AK>(nxt, wm * (16 * FM) + 16 * i, lane);
+#pragma unroll
+    for (int j = j0; j < j1; ++j) bn[j] = frag32<BN, BKC>(nxt + A_BYTES, wn * (16 * FN) + 16 * j, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (SWAP)
+        acc[i][j] = mfma16(bc[j], ac[i], acc[i][j]);
+      else
+        acc[i][j] = mfma16(ac[i], bc[j], acc[i][j]);
+    }
+    constexpr int nds = (AK ? 1 : 2) + (j1 - j0) * (BKC ? 1 : 2);  // b128 per k-contig frag, 2 tr reads otherwise
+    if constexpr (d1 > d0) __builtin_amdgcn_sched_group_barrier(0x020, d1 - d0, 0);  // VMEM read (LDS-DMA)
+    __builtin_amdgcn_sched_group_barrier(0x100, nds, 0);                              // DS read
+    __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);                               // MFMA
+  });
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64, WM* WN / 4) gemm_v3_kernel(GemmParams p) {
+  constexpr int NW = WM * WN, STAGES = 4;
+  constexpr int A_BYTES = BM * BK32 * 2, B_BYTES = BN * BK32 * 2, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int LPS = (A_BYTES / 1024 + B_BYTES / 1024) / NW;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // wave tile in 16x16 fragments
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = t / ntn, tn = t % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * p.k_split_len;
+  const int kend = min(p.K, kbeg + p.k_split_len);
+  const int nk = (kend - kbeg + BK32 - 1) / BK32;
+
+  const uint16_t* abase;
+  uint32_t abytes;
+  if constexpr (AK) {
+    abase = p.A + (int64_t)m0 * p.lda + kbeg;
+    abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg);
+  } else {
+    abase = p.A + (int64_t)kbeg * p.lda + m0;
+    abytes = rsrc_bytes((int64_t)(p.K - 1) * p.lda + p.M, (int64_t)kbeg * p.lda + m0);
+  }
+  const uint16_t* bbase;
+  uint32_t bbytes;
+  if constexpr (BKC) {
+    bbase = p.B + (int64_t)n0 * p.ldb + kbeg;
+    bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg);
+  } else {
+    bbase = p.B + (int64_t)kbeg * p.ldb + n0;
+    bbytes = rsrc_bytes((int64_t)(p.K - 1) * p.ldb + p.N, (int64_t)kbeg * p.ldb + n0);
+  }
+  const __amdgpu_buffer_rsrc_t ars = make_rsrc(abase, abytes);
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bbase, bbytes);
+  const __amdgpu_buffer_rsrc_t nul = make_rsrc(abase, 0);  // every access out of range: no traffic
+
+  v4f acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  stamp(p, 0);
+  // Prologue: stages 0..3 (stages >= nk use the null resource, keeping every vmcnt count uniform).
+#pragma unroll
+  for (int s = 0; s < STAGES; ++s) {
+    char* dst = smem + s * STAGE_BYTES;
+    stage32<BM, AK, NW>(pick_rsrc(s < nk, ars, nul), dst, p.lda, s * BK32, wave, lane);
+    stage32<BN, BKC, NW>(pick_rsrc(s < nk, brs, nul), dst + A_BYTES, p.ldb, s * BK32, wave, lane);
+  }
+  wait_barrier<2 * LPS>();  // stages 0 and 1 landed
+  v8s a0[FM], b0[FN], a1[FM], b1[FN];
+  load_frags<FM, FN, BM, BN, AK, BKC>(smem, wm, wn, lane, a0, b0);
+  wait_barrier_lds<2 * LPS>();  // every wave holds stage 0 in registers: slot 0 may be refilled
+  stamp(p, 1);
+
+  // Invariant at stage kt: its fragments are in registers, its LDS slot receives stage kt+4, stage
+  // kt+1 is visible. The barrier after stage kt waits for stage kt+2 and retires the LDS reads.
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    v3_stage<BM, BN, WM, WN, AK, BKC, SWAP>(acc, a0, b0, a1, b1, smem + ((kt + 1) % STAGES) * STAGE_BYTES,
+                                    smem + (kt % STAGES) * STAGE_BYTES, pick_rsrc(kt + 4 < nk, ars, nul),
+                                    pick_rsrc(kt + 4 < nk, brs, nul), p.lda, p.ldb, (kt + 4) * BK32, wave, lane, wm, wn);
+    wait_barrier_lds<2 * LPS>();
+    v3_stage<BM, BN, WM, WN, AK, BKC, SWAP>(acc, a1, b1, a0, b0, smem + ((kt + 2) % STAGES) * STAGE_BYTES,
+                                    smem + ((kt + 1) % STAGES) * STAGE_BYTES, pick_rsrc(kt + 5 < nk, ars, nul),
+                                    pick_rsrc(kt + 5 < nk, brs, nul), p.lda, p.ldb, (kt + 5) * BK32, wave, lane, wm, wn);
+    wait_barrier_lds<2 * LPS>();
+  }
+  if (kt < nk) mfma_block<FM, FN, SWAP>(acc, a0, b0);  // odd tail: set 0 holds the last stage
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // no LDS-DMA may outlive the workgroup
+  stamp(p, 2);
+  epilogue<FM, FN, SWAP, EPI>(p, acc, m0 + wm * (16 * FM), n0 + wn * (16 * FN), lane);
+  if (p.dbg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(p, 3);
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP, int EPI>
+hipError_t launch_v3(const GemmParams& p, hipStream_t s) {
+  constexpr int SMEM = 4 * (BM + BN) * BK32 * 2;
+  auto kern = gemm_v3_kernel<BM, BN, WM, WN, AK, BKC, SWAP, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int nsplit = (p.K + p.k_split_len - 1) / p.k_split_len;
+  hipLaunchKernelGGL(kern, dim3(ntm * ntn, 1, nsplit), dim3(WM * WN * 64), SMEM, s, p);
+  return hipGetLastError();
+}
+
 template <bool AK, bool BKC, bool SWAP, int EPI>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   switch (p.tile_cfg) {
     case 1: return launch_cfg<256, 128, 4, 2, AK, BKC, SWAP, EPI>(p, s);
     case 2: return launch_cfg<128, 256, 2, 4, AK, BKC, SWAP, EPI>(p, s);
+    case 3: return launch_ms<256, 256, 2, 4, 4, AK, BKC, SWAP, EPI>(p, s);
+    case 4: return launch_ms<256, 128, 4, 2, 4, AK, BKC, SWAP, EPI>(p, s);
+    case 5: return launch_ms<128, 256, 2, 4, 4, AK, BKC, SWAP, EPI>(p, s);
+    case 6: return launch_v3<256, 256, 2, 4, AK, BKC, SWAP, EPI>(p, s);
+    case 7: return launch_v3<256, 128, 2, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 8: return launch_v3<256, 256, 2, 2, AK, BKC, SWAP, EPI>(p, s);
     default: return launch_cfg<128, 128, 2, 2, AK, BKC, SWAP, EPI>(p, s);
   }
 }
@@ -327,6 +759,7 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
       if (ak && bk) return launch_tile<true, true, true, EPI_GELU>(p, s);
       break;
     case EPI_DGELU:
+      if (ak && bk) return launch_tile<true, true, true, EPI_DGELU>(p, s);
       if (ak && !bk) return launch_tile<true, false, true, EPI_DGELU>(p, s);
       break;
     case EPI_F32_ATOMIC:

@@ -37,6 +37,10 @@ class ViT(_FullViT):
         dev = x.device
         store = get_store(self, dev)
         store.refresh_shadow()
+        if not getattr(store, "_vit_t_registered", False):
+            store.register_transposed([w for blk in self.transformer_encoder for w in blk.fused_params()[2:12:2] if w.dim() == 2])
+            store._vit_t_registered = True
+        store.ensure_transposed()
         training = self.training
         if torch.is_grad_enabled():
             store.prepare_grads()

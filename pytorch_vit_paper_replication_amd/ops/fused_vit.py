@@ -122,7 +122,7 @@ class EncoderBlockFn(torch.autograd.Function):
             dz2 = dx2
             if b2.requires_grad:
                 gemm.bias_grad(dx2, g(b2))
-        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, drop=drop1)
+        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, drop=drop1, wt=store.bf16_t(w2))
         gw2 = g(w2)
         if gw2 is not None:
             gemm.linear_wgrad(dz2, h, gw2)
@@ -131,14 +131,14 @@ class EncoderBlockFn(torch.autograd.Function):
             gemm.linear_wgrad(du, xn2, gw1)
         if b1.requires_grad:
             gemm.bias_grad(du, g(b1))
-        dxn2 = gemm.linear_dgrad(du, store.bf16(w1))
+        dxn2 = gemm.linear_dgrad(du, store.bf16(w1), wt=store.bf16_t(w1))
         dx1 = torch.empty_like(dx2)
         ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T)
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
         if bo.requires_grad:
             gemm.bias_grad(dx1, g(bo))
-        do = gemm.linear_dgrad(dx1, store.bf16(wo))
+        do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
         gwo = g(wo)
         if gwo is not None:
             gemm.linear_wgrad(dx1, o, gwo)
@@ -148,7 +148,7 @@ class EncoderBlockFn(torch.autograd.Function):
         gwqkv = g(wqkv)
         if gwqkv is not None:
             gemm.linear_wgrad(dqkv, xn1, gwqkv)
-        dxn1 = gemm.linear_dgrad(dqkv, store.bf16(wqkv))
+        dxn1 = gemm.linear_dgrad(dqkv, store.bf16(wqkv), wt=store.bf16_t(wqkv))
         dx = torch.empty_like(dx2)
         ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])

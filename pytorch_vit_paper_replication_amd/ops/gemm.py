@@ -24,8 +24,13 @@ Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device
 
 
 def _tile(M: int, N: int, K: int, kind: str) -> int:
+    """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py):
+    k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave LDS-DMA ring (6); token-reduced
+    wgrad (both operands mn-contiguous, split-K atomics) -> 128x128 (0)."""
     if _FORCE_TILE is not None:
         return int(_FORCE_TILE)
+    if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
+        return 6
     return 0
 
 
@@ -52,17 +57,22 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch.Tensor] = None,
-                 drop: Drop = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 drop: Drop = None, out: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy . w ; optionally fused with the GELU + dropout backward of the producing layer:
-    dx = (dy . w) * mask * gelu'(aux)."""
+    dx = (dy . w) * mask * gelu'(aux). With ``wt`` (= w^T, [K, N] bf16) the weight operand is
+    k-contiguous and the fast forward-layout kernel runs; otherwise w is read with transposed LDS reads."""
     T, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(T, K, dtype=torch.bfloat16, device=dy.device)
     seed, soff, p = _drop_args(drop)
     epi = EPI_DGELU if dgelu_aux is not None else EPI_BF16
-    _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-                    seed, soff, p, 0, _tile(T, K, N, "dgrad"))
+    if wt is not None and N % 64 == 0:
+        _ext.ext().gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
+                        seed, soff, p, 0, _tile(T, K, N, "dgrad_t"))
+    else:
+        _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
+                        seed, soff, p, 0, _tile(T, K, N, "dgrad"))
     return out
 
 

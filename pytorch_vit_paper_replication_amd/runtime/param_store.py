@@ -77,6 +77,12 @@ class ParamStore:
                     p.grad = gv
                 p._pvr_store_ref = weakref.ref(self)
         self._shadow_key: Optional[int] = None
+        self._t_params: List[torch.nn.Parameter] = []
+        self._t_views: Dict[int, torch.Tensor] = {}
+        self._t_meta: Optional[torch.Tensor] = None
+        self._t_tiles = 0
+        self._t_dirty = True
+        self.shadow_t: Optional[torch.Tensor] = None
         self._listeners: List[Callable[[List[torch.nn.Parameter]], None]] = []
         self.refresh_shadow(force=True)
 
@@ -106,10 +112,48 @@ class ParamStore:
                 else:
                     self.shadow.copy_(self.flat)
             self._shadow_key = key
+            self._t_dirty = True
 
     def mark_shadow_fresh(self) -> None:
         """Called by the fused optimizer after it rewrote master + shadow in one pass."""
         self._shadow_key = self._version_key()
+        self._t_dirty = True
+
+    # ------------------------------------------------------------------ transposed bf16 weights
+    def register_transposed(self, params: Iterable[torch.nn.Parameter]) -> None:
+        """Keep a bf16 W^T copy of these 2-D weights (the dgrad GEMM's B operand, k-contiguous)."""
+        ps = [p for p in params if id(p) not in self._t_views and p.dim() == 2]
+        if not ps:
+            return
+        self._t_params.extend(ps)
+        total = sum((p.numel() + ALIGN - 1) // ALIGN * ALIGN for p in self._t_params)
+        with torch.inference_mode(False), torch.no_grad():
+            self.shadow_t = torch.empty(total, dtype=torch.bfloat16, device=self.device)
+            meta, off, tiles = [], 0, 0
+            self._t_views = {}
+            for p in self._t_params:
+                R, C = p.shape
+                self._t_views[id(p)] = self.shadow_t[off:off + p.numel()].view(C, R)
+                meta.append([self.offset(p), off, R, C, tiles])
+                tiles += ((R + 63) // 64) * ((C + 63) // 64)
+                off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+            self._t_meta = torch.tensor(meta, dtype=torch.int64, device=self.device)
+            self._t_tiles = tiles
+        self._t_dirty = True
+
+    def ensure_transposed(self) -> None:
+        if not self._t_params or not self._t_dirty:
+            return
+        with torch.inference_mode(False), torch.no_grad():
+            if self.flat.is_cuda and _ext.available():
+                _ext.ext().transpose_batched(self.shadow, self.shadow_t, self._t_meta, self._t_tiles)
+            else:
+                for p in self._t_params:
+                    self._t_views[id(p)].copy_(self.bf16(p).t())
+        self._t_dirty = False
+
+    def bf16_t(self, p: torch.nn.Parameter) -> Optional[torch.Tensor]:
+        return self._t_views.get(id(p))
 
     def bf16(self, p: torch.nn.Parameter) -> torch.Tensor:
         return self._sviews[self._index[id(p)]]

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Microbenchmarks of the hand-written gfx950 kernels at ViT-B/16 training shapes (batch 256 ->
+T = 50432 tokens), against the vendor-library / PyTorch equivalents on the same random data:
+  * GEMM fwd / dgrad / wgrad (ours, per tile config) vs torch.matmul (hipBLASLt)
+  * attention fwd / bwd vs torch scaled_dot_product_attention
+  * LayerNorm fwd / bwd vs torch
+Prints one line per case: time (ms), TFLOP/s (or GB/s), ratio vs the library.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
+from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
+
+
+def timeit(fn, iters=20, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--tiles", default="0,1,2")
+    ap.add_argument("--only", default="gemm,attn,ln")
+    a = ap.parse_args()
+    dev = "cuda"
+    T = a.batch * 197
+    D, M3, M = 768, 2304, 3072
+    tiles = [int(t) for t in a.tiles.split(",")]
+    torch.manual_seed(0)
+    if "gemm" in a.only:
+        for (n, k, name) in [(M3, D, "qkv"), (D, D, "out"), (M, D, "fc1"), (D, M, "fc2")]:
+            x = torch.randn(T, k, device=dev, dtype=torch.bfloat16)
+            w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
+            b = torch.randn(n, device=dev)
+            dy = torch.randn(T, n, device=dev, dtype=torch.bfloat16)
+            fl = 2.0 * T * n * k
+            t_lib = timeit(lambda: torch.matmul(x, w.t()))
+            print(f"fwd   {name:4s} T{T} N{n} K{k}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
+            for t in tiles:
+                G._FORCE_TILE = str(t)
+                tt = timeit(lambda: G.linear_fwd(x, w, b))
+                print(f"fwd   {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
+            t_lib = timeit(lambda: torch.matmul(dy, w))
+            print(f"dgrad {name:4s} T{T} N{k} K{n}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
+            wt = w.t().contiguous()
+            for t in tiles:
+                G._FORCE_TILE = str(t)
+                tt = timeit(lambda: G.linear_dgrad(dy, w, wt=wt))
+                print(f"dgrad {name:4s} tile{t}   ours(wT) {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
+            out = torch.zeros(n, k, device=dev)
+            t_lib = timeit(lambda: torch.matmul(dy.t(), x))
+            print(f"wgrad {name:4s} N{n} K{k} T{T}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
+            for t in tiles:
+                G._FORCE_TILE = str(t)
+                tt = timeit(lambda: G.linear_wgrad(dy, x, out))
+                print(f"wgrad {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
+            G._FORCE_TILE = None
+    if "attn" in a.only:
+        ext = _ext.ext()
+        B, N, H = a.batch, 197, 12
+        qkv = torch.randn(B * N, 3 * D, device=dev, dtype=torch.bfloat16)
+        fl = 4.0 * B * H * N * N * 64
+        tt = timeit(lambda: ext.attn_fwd(qkv, B, N, H, 0.125))
+        q, k, v = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4).contiguous()
+        t_lib = timeit(lambda: F.scaled_dot_product_attention(q, k, v))
+        print(f"attn_fwd B{B} N{N} H{H}: ours {tt:.3f} ms {fl / tt / 1e9:.1f} TF | sdpa {t_lib:.3f} ms x{t_lib / tt:.2f}", flush=True)
+        o, lse = ext.attn_fwd(qkv, B, N, H, 0.125)
+        do = torch.randn_like(o)
+        tt = timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125))
+        qr, kr, vr = (t.detach().requires_grad_(True) for t in (q, k, v))
+        orf = F.scaled_dot_product_attention(qr, kr, vr)
+        dor = torch.randn_like(orf)
+        t_lib = timeit(lambda: torch.autograd.grad(orf, (qr, kr, vr), dor, retain_graph=True))
+        print(f"attn_bwd B{B} N{N} H{H}: ours {tt:.3f} ms {2.5 * fl / tt / 1e9:.1f} TF | sdpa {t_lib:.3f} ms x{t_lib / tt:.2f}", flush=True)
+    if "ln" in a.only:
+        ext = _ext.ext()
+        x = torch.randn(T, D, device=dev, dtype=torch.bfloat16)
+        w, b = torch.ones(D, device=dev), torch.zeros(D, device=dev)
+        tt = timeit(lambda: ext.layernorm_fwd(x, w, b, 1e-5, T, D))
+        t_lib = timeit(lambda: F.layer_norm(x, (D,), w.bfloat16(), b.bfloat16()))
+        gb = 2 * T * D * 2 / 1e9
+        print(f"ln_fwd T{T} D{D}: ours {tt:.3f} ms {gb / tt * 1e3:.0f} GB/s | torch {t_lib:.3f} ms x{t_lib / tt:.2f}", flush=True)
+        y, mu, rs = ext.layernorm_fwd(x, w, b, 1e-5, T, D)
+        dx = torch.empty_like(x)
+        dw, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        tt = timeit(lambda: ext.layernorm_bwd(x, D, x, D, mu, rs, w, x, D, dx, D, dw, db, T))
+        print(f"ln_bwd T{T} D{D}: ours {tt:.3f} ms {4 * T * D * 2 / 1e9 / tt * 1e3:.0f} GB/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

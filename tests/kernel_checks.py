@@ -71,20 +71,20 @@ def check_gemm_gelu(M, N, K, tile=0):
     return (f"gemm_gelu M{M} N{N} K{K} t{tile}", max(e1, e2), 2e-2)
 
 
-def check_gemm_dgrad(M, N, K, tile=0):
+def check_gemm_dgrad(M, N, K, tile=0, transposed=False):
     dy, w = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05))
     old = G._FORCE_TILE
     G._FORCE_TILE = str(tile)
     try:
-        dx = G.linear_dgrad(dy, w)
+        dx = G.linear_dgrad(dy, w, wt=w.t().contiguous() if transposed else None)
     finally:
         G._FORCE_TILE = old
-    return (f"gemm_dgrad M{M} N{N} K{K} t{tile}", rel_err(dx, dy.float() @ w.float()), 2e-2)
+    return (f"gemm_dgrad M{M} N{N} K{K} t{tile} wt{int(transposed)}", rel_err(dx, dy.float() @ w.float()), 2e-2)
 
 
-def check_gemm_dgelu(M, N, K):
+def check_gemm_dgelu(M, N, K, transposed=False):
     dy, w, u = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05)), bf(rnd(M, K))
-    dx = G.linear_dgrad(dy, w, dgelu_aux=u)
+    dx = G.linear_dgrad(dy, w, dgelu_aux=u, wt=w.t().contiguous() if transposed else None)
     uf = u.float().requires_grad_(True)
     g = torch.autograd.grad(F.gelu(uf), uf, torch.ones_like(uf))[0]
     ref = (dy.float() @ w.float()) * g
@@ -255,15 +255,17 @@ def check_vit_fused_vs_reference(B=4, train=False):
 
 def all_checks() -> List[Callable]:
     c = []
-    for tile in (0, 1, 2):
+    for tile in (0, 6):
         c.append(lambda t=tile: check_gemm_fwd(50432 // 16, 768, 768, t))
         c.append(lambda t=tile: check_gemm_fwd(197 * 3, 2304, 768, t, True, True))
         c.append(lambda t=tile: check_gemm_gelu(197 * 2, 3072, 768, t))
         c.append(lambda t=tile: check_gemm_dgrad(197 * 2, 3072, 768, t))
+        c.append(lambda t=tile: check_gemm_dgrad(197 * 3, 768, 2304, t, True))
         c.append(lambda t=tile: check_gemm_wgrad(197 * 5, 768, 3072, t))
     c += [
         lambda: check_gemm_fwd(100, 64, 128, 0, True, True),
         lambda: check_gemm_dgelu(394, 768, 3072),
+        lambda: check_gemm_dgelu(4096, 768, 3072, True),
         lambda: check_gemm_wgrad(17, 64, 128),
         lambda: check_gemm_dropout(),
         lambda: check_layernorm(394, 768),
