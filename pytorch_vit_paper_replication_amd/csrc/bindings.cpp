@@ -21,6 +21,7 @@ struct GemmParams {
   int epi;
   int tile_cfg;
   uint64_t* dbg;
+  float* colsum;
 };
 struct AdamGroup {
   float lr, beta1, beta2, eps, weight_decay;
@@ -32,7 +33,7 @@ struct AdamGroup {
 extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
-hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, hipStream_t);
+hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
@@ -88,8 +89,9 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
           int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> addend,
           int64_t addend_period, c10::optional<torch::Tensor> aux, int64_t row_group, int64_t row_stride_group,
           int64_t row_offset, c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, int64_t k_split,
-          int64_t tile_cfg, c10::optional<torch::Tensor> dbg) {
+          int64_t tile_cfg, c10::optional<torch::Tensor> dbg, c10::optional<torch::Tensor> colsum) {
   pvr::GemmParams p{};
+  if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
   if (dbg.has_value() && dbg->defined()) p.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr());
   p.drop_scale = 1.f;
   p.M = (int)M; p.N = (int)N; p.K = (int)K;
@@ -147,11 +149,12 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor w, torch
 
 void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t x_stride, torch::Tensor mean, torch::Tensor rstd,
                    torch::Tensor w, c10::optional<torch::Tensor> dres, int64_t dres_stride, torch::Tensor dx, int64_t dx_stride,
-                   c10::optional<torch::Tensor> dw, c10::optional<torch::Tensor> db, int64_t rows) {
+                   c10::optional<torch::Tensor> dw, c10::optional<torch::Tensor> db, int64_t rows,
+                   c10::optional<torch::Tensor> dsum) {
   const int64_t D = w.numel();
   check(pvr_layernorm_bwd(bf(dy, "dy"), dy_stride, bf(x, "x"), x_stride, f32(mean, "mean"), f32(rstd, "rstd"), f32(w, "w"),
                           opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
-                          opt_ptr<float>(db), (int)rows, (int)D, stream()),
+                          opt_ptr<float>(db), opt_ptr<float>(dsum), (int)rows, (int)D, stream()),
         "layernorm_bwd");
 }
 
@@ -296,9 +299,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),
         py::arg("addend_period"), py::arg("aux"), py::arg("row_group"), py::arg("row_stride_group"),
         py::arg("row_offset"), py::arg("seed"), py::arg("seed_offset"), py::arg("drop_p"), py::arg("k_split"),
-        py::arg("tile_cfg"), py::arg("dbg") = py::none());
+        py::arg("tile_cfg"), py::arg("dbg") = py::none(), py::arg("colsum") = py::none());
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("dy_stride"), py::arg("x"), py::arg("x_stride"),
+        py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),
+        py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none());
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("transpose_batched", &transpose_batched);
   m.def("colsum", &colsum);

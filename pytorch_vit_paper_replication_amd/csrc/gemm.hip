@@ -24,8 +24,8 @@ namespace pvr {
 
 enum GemmEpi : int {
   EPI_BF16 = 0,        // out = resid + dropout(acc + bias + addend[row])      (bf16)
-  EPI_GELU = 1,        // aux = acc + bias (pre-act, bf16); out = dropout(gelu(aux))
-  EPI_DGELU = 2,       // out = acc * dropmask * gelu'(aux)                       (bf16)
+  EPI_GELU = 1,        // u = acc + bias; out = dropout(gelu(u)); aux = mask * scale * gelu'(u)
+  EPI_DGELU = 2,       // out = acc * aux   (aux as saved by EPI_GELU)            (bf16)
   EPI_F32_ATOMIC = 3,  // out += acc                                             (f32 atomics)
   EPI_F32_STORE = 4,   // out = acc                                              (f32)
 };
@@ -45,6 +45,7 @@ struct GemmParams {
   int epi;
   int tile_cfg;
   uint64_t* dbg;  // diagnostic s_memtime stamps [block][4] (null in normal runs)
+  float* colsum;  // optional: += column sums of the bf16-type output (a fused bias gradient)
 };
 
 namespace {
@@ -162,6 +163,9 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
         if (p.bias && n < p.N) bias[j] = *(const float4*)(p.bias + n);
       }
     }
+    float csum[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) csum[j][0] = csum[j][1] = csum[j][2] = csum[j][3] = 0.f;
     RowIn<FN, EPI> cur, nxt;
     load_row<FN, EPI>(p, mb + li, out_row(p, mb + li), nb, g, cur);
 #pragma unroll
@@ -176,7 +180,7 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
           if (n >= p.N) continue;
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           bool keep[4] = {true, true, true, true};
-          if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU) {
+          if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
             if (p.drop_thr) {
               const uint64_t idx = (uint64_t)orow * p.N + n;
               rng_keep2(seed, idx, p.drop_thr, keep[0], keep[1]);
@@ -202,20 +206,27 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
             uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
             *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
           } else if constexpr (EPI == EPI_GELU) {
-            uint2 u; u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]);
-            *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = u;
+            // h = dropout(gelu(u)); aux = dropout-mask * scale * gelu'(u): the backward's whole
+            // elementwise chain, computed while erf(u) is at hand (one exp more, no recompute later).
+            float gp[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float h = gelu_erf(v[r]);
-              v[r] = keep[r] ? h * p.drop_scale : 0.f;
+              const float u = v[r];
+              const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
+              const float pdf = 0.39894228040143268f * __expf(-0.5f * u * u);
+              const float sc = keep[r] ? p.drop_scale : 0.f;
+              v[r] = u * cdf * sc;
+              gp[r] = (cdf + u * pdf) * sc;
             }
+            uint2 a; a.x = pack2bf(gp[0], gp[1]); a.y = pack2bf(gp[2], gp[3]);
+            *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = a;
             uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
             *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
           } else if constexpr (EPI == EPI_DGELU) {
-            const uint2 uu = cur.r[j];
-            const float u[4] = {bf2f(uu.x & 0xFFFF), bf2f(uu.x >> 16), bf2f(uu.y & 0xFFFF), bf2f(uu.y >> 16)};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = keep[r] ? v[r] * p.drop_scale * gelu_erf_grad(u[r]) : 0.f;
+            const uint2 gg = cur.r[j];  // mask * scale * gelu'(u) saved by the forward epilogue
+            v[0] *= bf2f(gg.x & 0xFFFF); v[1] *= bf2f(gg.x >> 16);
+            v[2] *= bf2f(gg.y & 0xFFFF); v[3] *= bf2f(gg.y >> 16);
+            csum[j][0] += v[0]; csum[j][1] += v[1]; csum[j][2] += v[2]; csum[j][3] += v[3];
             uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
             *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
           } else if constexpr (EPI == EPI_F32_STORE) {
@@ -227,6 +238,31 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
         }
       }
       cur = nxt;
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      if (p.colsum) {
+        // reduce over the 16 rows held by lanes li = 0..15 of each 16-lane group, one atomic per column
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float c = csum[j][r];
+            c += __shfl_xor(c, 1, 64);
+            c += __shfl_xor(c, 2, 64);
+            c += __shfl_xor(c, 4, 64);
+            c += __shfl_xor(c, 8, 64);
+            csum[j][r] = c;
+          }
+        if (li == 0) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int n = nb + 16 * j + 4 * g;
+            if (n < p.N)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) atomicAdd(p.colsum + n + r, csum[j][r]);
+          }
+        }
+      }
     }
   } else {
     // lane holds C[m = mb + 16i + 4g + r][n = nb + 16j + li]; f32 outputs (64-B row segments per instruction)

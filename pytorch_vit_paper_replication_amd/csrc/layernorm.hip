@@ -94,15 +94,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       const float* __restrict__ w,
                                                       const uint16_t* __restrict__ dres, int64_t dres_stride,
                                                       uint16_t* __restrict__ dx, int64_t dx_stride,
-                                                      float* __restrict__ dw, float* __restrict__ db, int rows, int D) {
-  __shared__ float red[4][2][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];
+                                                      float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dsum,
+                                                      int rows, int D) {
+  __shared__ float red[4][3][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = D >> 3;
-  float gw[MAXCH][8], gb[MAXCH][8];
+  float gw[MAXCH][8], gb[MAXCH][8], gs[MAXCH][8];
 #pragma unroll
   for (int i = 0; i < MAXCH; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gw[i][j] = gb[i][j] = 0.f;
+    for (int j = 0; j < 8; ++j) gw[i][j] = gb[i][j] = gs[i][j] = 0.f;
 
   for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
@@ -142,6 +143,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += r[j];
         }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gs[i][j] += o[j];  // column sums of dx (a fused bias gradient)
         uint4 q;
         q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
         q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
@@ -158,6 +161,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
       for (int j = 0; j < 8; ++j) {
         red[wave][0][c * 8 + j] = gw[i][j];
         red[wave][1][c * 8 + j] = gb[i][j];
+        red[wave][2][c * 8 + j] = gs[i][j];
       }
     }
   }
@@ -167,6 +171,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
     const float bsum = red[0][1][col] + red[1][1][col] + red[2][1][col] + red[3][1][col];
     if (dw) atomicAdd(dw + col, a);
     if (db) atomicAdd(db + col, bsum);
+    if (dsum) atomicAdd(dsum + col, red[0][2][col] + red[1][2][col] + red[2][2][col] + red[3][2][col]);
   }
 }
 
@@ -193,7 +198,7 @@ extern "C" hipError_t pvr_layernorm_fwd(const uint16_t* x, int64_t x_stride, con
 extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, const uint16_t* x, int64_t x_stride,
                                         const float* mean, const float* rstd, const float* w, const uint16_t* dres,
                                         int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
-                                        int rows, int D, hipStream_t s) {
+                                        float* dsum, int rows, int D, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280) return hipErrorInvalidValue;
@@ -202,9 +207,9 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   const dim3 grid(nblk), block(256);
   const int maxch = (D / 8 + 63) / 64;
   switch (maxch) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, rows, D); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, rows, D); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, rows, D); break;
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, rows, D); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, rows, D); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, rows, D); break;
   }
   return hipGetLastError();
 }

@@ -98,7 +98,7 @@ class EncoderBlockFn(torch.autograd.Function):
         o, lse = ext.attn_fwd(qkv, B, N, H, scale)
         x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=x)
         xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
-        u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)
+        u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
         h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=drop1)
         x2 = gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=drop2)
         ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
@@ -122,22 +122,20 @@ class EncoderBlockFn(torch.autograd.Function):
             dz2 = dx2
             if b2.requires_grad:
                 gemm.bias_grad(dx2, g(b2))
-        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, drop=drop1, wt=store.bf16_t(w2))
+        # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
+        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=g(b1))
         gw2 = g(w2)
         if gw2 is not None:
             gemm.linear_wgrad(dz2, h, gw2)
         gw1 = g(w1)
         if gw1 is not None:
             gemm.linear_wgrad(du, xn2, gw1)
-        if b1.requires_grad:
-            gemm.bias_grad(du, g(b1))
         dxn2 = gemm.linear_dgrad(du, store.bf16(w1), wt=store.bf16_t(w1))
         dx1 = torch.empty_like(dx2)
-        ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T)
+        # dx1 = dx2 + LN2'(dxn2); d(bo) = colsum(dx1) reduced in the same kernel
+        ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T, dsum=g(bo))
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
-        if bo.requires_grad:
-            gemm.bias_grad(dx1, g(bo))
         do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
         gwo = g(wo)
         if gwo is not None:

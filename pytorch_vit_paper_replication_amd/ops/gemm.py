@@ -44,7 +44,10 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
                resid: Optional[torch.Tensor] = None, drop: Drop = None, gelu_aux: Optional[torch.Tensor] = None,
                addend: Optional[torch.Tensor] = None, addend_period: int = 0,
                row_remap: Tuple[int, int, int] = (0, 0, 0), out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = resid + dropout(x.w^T + bias + addend[row % period])  (or the GELU variant with aux)."""
+    """y = resid + dropout(x.w^T + bias + addend[row % period]).
+
+    GELU variant (``gelu_aux`` given): u = x.w^T + bias, y = dropout(gelu(u)) and gelu_aux receives
+    mask * scale * gelu'(u) — exactly the factor ``linear_dgrad(..., dgelu_aux=)`` multiplies by."""
     T, K = x.shape
     N = w.shape[0]
     if out is None:
@@ -57,22 +60,25 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch.Tensor] = None,
-                 drop: Drop = None, out: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 drop: Drop = None, out: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
+                 colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy . w ; optionally fused with the GELU + dropout backward of the producing layer:
-    dx = (dy . w) * mask * gelu'(aux). With ``wt`` (= w^T, [K, N] bf16) the weight operand is
+    dx = (dy . w) * dgelu_aux (the factor saved by the GELU forward epilogue). With ``wt`` (= w^T, [K, N] bf16) the weight operand is
     k-contiguous and the fast forward-layout kernel runs; otherwise w is read with transposed LDS reads."""
     T, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(T, K, dtype=torch.bfloat16, device=dy.device)
-    seed, soff, p = _drop_args(drop)
+    seed, soff, p = None, 0, 0.0  # the mask is already folded into dgelu_aux
     epi = EPI_DGELU if dgelu_aux is not None else EPI_BF16
+    if colsum is not None and dgelu_aux is None:
+        raise ValueError("colsum is fused only into the GELU-backward epilogue")
     if wt is not None and N % 64 == 0:
         _ext.ext().gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-                        seed, soff, p, 0, _tile(T, K, N, "dgrad_t"))
+                        seed, soff, p, 0, _tile(T, K, N, "dgrad_t"), colsum=colsum)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-                        seed, soff, p, 0, _tile(T, K, N, "dgrad"))
+                        seed, soff, p, 0, _tile(T, K, N, "dgrad"), colsum=colsum)
     return out
 
 

@@ -65,9 +65,10 @@ def check_gemm_gelu(M, N, K, tile=0):
         h = G.linear_fwd(x, w, b, gelu_aux=u)
     finally:
         G._FORCE_TILE = old
-    uref = x.float() @ w.float().t() + b
-    e1 = rel_err(u, uref)
-    e2 = rel_err(h, F.gelu(uref))
+    uref = (x.float() @ w.float().t() + b).requires_grad_(True)
+    gp = torch.autograd.grad(F.gelu(uref), uref, torch.ones_like(uref))[0]
+    e1 = rel_err(u, gp)
+    e2 = rel_err(h, F.gelu(uref.detach()))
     return (f"gemm_gelu M{M} N{N} K{K} t{tile}", max(e1, e2), 2e-2)
 
 
@@ -83,11 +84,9 @@ def check_gemm_dgrad(M, N, K, tile=0, transposed=False):
 
 
 def check_gemm_dgelu(M, N, K, transposed=False):
-    dy, w, u = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05)), bf(rnd(M, K))
-    dx = G.linear_dgrad(dy, w, dgelu_aux=u, wt=w.t().contiguous() if transposed else None)
-    uf = u.float().requires_grad_(True)
-    g = torch.autograd.grad(F.gelu(uf), uf, torch.ones_like(uf))[0]
-    ref = (dy.float() @ w.float()) * g
+    dy, w, g = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05)), bf(rnd(M, K))
+    dx = G.linear_dgrad(dy, w, dgelu_aux=g, wt=w.t().contiguous() if transposed else None)
+    ref = (dy.float() @ w.float()) * g.float()
     return (f"gemm_dgelu M{M} N{N} K{K}", rel_err(dx, ref), 2e-2)
 
 
