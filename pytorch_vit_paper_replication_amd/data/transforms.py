@@ -60,6 +60,8 @@ class Resize:
             x = img.unsqueeze(0) if img.dim() == 3 else img
             out = torch.nn.functional.interpolate(x.float(), size=(th, tw), mode="bilinear", align_corners=False,
                                                   antialias=True)
+            if img.dtype == torch.uint8:  # like torchvision: integer images stay integer
+                out = out.round_().clamp_(0, 255).to(torch.uint8)
             return out.squeeze(0) if img.dim() == 3 else out
         tw, th = self._target(*img.size)
         return img.resize((tw, th), self.interpolation)

@@ -116,9 +116,12 @@ class FusedAdam(torch.optim.Optimizer):
 
     # ------------------------------------------------------------------ public
     def zero_grad(self, set_to_none: bool = True):
-        fz = self._setup_fused()
-        if fz is not None:
-            fz[0].zero_grad()  # one memset, gradient views stay attached
+        from ..runtime.param_store import lookup_store
+
+        params = self._all_params()
+        st = lookup_store(params[0]) if params else None
+        if st is not None and all(lookup_store(p) is st for p in params):
+            st.zero_grad()  # one memset, gradient views (= DDP buckets) stay attached
             return
         super().zero_grad(set_to_none=set_to_none)
 

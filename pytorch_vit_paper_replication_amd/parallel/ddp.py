@@ -92,7 +92,7 @@ class DistributedDataParallel(nn.Module):
         store.add_listener(self._on_ready)
         for p in store.params:
             if p.requires_grad:
-                self._hooks.append(p.register_post_accumulate_grad_hook(lambda t: self._on_ready([t])))
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._autograd_hook))
         return store
 
     def _reset(self):
@@ -122,6 +122,12 @@ class DistributedDataParallel(nn.Module):
             self.require_backward_grad_sync = old
 
     # ------------------------------------------------------------------ backward hooks
+    def _autograd_hook(self, p):
+        # PyTorch-path gradient: if autograd allocated it (zero_grad(set_to_none) after forward, as the
+        # reference engine does), adopt it into the bucket view first.
+        self._store.adopt_grad(p)
+        self._on_ready([p])
+
     def _on_ready(self, params):
         if not self.require_backward_grad_sync or self._store is None:
             return

@@ -199,6 +199,17 @@ class ParamStore:
             p.grad = gv
         return gv
 
+    def adopt_grad(self, p: torch.nn.Parameter) -> None:
+        """Move a gradient autograd allocated outside the flat buffer into its view (DDP hook path)."""
+        i = self._index.get(id(p))
+        if i is None or p.grad is None:
+            return
+        gv = self._gviews[i]
+        if p.grad.data_ptr() != gv.data_ptr():
+            with torch.no_grad():
+                gv.copy_(p.grad)
+            p.grad = gv
+
     def zero_grad(self) -> None:
         self.grad_flat.zero_()
         for i, p in enumerate(self.params):

@@ -1,0 +1,160 @@
+"""Engine / data / utils conformance with the reference going_modular API."""
+import inspect
+import re
+
+import pytest
+import torch
+from PIL import Image
+from torch import nn
+from torch.utils.data import DataLoader, TensorDataset
+
+from going_modular import data_setup, engine, utils
+from going_modular.going_modular import engine as engine2
+from pytorch_vit_paper_replication_amd.data import transforms as T
+
+
+class Tiny(nn.Module):
+    def __init__(self, n=3):
+        super().__init__()
+        self.l = nn.Linear(4, n)
+
+    def forward(self, x):
+        return self.l(x)
+
+
+def _loader(n, bs):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(n, 4, generator=g)
+    y = torch.randint(0, 3, (n,), generator=g)
+    return DataLoader(TensorDataset(x, y), batch_size=bs, shuffle=False)
+
+
+def test_signatures_match_reference():
+    assert list(inspect.signature(engine.train).parameters)[:8] == [
+        "model", "train_dataloader", "test_dataloader", "optimizer", "loss_fn", "lr_scheduler", "epochs", "device"]
+    assert list(inspect.signature(engine.train_step).parameters)[:6] == [
+        "model", "dataloader", "loss_fn", "optimizer", "lr_scheduler", "device"]
+    assert list(inspect.signature(engine.test_step).parameters)[:4] == ["model", "dataloader", "loss_fn", "device"]
+    assert engine2.train is engine.train
+
+
+def test_train_returns_dict_prints_format_and_steps_scheduler(capsys):
+    torch.manual_seed(0)
+    m = Tiny()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    sched = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.5, total_iters=100)
+    res = engine.train(m, _loader(10, 4), _loader(6, 4), opt, nn.CrossEntropyLoss(), sched, epochs=2, device="cpu")
+    assert set(res) == {"train_loss", "train_acc", "test_loss", "test_acc"}
+    assert all(len(v) == 2 for v in res.values())
+    out = capsys.readouterr().out
+    lines = [l for l in out.splitlines() if l.startswith("Epoch:")]
+    assert len(lines) == 2
+    assert re.fullmatch(r"Epoch: 1 \| train_loss: \d+\.\d{4} \| train_acc: \d+\.\d{4} \| test_loss: \d+\.\d{4} \| "
+                        r"test_acc: \d+\.\d{4}", lines[0])
+    assert sched.last_epoch == 2 * 3  # stepped once per batch (3 batches of 4/4/2)
+
+
+def test_metrics_are_mean_of_per_batch_means():
+    """3 batches of 4/4/2: accuracy is the mean of three per-batch accuracies (GM/engine.py:77-78)."""
+    torch.manual_seed(0)
+    m = Tiny()
+    dl = _loader(10, 4)
+    loss, acc = engine.test_step(m, dl, nn.CrossEntropyLoss(), "cpu")
+    accs, losses = [], []
+    with torch.no_grad():
+        for x, y in dl:
+            p = m(x)
+            losses.append(nn.functional.cross_entropy(p, y).item())
+            accs.append((p.argmax(1) == y).float().mean().item())
+    assert acc == pytest.approx(sum(accs) / 3, abs=1e-6)
+    assert loss == pytest.approx(sum(losses) / 3, abs=1e-6)
+
+
+def test_clip_applied_before_step():
+    m = Tiny()
+    seen = {}
+
+    class Spy(torch.optim.SGD):
+        def step(self, closure=None):
+            seen["norm"] = torch.nn.utils.get_total_norm([p.grad for p in m.parameters()]).item()
+            return super().step(closure)
+
+    opt = Spy(m.parameters(), lr=0.0)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: 1.0)
+    x = torch.randn(8, 4) * 100
+    y = torch.randint(0, 3, (8,))
+    engine.train_step(m, [(x, y)], nn.CrossEntropyLoss(), opt, sched, "cpu")
+    assert seen["norm"] <= 1.0 + 1e-5
+
+
+def _make_folder(root, classes=("steak", "pizza", "sushi"), n=3, size=20):
+    for c in classes:
+        d = root / c
+        d.mkdir(parents=True)
+        for i in range(n):
+            Image.new("RGB", (size + i, size), color=(i * 40, 100, 200)).save(d / f"{i}.jpg")
+
+
+def test_create_dataloaders_sorted_classes(tmp_path):
+    _make_folder(tmp_path / "train")
+    _make_folder(tmp_path / "test", n=2)
+    tf = T.Compose([T.Resize((32, 32)), T.ToTensor()])
+    tr, te, names = data_setup.create_dataloaders(str(tmp_path / "train"), str(tmp_path / "test"), tf, batch_size=4,
+                                                  num_workers=0)
+    assert names == ["pizza", "steak", "sushi"]
+    x, y = next(iter(tr))
+    assert x.shape == (4, 3, 32, 32) and x.dtype == torch.float32 and 0 <= x.min() and x.max() <= 1
+    assert len(tr.dataset) == 9 and len(te.dataset) == 6
+
+
+def test_v2_style_transform_matches_reference_pipeline():
+    img = Image.new("RGB", (50, 40), color=(255, 0, 128))
+    t = T.v2.Compose([T.v2.ToImage(), T.v2.Resize((224, 224)), T.v2.ToDtype(torch.float32, scale=True)])
+    x = t(img)
+    assert x.shape == (3, 224, 224)
+    assert torch.allclose(x[:, 100, 100], torch.tensor([1.0, 0.0, 128 / 255]), atol=1e-3)
+
+
+def test_save_model_contract(tmp_path, capsys):
+    m = Tiny()
+    with pytest.raises(AssertionError, match="model_name should end with '.pt' or '.pth'"):
+        utils.save_model(m, str(tmp_path), "bad.bin")
+    p = utils.save_model(m, str(tmp_path / "a" / "b"), "m.pth")
+    assert "[INFO] Saving model to:" in capsys.readouterr().out
+    sd = torch.load(p, weights_only=True)
+    m2 = Tiny()
+    m2.load_state_dict(sd)
+    assert torch.equal(m2.l.weight, m.l.weight)
+
+
+def test_checkpoint_resume_roundtrip(tmp_path):
+    torch.manual_seed(1)
+    m = Tiny()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    sched = torch.optim.lr_scheduler.StepLR(opt, 1, gamma=0.5)
+    engine.train_step(m, _loader(8, 4), nn.CrossEntropyLoss(), opt, sched, "cpu")
+    utils.save_checkpoint(str(tmp_path), m, opt, sched, epoch=3, results={"train_loss": [1.0]})
+    m2 = Tiny()
+    opt2 = torch.optim.Adam(m2.parameters(), lr=1e-2)
+    sched2 = torch.optim.lr_scheduler.StepLR(opt2, 1, gamma=0.5)
+    info = utils.load_checkpoint(str(tmp_path / "checkpoint.pt"), m2, opt2, sched2)
+    assert info["epoch"] == 3 and info["results"]["train_loss"] == [1.0]
+    assert torch.equal(m2.l.weight, m.l.weight)
+    assert sched2.last_epoch == sched.last_epoch
+    assert opt2.param_groups[0]["lr"] == opt.param_groups[0]["lr"]
+
+
+def test_vit_trains_end_to_end_on_cpu():
+    """BASELINE.json config 1 (plumbing): a tiny ViT through engine.train on CPU, loss decreases."""
+    from pytorch_vit_paper_replication_amd.data import create_synthetic_dataloaders
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
+
+    torch.manual_seed(0)
+    tr, te, names = create_synthetic_dataloaders(batch_size=2, train_len=8, test_len=4, image_size=32, num_classes=3)
+    m = ViT(image_size=32, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=32, mlp_size=64,
+            num_classes=3, mlp_dropout=0.0, embedding_dropout=0.0)
+    opt = FusedAdam(param_groups_weight_decay(m, 0.03), lr=3e-3)
+    sched = warmup_linear_decay(opt, 8 * len(tr))
+    res = engine.train(m, tr, te, opt, nn.CrossEntropyLoss(), sched, epochs=8, device="cpu")
+    assert res["train_loss"][-1] < res["train_loss"][0]
