@@ -53,7 +53,7 @@ def _worker(rank, world, port, out_dir, bucket_mb):
 def test_ddp_grads_match_single_process(tmp_path, bucket_mb):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), bucket_mb), nprocs=world, join=True)
-    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=False) for i in range(world)]
+    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
     if bucket_mb < 1:
         assert r[0]["nbuckets"] > 5
     for k in r[0]["state"]:
@@ -92,6 +92,6 @@ def _engine_worker(rank, world, port, out_dir):
 def test_engine_under_ddp_consistent_across_ranks(tmp_path):
     world = 2
     mp.spawn(_engine_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    a, b = (torch.load(tmp_path / f"e{i}.pt", weights_only=False) for i in range(world))
+    a, b = (torch.load(tmp_path / f"e{i}.pt", weights_only=True) for i in range(world))
     assert a["res"] == b["res"]
     assert torch.equal(a["w"], b["w"]), "replicas diverged"
