@@ -117,7 +117,9 @@ def main():
     seq = (args.image_size // int(model.config["patch_size"])) ** 2 + 1
     if rank == 0:
         out = {
-            "metric": "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X",
+            "metric": ("images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
+                       if (name, args.image_size) == ("ViT-B/16", 224)
+                       else f"images/sec (whole node) {name} {args.image_size}px bf16"),
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,

@@ -1,8 +1,12 @@
-// Multi-head self-attention forward/backward for ViT (no mask, head_dim 64), gfx950.
+// Multi-head self-attention forward/backward for ViT (no mask, head_dim 64/80/96/128), gfx950.
 //
 // Replaces nn.MultiheadAttention's scaled_dot_product_attention core (reference models/vit.py:86-97;
 // SURVEY.md K7). Q, K and V are read in place from the fused QKV GEMM output [tokens][3*D]
-// (row = token, head h at columns h*64, D + h*64, 2D + h*64), so there are no head transposes.
+// (row = token, head h at columns h*dh, D + h*dh, 2D + h*dh), so there are no head transposes.
+// A head row is staged in LDS as ceil(dh/64) "half" images of 128-B rows (the swizzle below works
+// on 8 chunks); for dh = 80 (ViT-H/14) the MFMA k-steps over dh run to 96 with the Q / K / V
+// register fragments zeroed past dh, so the finite neighbour data staged in the LDS tail of a row
+// never contributes.
 //
 // Forward: one workgroup = 4 waves = 64 queries of one (batch, head); each wave owns 16 queries
 // and computes S^T = K . Q^T so that the query sits on the MFMA lane: the softmax row reduction
@@ -21,7 +25,13 @@
 namespace pvr {
 namespace {
 
-constexpr int DH = 64;
+template <int DH>
+struct Hd {
+  static_assert(DH % 16 == 0 && DH <= 128, "head dim must be a multiple of 16, at most 128");
+  static constexpr int NH = (DH + 63) / 64;  // 128-B row images per head row
+  static constexpr int KS = (DH + 31) / 32;  // MFMA k-steps over the head dim
+  static constexpr int NE = DH / 16;         // 16-wide output fragments over the head dim
+};
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -29,32 +39,47 @@ constexpr float LN2 = 0.6931471805599453f;
 // one chunk), and for transposed reads of rows {4g+q, 16+4g+q} and {8g+q, 8g+4+q}.
 PVR_DEV int swz_a(int r) { return (((r >> 1) & 1) << 1) ^ (((r >> 2) & 1) << 2) ^ (((r >> 3) & 1) * 5); }
 
-PVR_DEV int lds_off(int row, int chunk) { return row * 128 + ((chunk ^ swz_a(row)) << 4); }
+// Byte offset of 16-B chunk `chunk` (0 .. 8*NH-1) of row `row` in an image of `rows` rows: the head
+// row is split into 64-dim halves, each its own [rows][128 B] swizzled image.
+PVR_DEV int lds_off(int rows, int row, int chunk) {
+  return (chunk >> 3) * rows * 128 + row * 128 + (((chunk & 7) ^ swz_a(row)) << 4);
+}
 
-// DMA `rows` rows (multiple of 8) of a [row][64] bf16 operand into a swizzled 128-B-row LDS image.
-// Row r of the image comes from element offset (r * ld) of the buffer resource.
+// DMA `rows` rows (multiple of 8) of a [row][NH*64] bf16 operand into NH swizzled 128-B-row images.
+// Row r of the image comes from element offset (r * ld) of the buffer resource; bytes past the
+// resource's extent (last row's tail past dh) read as zero.
+template <int NH>
 PVR_DEV void dma_rows(__amdgpu_buffer_rsrc_t rs, char* lds, int rows, int64_t ld, int row_base, int wave, int nwaves, int lane) {
-  for (int s = wave; s < rows / 8; s += nwaves) {
-    const int row = s * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ swz_a(row);
-    const uint32_t voff = (uint32_t)((int64_t)(row_base + row) * ld * 2 + c * 16);
-    dma16(rs, to_lds(lds + s * 1024), voff);
-  }
+#pragma unroll
+  for (int hh = 0; hh < NH; ++hh)
+    for (int s = wave; s < rows / 8; s += nwaves) {
+      const int row = s * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ swz_a(row);
+      const uint32_t voff = (uint32_t)((int64_t)(row_base + row) * ld * 2 + hh * 128 + c * 16);
+      dma16(rs, to_lds(lds + hh * rows * 128 + s * 1024), voff);
+    }
 }
 
 // 16x32 operand fragment from a swizzled image, rows r0 + (l&15), k = 32ks + 8(l>>4) + j.
-PVR_DEV v8s frag_rows(const char* img, int r0, int ks, int lane) {
-  return ds_read_b128(img + lds_off(r0 + (lane & 15), ks * 4 + (lane >> 4)));
+PVR_DEV v8s frag_rows(const char* img, int rows, int r0, int ks, int lane) {
+  return ds_read_b128(img + lds_off(rows, r0 + (lane & 15), ks * 4 + (lane >> 4)));
 }
 
 // Transposed fragment: lane i (of group g) gets img[row_of(g, j)][c0 + i] for j = 0..7 where rows are
 // rowA + q (j = q) and rowB + q (j = 4 + q); cols c0..c0+15 (c0 multiple of 16).
-PVR_DEV v8s frag_tr(const char* img, int rowA, int rowB, int c0, int lane) {
+PVR_DEV v8s frag_tr(const char* img, int rows, int rowA, int rowB, int c0, int lane) {
   const int q = (lane >> 2) & 3, p = lane & 3;
   const int chunk = (c0 >> 3) + (p >> 1);
-  const v4s lo = ds_read_tr(img + lds_off(rowA + q, chunk) + 8 * (p & 1));
-  const v4s hi = ds_read_tr(img + lds_off(rowB + q, chunk) + 8 * (p & 1));
+  const v4s lo = ds_read_tr(img + lds_off(rows, rowA + q, chunk) + 8 * (p & 1));
+  const v4s hi = ds_read_tr(img + lds_off(rows, rowB + q, chunk) + 8 * (p & 1));
   return cat44(lo, hi);
+}
+
+// Global 8-element fragment at head-dim offset d0, zero past the head dim.
+template <int DH>
+PVR_DEV v8s load_frag(const uint16_t* p, int d0) {
+  if (d0 >= DH) return v8s{0, 0, 0, 0, 0, 0, 0, 0};
+  return *(const v8s*)(p + d0);
 }
 
 PVR_DEV v8s pack_p(const v4f& a, const v4f& b) {
@@ -71,10 +96,12 @@ PVR_DEV v8s pack_p(const v4f& a, const v4f& b) {
 PVR_DEV uint32_t clamp_bytes(int64_t b) { return b < 0 ? 0u : (b > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)b); }
 
 // ----------------------------------------------------------------------------------- forward
+template <int DH>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
                                                         int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale) {
-  constexpr int KT = 64;                       // keys per tile
-  constexpr int TILE_BYTES = KT * DH * 2;      // 8 KiB
+  using C = Hd<DH>;
+  constexpr int KT = 64;                         // keys per tile
+  constexpr int TILE_BYTES = KT * 128 * C::NH;   // one K or V tile image (8 or 16 KiB)
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [stage][K|V]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -88,22 +115,22 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   const __amdgpu_buffer_rsrc_t vrs = make_rsrc(base + 2 * D + h * DH, clamp_bytes(extent));
 
   // Q fragments (B operand): lane holds Q[q0 + li][32ks + 8g + j]
-  v8s qf[2];
+  v8s qf[C::KS];
   {
     const int q = min(q0 + li, N - 1);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[ks] = *(const v8s*)(base + (int64_t)q * ld + h * DH + ks * 32 + 8 * g);
+    for (int ks = 0; ks < C::KS; ++ks) qf[ks] = load_frag<DH>(base + (int64_t)q * ld + h * DH, ks * 32 + 8 * g);
   }
 
   const float c = scale * LOG2E;
   float m_run = -INFINITY, l_run = 0.f;
-  v4f o[4];
+  v4f o[C::NE];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < C::NE; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = (N + KT - 1) / KT;
-  dma_rows(krs, smem, KT, ld, 0, wave, 4, lane);
-  dma_rows(vrs, smem + TILE_BYTES, KT, ld, 0, wave, 4, lane);
+  dma_rows<C::NH>(krs, smem, KT, ld, 0, wave, 4, lane);
+  dma_rows<C::NH>(vrs, smem + TILE_BYTES, KT, ld, 0, wave, 4, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -112,8 +139,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     const char* vimg = kimg + TILE_BYTES;
     if (t + 1 < ntiles) {
       char* nk = smem + ((t + 1) & 1) * 2 * TILE_BYTES;
-      dma_rows(krs, nk, KT, ld, (t + 1) * KT, wave, 4, lane);
-      dma_rows(vrs, nk + TILE_BYTES, KT, ld, (t + 1) * KT, wave, 4, lane);
+      dma_rows<C::NH>(krs, nk, KT, ld, (t + 1) * KT, wave, 4, lane);
+      dma_rows<C::NH>(vrs, nk + TILE_BYTES, KT, ld, (t + 1) * KT, wave, 4, lane);
     }
     // S^T[key][q] for 4 key fragments
     v4f s[4];
@@ -121,7 +148,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     for (int f = 0; f < 4; ++f) {
       s[f] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) s[f] = mfma16(frag_rows(kimg, 16 * f, ks, lane), qf[ks], s[f]);
+      for (int ks = 0; ks < C::KS; ++ks) s[f] = mfma16(frag_rows(kimg, KT, 16 * f, ks, lane), qf[ks], s[f]);
     }
     const int kbase = t * KT;
     float tmax = -INFINITY;
@@ -150,14 +177,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     l_run = l_run * alpha + psum;
     m_run = m_new;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] *= alpha;
+    for (int e = 0; e < C::NE; ++e) o[e] *= alpha;
     // O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const v8s vf = frag_tr(vimg, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane);
+      for (int e = 0; e < C::NE; ++e) {
+        const v8s vf = frag_tr(vimg, KT, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane);
         o[e] = mfma16(vf, pf, o[e]);
       }
     }
@@ -171,7 +198,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     const float inv = 1.f / l_run;
     uint16_t* orow = out + ((int64_t)b * N + q) * ld_o + h * DH;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < C::NE; ++e) {
       uint2 w;
       w.x = pack2bf(o[e][0] * inv, o[e][1] * inv);
       w.y = pack2bf(o[e][2] * inv, o[e][3] * inv);
@@ -182,7 +209,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
 }
 
 // ------------------------------------------------------------------------- backward: delta
-// delta[bh][q] = sum_d dO[q][h*64 + d] * O[q][h*64 + d]
+// delta[bh][q] = sum_d dO[q][h*dh + d] * O[q][h*dh + d]
+template <int DH>
 __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout, int64_t ld_do,
                                                               const uint16_t* __restrict__ o, int64_t ld_o,
                                                               float* __restrict__ delta, int B, int N, int H) {
@@ -207,12 +235,15 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __r
 
 // ------------------------------------------------------------------------- backward: main
 // grid (nkb, B*H), block NW*64 (NW in {1,2,4,8}); workgroup keys [kb*KB, kb*KB + KB), KB = 32*NW.
+template <int DH>
 __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                         const uint16_t* __restrict__ dout, int64_t ld_do,
                                                         const float* __restrict__ lse, const float* __restrict__ delta,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
                                                         int N, int H, int D, float scale) {
+  using C = Hd<DH>;
   constexpr int QB = 32;
+  constexpr int RB = 128 * C::NH;  // LDS bytes per staged head row
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int NW = blockDim.x >> 6;
   const int KB = NW * 32;
@@ -223,11 +254,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int kb0 = blockIdx.x * KB;
   const int kw0 = kb0 + wave * 32;
 
-  // LDS carve: K image [KB][64] | Q blk [32][64] | dO blk [32][64] | dS [32][KB] | lse2[32] | delta[32]
+  // LDS carve: K image [KB][dh] | Q blk [32][dh] | dO blk [32][dh] | dS [32][KB] | lse2[32] | delta[32]
   char* kimg = smem;
-  char* qimg = kimg + KB * 128;
-  char* doimg = qimg + QB * 128;
-  char* dsimg = doimg + QB * 128;
+  char* qimg = kimg + KB * RB;
+  char* doimg = qimg + QB * RB;
+  char* dsimg = doimg + QB * RB;
   float* s_lse = (float*)(dsimg + QB * KB * 2);
   float* s_del = s_lse + QB;
   const int ds_cpr = KB / 8;  // 16-B chunks per dS row (power of two)
@@ -240,27 +271,30 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const __amdgpu_buffer_rsrc_t dors = make_rsrc(dobase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2));
 
   // own keys' K and V fragments (B operands): lane holds X[kw0 + 16f + li][32ks + 8g + j]
-  v8s kf[2][2], vf[2][2];
+  v8s kf[2][C::KS], vf[2][C::KS];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     const int key = kw0 + 16 * f + li;
     const bool ok = key < N;
     const int kc = ok ? key : 0;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      v8s kk = *(const v8s*)(base + (int64_t)kc * ld + D + h * DH + ks * 32 + 8 * g);
-      v8s vv = *(const v8s*)(base + (int64_t)kc * ld + 2 * D + h * DH + ks * 32 + 8 * g);
+    for (int ks = 0; ks < C::KS; ++ks) {
+      v8s kk = load_frag<DH>(base + (int64_t)kc * ld + D + h * DH, ks * 32 + 8 * g);
+      v8s vv = load_frag<DH>(base + (int64_t)kc * ld + 2 * D + h * DH, ks * 32 + 8 * g);
       if (!ok) { kk = v8s{0, 0, 0, 0, 0, 0, 0, 0}; vv = kk; }
       kf[f][ks] = kk;
       vf[f][ks] = vv;
     }
   }
   // whole key block's K image for the dQ product
-  dma_rows(krs, kimg, KB, ld, kb0, wave, NW, lane);
+  dma_rows<C::NH>(krs, kimg, KB, ld, kb0, wave, NW, lane);
+  // waves whose 32 keys all lie past N skip the math; dQ only reduces over key slices with a valid key
+  const bool active = kw0 < N;
+  const int nks_dq = min(KB, N - kb0 + 31) / 32;
 
-  v4f dk[4][2], dv[4][2];
+  v4f dk[C::NE][2], dv[C::NE][2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int e = 0; e < C::NE; ++e)
 #pragma unroll
     for (int f = 0; f < 2; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
 
@@ -268,8 +302,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int nqb = (N + QB - 1) / QB;
   for (int qb = 0; qb < nqb; ++qb) {
     const int q0 = qb * QB;
-    dma_rows(qrs, qimg, QB, ld, q0, wave, NW, lane);
-    dma_rows(dors, doimg, QB, ld_do, q0, wave, NW, lane);
+    dma_rows<C::NH>(qrs, qimg, QB, ld, q0, wave, NW, lane);
+    dma_rows<C::NH>(dors, doimg, QB, ld_do, q0, wave, NW, lane);
     if (threadIdx.x < QB) {
       const int q = q0 + threadIdx.x;
       s_lse[threadIdx.x] = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
@@ -278,6 +312,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
+    if (active) {
     // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]
     v4f s[2][2], dp[2][2];
 #pragma unroll
@@ -285,11 +320,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int f = 0; f < 2; ++f) s[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < C::KS; ++ks) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        const v8s qa = frag_rows(qimg, 16 * a, ks, lane);
-        const v8s da = frag_rows(doimg, 16 * a, ks, lane);
+        const v8s qa = frag_rows(qimg, QB, 16 * a, ks, lane);
+        const v8s da = frag_rows(doimg, QB, 16 * a, ks, lane);
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           s[a][f] = mfma16(qa, kf[f][ks], s[a][f]);
@@ -317,9 +352,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       const v8s pf = pack_p(s[0][f], s[1][f]);
       const v8s sf = pack_p(dp[0][f], dp[1][f]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const v8s dot = frag_tr(doimg, 4 * g, 16 + 4 * g, 16 * e, lane);
-        const v8s qt = frag_tr(qimg, 4 * g, 16 + 4 * g, 16 * e, lane);
+      for (int e = 0; e < C::NE; ++e) {
+        const v8s dot = frag_tr(doimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane);
+        const v8s qt = frag_tr(qimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane);
         dv[e][f] = mfma16(dot, pf, dv[e][f]);
         dk[e][f] = mfma16(qt, sf, dk[e][f]);
       }
@@ -336,16 +371,17 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
           const int chunk = (kl >> 3) ^ (ql & (ds_cpr - 1) & 15);
           *(uint16_t*)(dsimg + ql * KB * 2 + chunk * 16 + (kl & 7) * 2) = f2bf(dp[a][f][r]);
         }
+    }  // active
     __syncthreads();
-    // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 8 output fragments split over the waves
-    for (int fr = wave; fr < 8; fr += NW) {
-      const int a = fr >> 2, e = fr & 3;
+    // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 2*NE output fragments split over the waves
+    for (int fr = wave; fr < 2 * C::NE; fr += NW) {
+      const int a = fr / C::NE, e = fr % C::NE;
       v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-      for (int ks = 0; ks < KB / 32; ++ks) {
+      for (int ks = 0; ks < nks_dq; ++ks) {
         const int ql = 16 * a + li;
         const int chunk = (ks * 4 + g) ^ (ql & (ds_cpr - 1) & 15);
         const v8s af = ds_read_b128(dsimg + ql * KB * 2 + chunk * 16);
-        const v8s bf = frag_tr(kimg, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane);
+        const v8s bf = frag_tr(kimg, KB, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane);
         acc = mfma16(af, bf, acc);
       }
 #pragma unroll
@@ -368,7 +404,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     if (key >= N) continue;
     uint16_t* row = dqkv + ((int64_t)b * N + key) * ld_dq;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < C::NE; ++e) {
       uint2 wk, wv;
       wk.x = pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale);
       wk.y = pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale);
@@ -393,39 +429,56 @@ __global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict
 }  // namespace
 }  // namespace pvr
 
+template <int DH>
+static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
+                                  int D, float scale, hipStream_t s) {
+  using namespace pvr;
+  hipLaunchKernelGGL(attn_fwd_kernel<DH>, dim3((N + 63) / 64, B * H), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
                                    int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
-  if (D != H * DH || B <= 0 || N <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((N + 63) / 64, B * H), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
-  return hipGetLastError();
+  if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
+  switch (D / H) {
+    case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
+    case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
+    case 96: return attn_fwd_launch<96>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
+    case 128: return attn_fwd_launch<128>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
+    default: return hipErrorInvalidValue;
+  }
 }
+
+extern "C" int pvr_attn_head_dim_supported(int dh) { return dh == 64 || dh == 80 || dh == 96 || dh == 128; }
 
 extern "C" int pvr_attn_bwd_waves(int N) {
   const int need = (N + 31) / 32;
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
 }
 
-// dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
-extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                   int B, int N, int H, int D, float scale, hipStream_t s) {
+template <int DH>
+static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                  int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                  int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
-  if (D != H * DH || B <= 0 || N <= 0) return hipErrorInvalidValue;
   const int64_t nrows = (int64_t)B * N * H;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, dout, ld_do, out, ld_o, delta, B, N, H);
+  hipLaunchKernelGGL(attn_bwd_delta_kernel<DH>, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, dout, ld_do, out, ld_o, delta,
+                     B, N, H);
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
   if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
-  const size_t smem = (size_t)KB * 128 + 2 * 32 * 128 + 32 * KB * 2 + 2 * 32 * 4;
+  const int RB = 128 * Hd<DH>::NH;
+  const size_t smem = (size_t)KB * RB + 2 * 32 * RB + 32 * KB * 2 + 2 * 32 * 4;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)(8 * 32 * RB + 2 * 32 * RB + 32 * 8 * 32 * 2 + 2 * 32 * 4));
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(nkb, B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
+  hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb, B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
                      nkb > 1 ? dq_acc : nullptr, N, H, D, scale);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
@@ -434,4 +487,18 @@ extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16
     hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dq_acc, dqkv, ld_dq, rows, D);
   }
   return hipGetLastError();
+}
+
+// dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
+extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                   int B, int N, int H, int D, float scale, hipStream_t s) {
+  if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
+  switch (D / H) {
+    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
+    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
+    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
+    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
+    default: return hipErrorInvalidValue;
+  }
 }

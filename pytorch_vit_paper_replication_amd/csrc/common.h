@@ -92,6 +92,24 @@ PVR_DEV void rng_keep2(uint64_t seed, uint64_t idx_even, uint32_t thr16, bool& k
 }
 
 PVR_DEV float gelu_erf(float u) { return 0.5f * u * (1.0f + erff(u * 0.70710678118654752f)); }
+
+// Exact-erf GELU and its derivative from ONE exponential: Phi(u) = 1 - erfc(u/sqrt2)/2 with the
+// Abramowitz-Stegun 7.1.26 erfc (|error| <= 1.5e-7, far below bf16 resolution), whose exp(-u^2/2)
+// is exactly the normal pdf's exponential. ~15 VALU ops incl. one v_exp / one v_rcp instead of
+// ocml erff + expf (the fc1 epilogue runs it 155M times per ViT-B/16 step).
+PVR_DEV void gelu_and_grad(float u, float& g, float& gp) {
+  const float au = fabsf(u);
+  const float e = __builtin_amdgcn_exp2f(-0.72134752044448170f * u * u);  // exp(-u^2/2)
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.23164190f, au, 1.0f));     // 1/(1 + p*|u|/sqrt2)
+  float poly = fmaf(t, 1.061405429f, -1.453152027f);
+  poly = fmaf(t, poly, 1.421413741f);
+  poly = fmaf(t, poly, -0.284496736f);
+  poly = fmaf(t, poly, 0.254829592f);
+  const float half_erfc = 0.5f * t * poly * e;  // erfc(|u|/sqrt2) / 2
+  const float cdf = u >= 0.f ? 1.0f - half_erfc : half_erfc;
+  g = u * cdf;
+  gp = fmaf(u * 0.39894228040143268f, e, cdf);
+}
 PVR_DEV float gelu_erf_grad(float u) {
   const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
   const float pdf = 0.39894228040143268f * __expf(-0.5f * u * u);

@@ -211,12 +211,11 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
             float gp[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float u = v[r];
-              const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
-              const float pdf = 0.39894228040143268f * __expf(-0.5f * u * u);
+              float gv, gd;
+              gelu_and_grad(v[r], gv, gd);
               const float sc = keep[r] ? p.drop_scale : 0.f;
-              v[r] = u * cdf * sc;
-              gp[r] = (cdf + u * pdf) * sc;
+              v[r] = gv * sc;
+              gp[r] = gd * sc;
             }
             uint2 a; a.x = pack2bf(gp[0], gp[1]); a.y = pack2bf(gp[2], gp[3]);
             *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = a;

@@ -96,7 +96,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       uint16_t* __restrict__ dx, int64_t dx_stride,
                                                       float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dsum,
                                                       int rows, int D) {
-  __shared__ float red[4][3][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];
+  __shared__ float red[4][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];  // one partial at a time
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = D >> 3;
   float gw[MAXCH][8], gb[MAXCH][8], gs[MAXCH][8];
@@ -152,26 +152,25 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
       }
     }
   }
-  // block reduction of dgamma/dbeta partials, then one atomic per column per block
+  // block reduction of the dgamma / dbeta / dsum partials, one quantity at a time through a
+  // [4][D] LDS buffer (keeps LDS at 4*D*4 bytes so occupancy is register-, not LDS-, bound),
+  // then one atomic per column per block
+  float* outs[3] = {dw, db, dsum};
 #pragma unroll
-  for (int i = 0; i < MAXCH; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
+  for (int qn = 0; qn < 3; ++qn) {
+    if (!outs[qn]) continue;  // uniform
+    if (qn) __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[wave][0][c * 8 + j] = gw[i][j];
-        red[wave][1][c * 8 + j] = gb[i][j];
-        red[wave][2][c * 8 + j] = gs[i][j];
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wave][c * 8 + j] = qn == 0 ? gw[i][j] : (qn == 1 ? gb[i][j] : gs[i][j]);
       }
     }
-  }
-  __syncthreads();
-  for (int col = threadIdx.x; col < D; col += 256) {
-    const float a = red[0][0][col] + red[1][0][col] + red[2][0][col] + red[3][0][col];
-    const float bsum = red[0][1][col] + red[1][1][col] + red[2][1][col] + red[3][1][col];
-    if (dw) atomicAdd(dw + col, a);
-    if (db) atomicAdd(db + col, bsum);
-    if (dsum) atomicAdd(dsum + col, red[0][2][col] + red[1][2][col] + red[2][2][col] + red[3][2][col]);
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += 256)
+      atomicAdd(outs[qn] + col, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
   }
 }
 

@@ -210,7 +210,7 @@ class ViT(nn.Module):
     def _fused_supported(self, x: torch.Tensor) -> bool:
         c = self.config
         D, H = c["embedding_dim"], c["num_heads"]
-        if x.dim() != 4 or x.shape[1] != 3 or D % H != 0 or D // H != 64 or D % 64 != 0:
+        if x.dim() != 4 or x.shape[1] != 3 or D % H != 0 or D // H not in (64, 80, 96, 128) or D % 64 != 0:
             return False
         if c["mlp_size"] % 64 != 0:
             return False

@@ -154,26 +154,26 @@ def _attn_ref(qkv, B, N, H):
     return o.transpose(1, 2).reshape(B * N, D), lse.reshape(B * H, N)
 
 
-def check_attn_fwd(B, N, H):
+def check_attn_fwd(B, N, H, dh=64):
     ext = _ext.ext()
-    D = H * 64
+    D = H * dh
     qkv = bf(rnd(B * N, 3 * D))
-    o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / 8.0)
+    o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / math.sqrt(dh))
     oref, lref = _attn_ref(qkv, B, N, H)
-    return (f"attn_fwd B{B} N{N} H{H}", max(rel_err(o, oref), rel_err(lse, lref) / 5), 2e-2)
+    return (f"attn_fwd B{B} N{N} H{H} dh{dh}", max(rel_err(o, oref), rel_err(lse, lref) / 5), 2e-2)
 
 
-def check_attn_bwd(B, N, H):
+def check_attn_bwd(B, N, H, dh=64):
     ext = _ext.ext()
-    D = H * 64
+    D = H * dh
     qkv = bf(rnd(B * N, 3 * D))
-    o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / 8.0)
+    o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / math.sqrt(dh))
     do = bf(rnd(B * N, D))
-    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / 8.0)
+    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh))
     qr = qkv.float().requires_grad_(True)
     oref, _ = _attn_ref(qr, B, N, H)
     oref.backward(do.float())
-    return (f"attn_bwd B{B} N{N} H{H}", rel_err(dqkv, qr.grad), 3e-2)
+    return (f"attn_bwd B{B} N{N} H{H} dh{dh}", rel_err(dqkv, qr.grad), 3e-2)
 
 
 # ----------------------------------------------------------------------------- misc
@@ -219,17 +219,19 @@ def check_adam():
     return ("fused adam+clip vs torch.optim.Adam", err + (0 if sh < 1e-2 else 1), 1e-5)
 
 
-def check_vit_fused_vs_reference(B=4, train=False):
+def check_vit_fused_vs_reference(B=4, train=False, **over):
     """Whole-model forward logits and parameter gradients, fused bf16 vs PyTorch fp32 (dropout 0)."""
     from pytorch_vit_paper_replication_amd.models import ViT
 
     torch.manual_seed(0)
     cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=128, mlp_size=256,
                num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0)
+    cfg.update(over)
     mf = ViT(**cfg).to(DEV)
     mr = ViT(**cfg).to(DEV)
     mr.load_state_dict(mf.state_dict())
-    x = torch.rand(B, 3, 64, 64, device=DEV)
+    assert mf._fused_supported(torch.empty(1, 3, cfg["image_size"], cfg["image_size"]))
+    x = torch.rand(B, 3, cfg["image_size"], cfg["image_size"], device=DEV)
     y = torch.randint(0, 10, (B,), device=DEV)
     mf.train(train)
     mr.train(train)
@@ -278,11 +280,21 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_bwd(1, 64, 1),
         lambda: check_attn_bwd(1, 257, 2),
         lambda: check_attn_bwd(1, 577, 2),
+        lambda: check_attn_fwd(2, 257, 3, 80),
+        lambda: check_attn_fwd(1, 33, 2, 80),
+        lambda: check_attn_bwd(2, 257, 3, 80),
+        lambda: check_attn_bwd(1, 40, 2, 80),
+        lambda: check_attn_fwd(1, 197, 2, 128),
+        lambda: check_attn_bwd(1, 300, 2, 128),
+        lambda: check_attn_bwd(1, 100, 2, 96),
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
         lambda: check_adam(),
         lambda: check_vit_fused_vs_reference(4, False),
         lambda: check_vit_fused_vs_reference(3, True),
+        # ViT-H/14-like geometry: patch 14, head dim 80, D = 5 x 64
+        lambda: check_vit_fused_vs_reference(2, True, image_size=56, patch_size=14, num_heads=4, embedding_dim=320,
+                                             mlp_size=640),
     ]
     return c
 
