@@ -34,6 +34,9 @@ def parse():
     p.add_argument("--num-classes", type=int, default=1000)
     p.add_argument("--impl", choices=["fused", "torch"], default="fused")
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
+    p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
+    p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
+    p.add_argument("--bucket-mb", type=float, default=28.0)
     return p.parse_args()
 
 
@@ -52,6 +55,13 @@ def main():
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     n = max(args.gpus, world_env)
     rank, world, device = init_distributed()
+    if args.force_ddp and not torch.distributed.is_initialized():
+        import datetime
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=device,
+                                             timeout=datetime.timedelta(seconds=600))
     per_gpu = args.batch or (256 if world == 1 else 512)
     torch.manual_seed(1234)
 
@@ -63,7 +73,8 @@ def main():
     else:
         opt = torch.optim.Adam(groups, lr=1e-3, betas=(0.9, 0.999))
     sched = warmup_linear_decay(opt, max(total_steps, 20), 0.05)
-    net = DistributedDataParallel(model) if world > 1 else model
+    use_ddp = world > 1 or args.force_ddp
+    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, comm=args.comm) if use_ddp else model
 
     g = torch.Generator(device=device).manual_seed(rank)
     x = torch.rand(per_gpu, 3, args.image_size, args.image_size, device=device, generator=g)
@@ -100,7 +111,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_ddp:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -133,11 +144,12 @@ def main():
             "data": "synthetic (random [B,3,224,224] in [0,1), 1000 classes, random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
                        "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl,
+                       "grad_transport": net.transport if use_ddp else "none",
                        "optimizer": "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
                        "dropout": "0.1 (mlp, embedding)", "final_loss": round(final_loss, 4)},
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_ddp:
         torch.distributed.destroy_process_group()
 
 

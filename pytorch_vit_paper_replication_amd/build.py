@@ -73,21 +73,21 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
         objs.append(obj)
         if force or _newer([src, *headers], obj):
             jobs_list.append([_hipcc(), *hip_flags, "-c", str(src), "-o", str(obj)])
-    bind_src = CSRC / "bindings.cpp"
-    bind_obj = BUILD_DIR / "bindings.o"
-    objs.append(bind_obj)
-    if force or _newer([bind_src], bind_obj):
-        cxx = os.environ.get("CXX", "g++")
-        import torch
+    import torch
 
-        abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
-        jobs_list.append([
-            cxx, "-O2", "-std=c++17", "-fPIC", "-c", str(bind_src), "-o", str(bind_obj),
-            "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-            "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-            f"-I{inc}", f"-I{inc / 'torch' / 'csrc' / 'api' / 'include'}", "-I/opt/rocm/include", f"-I{py_inc}",
-            "-w",
-        ])
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cxx = os.environ.get("CXX", "g++")
+    for cpp in sorted(CSRC.glob("*.cpp")):  # host-only translation units (ATen / pybind11 / RCCL)
+        obj = BUILD_DIR / (cpp.stem + ".o")
+        objs.append(obj)
+        if force or _newer([cpp, *headers], obj):
+            jobs_list.append([
+                cxx, "-O2", "-std=c++17", "-fPIC", "-c", str(cpp), "-o", str(obj),
+                "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                f"-I{inc}", f"-I{inc / 'torch' / 'csrc' / 'api' / 'include'}", "-I/opt/rocm/include", f"-I{py_inc}",
+                "-w",
+            ])
     if jobs_list:
         n = jobs or min(len(jobs_list), max(1, (os.cpu_count() or 4)), 16)
         with cf.ThreadPoolExecutor(max_workers=n) as ex:
@@ -99,7 +99,7 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
         link = [
             _hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(so),
             f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
-            f"-Wl,-rpath,{lib}",
+            f"-Wl,-rpath,{lib}", "-ldl",
         ]
         _run(link)
         if verbose:

@@ -5,6 +5,9 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+namespace pybind11 { class module_; }
+namespace pvr_comm { void register_comm(pybind11::module_& m); }
+
 namespace pvr {
 struct GemmParams {
   int M, N, K;
@@ -294,6 +297,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  pvr_comm::register_comm(m);
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
   m.def("gemm", &gemm, py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

@@ -13,10 +13,18 @@ Design, MI355X-first rather than a copy of torch 
   * buckets launch strictly in index order on every rank (no collective-order mismatch), and an
     autograd end-of-backward callback flushes the rest and joins the stream before the optimizer
     (the global-norm clip therefore sees averaged gradients, C3).
+
+Transport (``comm``): on GPUs the default is the native C++ RCCL communicator
+(``parallel/comm.py`` -> ``csrc/comm.cpp``): each bucket is all-reduced (``ncclAvg``) on the
+communicator's own high-priority HIP stream, gated by an event on the compute stream, and the
+optimizer's stream waits on the last bucket's event — no host synchronisation anywhere. ``comm="torch"``
+(or ``PVR_COMM=torch``) uses ``torch.distributed`` collectives instead; gloo/CPU always does.
 """
 from __future__ import annotations
 
 import contextlib
+import os
+import warnings
 from typing import Dict, List, Optional
 
 import torch
@@ -28,7 +36,7 @@ from ..runtime.param_store import ParamStore, get_store
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 28.0,
-                 broadcast_parameters: bool = True, comm_dtype: Optional[torch.dtype] = None):
+                 broadcast_parameters: bool = True, comm_dtype: Optional[torch.dtype] = None, comm: str = "auto"):
         super().__init__()
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("DistributedDataParallel needs an initialised torch.distributed process group")
@@ -49,6 +57,23 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._hooks = []
         self._avg = dist.get_backend(process_group) == "nccl"
+        self._comm_mode = comm
+        self._native = None          # parallel.comm.NativeCommunicator when the native transport is used
+        self._comm_buf: Optional[torch.Tensor] = None  # persistent low-precision gradient mirror
+
+    def _pick_transport(self, device):
+        mode = os.environ.get("PVR_COMM", self._comm_mode)
+        if mode == "torch" or device.type != "cuda" or not self._avg:
+            return None
+        from .comm import NativeCommunicator
+
+        try:
+            return NativeCommunicator.create(device, self.process_group)
+        except Exception as e:  # pragma: no cover - only on GPU boxes
+            if mode == "native":
+                raise
+            warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed collectives")
+            return None
 
     # ------------------------------------------------------------------ setup
     def _setup(self, device):
@@ -61,13 +86,23 @@ class DistributedDataParallel(nn.Module):
         if self._store is not None:
             self._store.remove_listener(self._on_ready)
         self._store = store
+        if self._native is None:
+            self._native = self._pick_transport(device)
         if self.broadcast_parameters:
             with torch.no_grad():
-                src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
-                dist.broadcast(store.flat, src=src, group=self.process_group)
-                for b in self.module.buffers():
-                    dist.broadcast(b, src=src, group=self.process_group)
+                if self._native is not None:
+                    self._native.wait(self._native.broadcast(store.flat, root=0))
+                    for b in self.module.buffers():
+                        if b.is_cuda and b.is_contiguous():
+                            self._native.wait(self._native.broadcast(b, root=0))
+                else:
+                    src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+                    dist.broadcast(store.flat, src=src, group=self.process_group)
+                    for b in self.module.buffers():
+                        dist.broadcast(b, src=src, group=self.process_group)
             store.refresh_shadow(force=True)
+        if self.comm_dtype is not None and self.comm_dtype != store.grad_flat.dtype:
+            self._comm_buf = torch.empty(store.numel, dtype=self.comm_dtype, device=store.grad_flat.device)
         # buckets: reverse parameter order, contiguous flat ranges of about bucket_cap bytes
         buckets = []
         cur: List[int] = []
@@ -147,6 +182,14 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, b: int):
         lo, hi, _ = self._buckets[b]
         buf = self._store.grad_flat[lo:hi]
+        if self._native is not None:
+            if self._comm_buf is not None:  # low-precision wire format, persistent mirror: no allocator traffic
+                tmp = self._comm_buf[lo:hi]
+                tmp.copy_(buf)
+                self._works.append((self._native.all_reduce(tmp), buf, tmp))
+            else:
+                self._works.append((self._native.all_reduce(buf), buf, None))
+            return
         if self.comm_dtype is not None and self.comm_dtype != buf.dtype:
             tmp = buf.to(self.comm_dtype)
             op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
@@ -161,6 +204,13 @@ class DistributedDataParallel(nn.Module):
         while self._next_launch < len(self._buckets):
             self._launch(self._next_launch)
             self._next_launch += 1
+        if self._native is not None:
+            for h, buf, tmp in self._works:
+                self._native.wait(h)  # compute stream waits on the comm stream: no host sync
+                if tmp is not None:
+                    buf.copy_(tmp)
+            self._works = []
+            return
         for w, buf, tmp in self._works:
             w.wait()
             if tmp is not None:
@@ -168,6 +218,10 @@ class DistributedDataParallel(nn.Module):
             if not self._avg:
                 buf.div_(self.world)
         self._works = []
+
+    @property
+    def transport(self) -> str:
+        return "native-rccl" if self._native is not None else f"torch-{dist.get_backend(self.process_group)}"
 
     # convenience passthroughs
     def state_dict(self, *a, **k):

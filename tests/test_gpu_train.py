@@ -93,7 +93,8 @@ def test_fused_training_tracks_fp32_reference():
     assert cos > 0.9, f"fused vs fp32 update direction cosine {cos:.3f}"
 
 
-def test_ddp_rccl_world1_matches_local():
+@pytest.mark.parametrize("comm", ["native", "torch"])
+def test_ddp_rccl_world1_matches_local(comm):
     import torch.distributed as dist
 
     from pytorch_vit_paper_replication_amd.models import ViT
@@ -109,7 +110,7 @@ def test_ddp_rccl_world1_matches_local():
         cfg = dict(CFG, mlp_dropout=0.0, embedding_dropout=0.0)
         m1, m2 = ViT(**cfg).to(dev), ViT(**cfg).to(dev)
         m2.load_state_dict(m1.state_dict())
-        ddp = DistributedDataParallel(m1, bucket_cap_mb=0.25)
+        ddp = DistributedDataParallel(m1, bucket_cap_mb=0.25, comm=comm)
         x = torch.rand(4, 3, 64, 64, device=dev)
         y = torch.randint(0, 10, (4,), device=dev)
         for _ in range(2):
@@ -121,7 +122,46 @@ def test_ddp_rccl_world1_matches_local():
             cross_entropy(m2(x), y).backward()
         torch.cuda.synchronize()
         assert len(ddp._buckets) > 1
+        assert ddp.transport == ("native-rccl" if comm == "native" else "torch-nccl")
         for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
             assert torch.allclose(p1.grad, p2.grad, rtol=1e-4, atol=1e-5), n
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_communicator_collectives_world1():
+    """The C++ RCCL communicator's collectives, stream ordering and handles (world_size 1)."""
+    import torch.distributed as dist
+
+    from pytorch_vit_paper_replication_amd.parallel.comm import NativeCommunicator
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        c = NativeCommunicator.create(dev)
+        x = torch.randn(1 << 20, device=dev)
+        ref = x.clone()
+        x.mul_(2.0)  # queued on the compute stream: the all-reduce must observe it
+        h = c.all_reduce(x, average=True)
+        c.wait(h)
+        y = x + 0  # runs after the wait on the compute stream
+        assert torch.equal(y, ref * 2)
+        out = torch.empty_like(x)
+        c.wait(c.all_gather(x, out))
+        assert torch.equal(out, x)
+        rs = torch.empty_like(x)
+        c.wait(c.reduce_scatter(x, rs, average=False))
+        assert torch.equal(rs, x)
+        b = torch.arange(10, device=dev, dtype=torch.bfloat16)
+        c.wait(c.broadcast(b, 0))
+        assert torch.equal(b, torch.arange(10, device=dev, dtype=torch.bfloat16))
+        c.barrier()
+        hs = [c.all_reduce(torch.ones(4096, device=dev)) for _ in range(300)]  # > event-ring size
+        c.wait_all()
+        with pytest.raises(RuntimeError):
+            c.wait(hs[0])  # recycled handle is rejected
+        c.destroy()
     finally:
         dist.destroy_process_group()
