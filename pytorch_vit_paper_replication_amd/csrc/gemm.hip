@@ -398,6 +398,8 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 // across the barrier), one raw s_barrier per stage, 8 waves. 256-row tiles halve the L2->LDS bytes
 // per MFMA against 128x128 (which needs ~64 B/clk/CU at peak MFMA rate, the whole L2 bandwidth).
 constexpr int BK32 = 32;
+// LDS-DMA wave-instructions per wave per BK=32 stage of a BM x BN tile (1 KiB each)
+#define LPS_OF(BM, BN, NW) (((BM) * BK32 * 2 / 1024 + (BN) * BK32 * 2 / 1024) / (NW))
 
 PVR_DEV int swz_k32(int row) { return (row >> 1) & 3; }  // 64-B rows: conflict-free ds_read_b128
 
@@ -661,11 +663,12 @@ PVR_DEV void v3_stage(v4f (&acc)[BM / WM / 16][BN / WN / 16], const v8s (&ac)[BM
   });
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP, int EPI>
-__global__ void __launch_bounds__(WM* WN * 64, WM* WN / 4) gemm_v3_kernel(GemmParams p) {
-  constexpr int NW = WM * WN, STAGES = 4;
+template <int BM, int BN, int WM, int WN, int STAGES, int WPE, bool AK, bool BKC, bool SWAP, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64, WPE) gemm_v3_kernel(GemmParams p) {
+  static_assert(STAGES == 3 || STAGES == 4, "ring depth");
+  constexpr int NW = WM * WN;
+  constexpr int INFL = (STAGES - 2) * LPS_OF(BM, BN, NW);  // DMA instructions allowed in flight at a stage barrier
   constexpr int A_BYTES = BM * BK32 * 2, B_BYTES = BN * BK32 * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int LPS = (A_BYTES / 1024 + B_BYTES / 1024) / NW;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // wave tile in 16x16 fragments
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -710,31 +713,33 @@ __global__ void __launch_bounds__(WM* WN * 64, WM* WN / 4) gemm_v3_kernel(GemmPa
     for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
   stamp(p, 0);
-  // Prologue: stages 0..3 (stages >= nk use the null resource, keeping every vmcnt count uniform).
+  // Prologue: stages 0..STAGES-1 (stages >= nk use the null resource, keeping every vmcnt count uniform).
 #pragma unroll
   for (int s = 0; s < STAGES; ++s) {
     char* dst = smem + s * STAGE_BYTES;
     stage32<BM, AK, NW>(pick_rsrc(s < nk, ars, nul), dst, p.lda, s * BK32, wave, lane);
     stage32<BN, BKC, NW>(pick_rsrc(s < nk, brs, nul), dst + A_BYTES, p.ldb, s * BK32, wave, lane);
   }
-  wait_barrier<2 * LPS>();  // stages 0 and 1 landed
+  wait_barrier<INFL>();  // stages 0 and 1 landed
   v8s a0[FM], b0[FN], a1[FM], b1[FN];
   load_frags<FM, FN, BM, BN, AK, BKC>(smem, wm, wn, lane, a0, b0);
-  wait_barrier_lds<2 * LPS>();  // every wave holds stage 0 in registers: slot 0 may be refilled
+  wait_barrier_lds<INFL>();  // every wave holds stage 0 in registers: slot 0 may be refilled
   stamp(p, 1);
 
-  // Invariant at stage kt: its fragments are in registers, its LDS slot receives stage kt+4, stage
-  // kt+1 is visible. The barrier after stage kt waits for stage kt+2 and retires the LDS reads.
+  // Invariant at stage kt: its fragments are in registers, its LDS slot receives stage kt+STAGES,
+  // stage kt+1 is visible. The barrier after stage kt waits for stage kt+2 and retires the LDS reads.
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
     v3_stage<BM, BN, WM, WN, AK, BKC, SWAP>(acc, a0, b0, a1, b1, smem + ((kt + 1) % STAGES) * STAGE_BYTES,
-                                    smem + (kt % STAGES) * STAGE_BYTES, pick_rsrc(kt + 4 < nk, ars, nul),
-                                    pick_rsrc(kt + 4 < nk, brs, nul), p.lda, p.ldb, (kt + 4) * BK32, wave, lane, wm, wn);
-    wait_barrier_lds<2 * LPS>();
+                                    smem + (kt % STAGES) * STAGE_BYTES, pick_rsrc(kt + STAGES < nk, ars, nul),
+                                    pick_rsrc(kt + STAGES < nk, brs, nul), p.lda, p.ldb, (kt + STAGES) * BK32, wave, lane,
+                                    wm, wn);
+    wait_barrier_lds<INFL>();
     v3_stage<BM, BN, WM, WN, AK, BKC, SWAP>(acc, a1, b1, a0, b0, smem + ((kt + 2) % STAGES) * STAGE_BYTES,
-                                    smem + ((kt + 1) % STAGES) * STAGE_BYTES, pick_rsrc(kt + 5 < nk, ars, nul),
-                                    pick_rsrc(kt + 5 < nk, brs, nul), p.lda, p.ldb, (kt + 5) * BK32, wave, lane, wm, wn);
-    wait_barrier_lds<2 * LPS>();
+                                    smem + ((kt + 1) % STAGES) * STAGE_BYTES, pick_rsrc(kt + 1 + STAGES < nk, ars, nul),
+                                    pick_rsrc(kt + 1 + STAGES < nk, brs, nul), p.lda, p.ldb, (kt + 1 + STAGES) * BK32, wave,
+                                    lane, wm, wn);
+    wait_barrier_lds<INFL>();
   }
   if (kt < nk) mfma_block<FM, FN, SWAP>(acc, a0, b0);  // odd tail: set 0 holds the last stage
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // no LDS-DMA may outlive the workgroup
@@ -744,10 +749,10 @@ __global__ void __launch_bounds__(WM* WN * 64, WM* WN / 4) gemm_v3_kernel(GemmPa
   stamp(p, 3);
 }
 
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, bool SWAP, int EPI>
+template <int BM, int BN, int WM, int WN, int STAGES, int WPE, bool AK, bool BKC, bool SWAP, int EPI>
 hipError_t launch_v3(const GemmParams& p, hipStream_t s) {
-  constexpr int SMEM = 4 * (BM + BN) * BK32 * 2;
-  auto kern = gemm_v3_kernel<BM, BN, WM, WN, AK, BKC, SWAP, EPI>;
+  constexpr int SMEM = STAGES * (BM + BN) * BK32 * 2;
+  auto kern = gemm_v3_kernel<BM, BN, WM, WN, STAGES, WPE, AK, BKC, SWAP, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -768,9 +773,14 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     case 3: return launch_ms<256, 256, 2, 4, 4, AK, BKC, SWAP, EPI>(p, s);
     case 4: return launch_ms<256, 128, 4, 2, 4, AK, BKC, SWAP, EPI>(p, s);
     case 5: return launch_ms<128, 256, 2, 4, 4, AK, BKC, SWAP, EPI>(p, s);
-    case 6: return launch_v3<256, 256, 2, 4, AK, BKC, SWAP, EPI>(p, s);
-    case 7: return launch_v3<256, 128, 2, 2, AK, BKC, SWAP, EPI>(p, s);
-    case 8: return launch_v3<256, 256, 2, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 6: return launch_v3<256, 256, 2, 4, 4, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 7: return launch_v3<256, 128, 2, 2, 4, 1, AK, BKC, SWAP, EPI>(p, s);
+    case 8: return launch_v3<256, 256, 2, 2, 4, 1, AK, BKC, SWAP, EPI>(p, s);
+    // 4-wave tiles with a 3-deep ring (72 KB LDS): two workgroups per CU, so one's epilogue overlaps
+    // the other's main loop, and half-size tiles cut the last-round quantisation at N = 768
+    case 9: return launch_v3<256, 128, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 10: return launch_v3<128, 256, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 11: return launch_v3<256, 256, 2, 4, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     default: return launch_cfg<128, 128, 2, 2, AK, BKC, SWAP, EPI>(p, s);
   }
 }

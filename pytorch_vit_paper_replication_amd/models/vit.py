@@ -241,6 +241,7 @@ class ViT(nn.Module):
             if p.device != dev:
                 raise RuntimeError(f"input is on {dev} but model parameters are on {p.device}")
         store = get_store(self, dev)
+        store.join_side()
         store.refresh_shadow()
         if not getattr(store, "_vit_t_registered", False):
             store.register_transposed([w for blk in self.transformer_encoder for w in blk.fused_params()[2:12:2] if w.dim() == 2])

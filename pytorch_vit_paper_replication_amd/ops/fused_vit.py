@@ -124,12 +124,15 @@ class EncoderBlockFn(torch.autograd.Function):
                 gemm.bias_grad(dx2, g(b2))
         # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
         du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=g(b1))
-        gw2 = g(w2)
-        if gw2 is not None:
-            gemm.linear_wgrad(dz2, h, gw2)
-        gw1 = g(w1)
-        if gw1 is not None:
-            gemm.linear_wgrad(du, xn2, gw1)
+        gw2, gw1 = g(w2), g(w1)
+
+        def mlp_wgrads():
+            if gw2 is not None:
+                gemm.linear_wgrad(dz2, h, gw2)
+            if gw1 is not None:
+                gemm.linear_wgrad(du, xn2, gw1)
+
+        store.on_side(mlp_wgrads, dz2, h, du, xn2)  # weight grads off the critical path
         dxn2 = gemm.linear_dgrad(du, store.bf16(w1), wt=store.bf16_t(w1))
         dx1 = torch.empty_like(dx2)
         # dx1 = dx2 + LN2'(dxn2); d(bo) = colsum(dx1) reduced in the same kernel
@@ -137,15 +140,18 @@ class EncoderBlockFn(torch.autograd.Function):
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
         do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
-        gwo = g(wo)
-        if gwo is not None:
-            gemm.linear_wgrad(dx1, o, gwo)
         dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
         if bqkv.requires_grad:
             gemm.bias_grad(dqkv, g(bqkv))
-        gwqkv = g(wqkv)
-        if gwqkv is not None:
-            gemm.linear_wgrad(dqkv, xn1, gwqkv)
+        gwo, gwqkv = g(wo), g(wqkv)
+
+        def attn_wgrads():
+            if gwo is not None:
+                gemm.linear_wgrad(dx1, o, gwo)
+            if gwqkv is not None:
+                gemm.linear_wgrad(dqkv, xn1, gwqkv)
+
+        store.on_side(attn_wgrads, dx1, o, dqkv, xn1)
         dxn1 = gemm.linear_dgrad(dqkv, store.bf16(wqkv), wt=store.bf16_t(wqkv))
         dx = torch.empty_like(dx2)
         ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)

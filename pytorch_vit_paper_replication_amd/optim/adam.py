@@ -135,6 +135,7 @@ class FusedAdam(torch.optim.Optimizer):
             self.last_grad_norm = n
             return n
         store, m, v, seg_start, seg_group, ws, clip = fz
+        store.join_side()
         _ext.ext().grad_norm(store.grad_flat, float(max_norm), ws, clip)
         self._pending_clip = True
         self.last_grad_norm = clip[0]
@@ -151,6 +152,7 @@ class FusedAdam(torch.optim.Optimizer):
         step = self.step_count
         if fz is not None:
             store, m, v, seg_start, seg_group, ws, clip = fz
+            store.join_side()  # weight gradients may still be in flight on the side stream
             use_clip = getattr(self, "_pending_clip", False)
             if clip_norm is not None:
                 _ext.ext().grad_norm(store.grad_flat, float(clip_norm), ws, clip)

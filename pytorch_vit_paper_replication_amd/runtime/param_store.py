@@ -16,6 +16,7 @@ bucketer) as soon as a group of parameters has its final gradient.
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Callable, Dict, Iterable, List, Optional
 
@@ -84,6 +85,10 @@ class ParamStore:
         self._t_dirty = True
         self.shadow_t: Optional[torch.Tensor] = None
         self._listeners: List[Callable[[List[torch.nn.Parameter]], None]] = []
+        # weight-gradient side stream (see on_side): created lazily on GPU stores
+        self._side: Optional[torch.cuda.Stream] = None
+        self._side_pending = False
+        self._join_queued = False
         self.refresh_shadow(force=True)
 
     # ------------------------------------------------------------------ validity
@@ -166,6 +171,10 @@ class ParamStore:
 
     # ------------------------------------------------------------------ gradients
     def prepare_grads(self) -> None:
+        self.join_side()
+        self._prepare_grads()
+
+    def _prepare_grads(self) -> None:
         """Make every trainable parameter's .grad a view of the flat gradient buffer.
 
         ``zero_grad(set_to_none=True)`` leaves ``p.grad is None``, which means "zero": the region is
@@ -210,7 +219,55 @@ class ParamStore:
                 gv.copy_(p.grad)
             p.grad = gv
 
+    # ------------------------------------------------------------------ weight-gradient side stream
+    # The weight-gradient GEMMs of a backward pass are off the critical path (only the optimizer and
+    # the gradient all-reduce consume them), so the fused backward queues them on a second HIP stream:
+    # they fill the CUs the dgrad chain leaves idle (last-round tile quantisation of N = 768 GEMMs,
+    # memory-bound LayerNorm / attention phases). Ordering: the side stream waits for the main stream
+    # before each batch of wgrads; gradient-ready notifications (DDP buckets) are issued from the side
+    # stream after it has caught up with main; an end-of-backward autograd callback joins the side
+    # stream back into the caller's stream, so anything after backward() sees complete gradients.
+    def side_stream(self) -> Optional[torch.cuda.Stream]:
+        if self.device.type != "cuda" or os.environ.get("PVR_SIDE_WGRAD", "1") == "0":
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def on_side(self, fn: Callable[[], None], *tensors: torch.Tensor) -> None:
+        """Run ``fn`` (kernel launches) on the side stream after the work queued so far on the
+        current stream; ``tensors`` are kept alive for the side stream by the caching allocator."""
+        side = self.side_stream()
+        if side is None:
+            fn()
+            return
+        main = torch.cuda.current_stream(self.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            fn()
+        for t in tensors:
+            t.record_stream(side)
+        self._side_pending = True
+        self._queue_join()
+
+    def _queue_join(self) -> None:
+        if self._join_queued:
+            return
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(self.join_side)
+            self._join_queued = True
+        except RuntimeError:  # not inside a backward pass: join eagerly
+            self.join_side()
+
+    def join_side(self) -> None:
+        """Make the current stream wait for every side-stream launch so far."""
+        self._join_queued = False
+        if self._side_pending and self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._side_pending = False
+
     def zero_grad(self) -> None:
+        self.join_side()
         self.grad_flat.zero_()
         for i, p in enumerate(self.params):
             if p.requires_grad:
@@ -226,6 +283,15 @@ class ParamStore:
     def grad_ready(self, params: Iterable[torch.nn.Parameter]) -> None:
         if self._listeners:
             ps = [p for p in params if p is not None]
+            if self._side_pending and self._side is not None:
+                # gradients of this batch live on both streams: notify from the side stream once it
+                # has caught up with main, so a collective gated on the current stream sees all of them
+                self._queue_join()  # keep the join callback ahead of any listener's own callback
+                self._side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self._side):
+                    for fn in self._listeners:
+                        fn(ps)
+                return
             for fn in self._listeners:
                 fn(ps)
 

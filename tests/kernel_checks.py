@@ -256,7 +256,7 @@ def check_vit_fused_vs_reference(B=4, train=False, **over):
 
 def all_checks() -> List[Callable]:
     c = []
-    for tile in (0, 6):
+    for tile in (0, 6, 9, 10):
         c.append(lambda t=tile: check_gemm_fwd(50432 // 16, 768, 768, t))
         c.append(lambda t=tile: check_gemm_fwd(197 * 3, 2304, 768, t, True, True))
         c.append(lambda t=tile: check_gemm_gelu(197 * 2, 3072, 768, t))
