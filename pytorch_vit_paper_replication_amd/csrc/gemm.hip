@@ -765,6 +765,271 @@ hipError_t launch_v3(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ===================================================================================== ping-pong
+// 256x256 tile, BK = 64, 8 waves as 2 groups of 4 (group = wm: one wave of each group per SIMD),
+// k-contiguous operands only. Each wave owns a 128x64 output (8x4 fragments) processed as four
+// 64x32 quadrants per K-tile ("phases"). A phase is
+//     R: ds_read this quadrant's register subtile | issue one half-tile of LDS-DMA | counted vmcnt
+//     barrier | lgkmcnt(0) | prio 1: 16 MFMAs (quadrant x K 64) | prio 0 | barrier
+// and group 1 runs one barrier behind group 0, so on every SIMD one wave's MFMA block overlaps the
+// other wave's fragment reads and DMA issue (the two never compete for the same phase).
+//
+// LDS: two 64 KiB buffers (K-tile t in buffer t&1), each an A image [256][64] and a B image
+// [256][64] of 128-B swizzled rows. "Half-tiles" are the rows one quadrant reads:
+//   A0 = A rows {0-63, 128-191} (qm = 0 of both wave rows), A1 = {64-127, 192-255},
+//   B0 = B rows {32-row blocks 0,2,4,6} (qn = 0 of every wave column), B1 = blocks {1,3,5,7}.
+// Phase order per K-tile: (qm,qn) = (0,0) reads A0,B0 | (0,1) reads B1 | (1,1) reads A1 | (1,0) -.
+// A half-tile is dead two phases after its last read, so K-tile t+2 is staged into buffer t&1 in
+// the order A0,B0 (phases 3,4 of t), B1,A1 (phases 1,2 of t+1): half-tile h = 4t + {0:A0,1:B0,2:B1,
+// 3:A1} is issued at global phase h - 6, and the vmcnt(8) before each phase's first barrier (four
+// half-tiles = 8 DMA instructions per wave stay in flight) retires exactly what the next phase
+// reads — every read is one phase after the wait that retires it, across one barrier more than
+// the group stagger needs.
+constexpr int PP_BK = 64;
+constexpr int PP_BUF = 2 * 256 * 128;  // A + B image of one K-tile
+
+template <int W>
+PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem,
+                      int64_t lda, int64_t ldb, int t, int nk, int wave, int lane) {
+  char* buf = smem + (t & 1) * PP_BUF;
+  const int k0 = t * PP_BK;
+  const bool live = t < nk;
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int d = wave + 8 * x;  // 16 wave-instructions of 1 KiB per half-tile
+    if constexpr (W == 0 || W == 3) {
+      constexpr int hh = W == 3;
+      const int rowb = (2 * (d >> 3) + hh) * 64 + (d & 7) * 8;  // first image row of this instruction
+      const int row = rowb + (lane >> 3);
+      const int c = (lane & 7) ^ swz_k(row);
+      dma16(live ? ars : nul, to_lds(buf + rowb * 128), (uint32_t)(row * lda * 2 + (int64_t)(k0 + c * 8) * 2));
+    } else {
+      constexpr int hh = W == 2;
+      const int rowb = (2 * (d >> 2) + hh) * 32 + (d & 3) * 8;
+      const int row = rowb + (lane >> 3);
+      const int c = (lane & 7) ^ swz_k(row);
+      dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * 2 + (int64_t)(k0 + c * 8) * 2));
+    }
+  }
+}
+
+// issue half-tile h (compile-time kind h & 3)
+template <int KIND>
+PVR_DEV void pp_issue_h(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem,
+                        int64_t lda, int64_t ldb, int t, int nk, int wave, int lane) {
+  pp_issue<KIND>(ars, brs, nul, smem, lda, ldb, t, nk, wave, lane);
+}
+
+PVR_DEV void pp_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int QM, int QN, int RD_A, int RD_B, int KIND, bool SWAP>
+PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
+                      __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
+                      int t_issue, int nk, int wave, int lane, int wm, int wn) {
+  // R: register subtile for this quadrant
+  if constexpr (RD_A) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+  }
+  if constexpr (RD_B) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
+  }
+  pp_issue_h<KIND>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  pp_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        v4f& c = acc[QM * 4 + ii][QN * 2 + jj];
+        if constexpr (SWAP)
+          c = mfma16(bf[QN][jj][ks], af[ii][ks], c);
+        else
+          c = mfma16(af[ii][ks], bf[QN][jj][ks], c);
+      }
+  __builtin_amdgcn_s_setprio(0);
+  pp_barrier();
+}
+
+// LDS-staged epilogue of the ping-pong kernel (SWAP layout, bf16-output epilogues): the fp32
+// accumulators cross LDS in two 128-row halves (the 128 KiB of K-tile buffers are free by then),
+// and every thread then owns 4 consecutive columns of rows t/64 + 8k, so each wave instruction
+// reads/writes one whole 512-B row segment — residual / aux loads and bf16 stores are fully
+// coalesced instead of 16 rows x 32 B per instruction. The math is the per-element epilogue above,
+// in fp32, unchanged. Row images are 1 KiB (256 fp32) with the 16-B chunk index XOR-swizzled by
+// the row (ds_write_b128 2-way, ds_read_b128 conflict-free).
+template <int EPI>
+PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, int m0, int n0, int wm, int wn, int lane) {
+  const int tid = threadIdx.x;
+  const int g = lane >> 4, li = lane & 15;
+  const int cq = tid & 63;           // this thread's 4-column group within the tile row
+  const int n = n0 + 4 * cq;
+  const bool ncol = n < p.N;
+  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+    if (p.bias && ncol) bias = *(const float4*)(p.bias + n);
+  }
+  const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();  // previous half's LDS reads (or the main loop's) are done
+    if (wm == half) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * i + li;                 // row within the half
+          const int ch = wn * 16 + 4 * j + g;        // 16-B chunk (4 fp32 columns) within the row
+          *(v4f*)(smem + r * 1024 + ((ch ^ (r & 63)) << 4)) = acc[i][j];
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int r = (tid >> 6) + 8 * k;
+      const int m = m0 + half * 128 + r;
+      const v4f a = *(const v4f*)(smem + r * 1024 + ((cq ^ (r & 63)) << 4));
+      if (m >= p.M || !ncol) continue;
+      float v[4] = {a[0], a[1], a[2], a[3]};
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+        v[0] += bias.x; v[1] += bias.y; v[2] += bias.z; v[3] += bias.w;
+        bool keep[4] = {true, true, true, true};
+        if (p.drop_thr) {
+          const uint64_t idx = (uint64_t)m * p.N + n;
+          rng_keep2(seed, idx, p.drop_thr, keep[0], keep[1]);
+          rng_keep2(seed, idx + 2, p.drop_thr, keep[2], keep[3]);
+        }
+        if constexpr (EPI == EPI_BF16) {
+          if (p.drop_thr) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = keep[q] ? v[q] * p.drop_scale : 0.f;
+          }
+          if (p.resid) {
+            const uint2 rr = *(const uint2*)(p.resid + (int64_t)m * p.ld_resid + n);
+            v[0] += bf2f(rr.x & 0xFFFF); v[1] += bf2f(rr.x >> 16);
+            v[2] += bf2f(rr.y & 0xFFFF); v[3] += bf2f(rr.y >> 16);
+          }
+        } else {
+          float gp[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float gv, gd;
+            gelu_and_grad(v[q], gv, gd);
+            const float sc = keep[q] ? p.drop_scale : 0.f;
+            v[q] = gv * sc;
+            gp[q] = gd * sc;
+          }
+          uint2 ax; ax.x = pack2bf(gp[0], gp[1]); ax.y = pack2bf(gp[2], gp[3]);
+          *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = ax;
+        }
+      } else {  // EPI_DGELU
+        const uint2 gg = *(const uint2*)(p.aux + (int64_t)m * p.ld_aux + n);
+        v[0] *= bf2f(gg.x & 0xFFFF); v[1] *= bf2f(gg.x >> 16);
+        v[2] *= bf2f(gg.y & 0xFFFF); v[3] *= bf2f(gg.y >> 16);
+        csum[0] += v[0]; csum[1] += v[1]; csum[2] += v[2]; csum[3] += v[3];
+      }
+      uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+      *(uint2*)((uint16_t*)p.C + (int64_t)m * p.ldc + n) = o;
+    }
+  }
+  if constexpr (EPI == EPI_DGELU) {
+    if (p.colsum && ncol) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) atomicAdd(p.colsum + n + q, csum[q]);
+    }
+  }
+}
+
+template <bool SWAP, int EPI>
+__global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // group = wm
+
+  const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
+  const int tt = xcd_remap(blockIdx.x, ntm * ntn);
+  const int m0 = (tt / ntn) * 256, n0 = (tt % ntn) * 256;
+  const int nk = p.K / PP_BK;
+
+  const uint16_t* abase = p.A + (int64_t)m0 * p.lda;
+  const uint16_t* bbase = p.B + (int64_t)n0 * p.ldb;
+  const __amdgpu_buffer_rsrc_t ars = make_rsrc(abase, rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda));
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bbase, rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb));
+  const __amdgpu_buffer_rsrc_t nul = make_rsrc(abase, 0);
+
+  v4f acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  v8s af[4][2], bf[2][2][2];
+
+  stamp(p, 0);
+  // prologue: half-tiles 0..5 = all of K-tile 0, A0/B0 of K-tile 1
+  pp_issue<0>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<1>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<2>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<3>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<0>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
+  pp_issue<1>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0 of K-tile 0 landed
+  pp_barrier();
+  if (wm == 1) pp_barrier();  // group 1 runs one barrier behind
+  stamp(p, 1);
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * PP_BUF;
+    // phase P = 4t + ph issues half-tile P + 6 = 4(t+1) + ph + 2
+    pp_phase<0, 0, 1, 1, 2, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
+    pp_phase<0, 1, 0, 1, 3, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
+    pp_phase<1, 1, 1, 0, 0, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+    pp_phase<1, 0, 0, 0, 1, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
+  if (wm == 0) pp_barrier();  // equal barrier counts for both groups
+  stamp(p, 2);
+  if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
+    if (!p.addend && !p.row_group && (p.N & 3) == 0)
+      epilogue_staged<EPI>(p, acc, smem, m0, n0, wm, wn, lane);
+    else
+      epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  } else {
+    epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  }
+  if (p.dbg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(p, 3);
+}
+
+template <bool SWAP, int EPI>
+hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
+  constexpr int SMEM = 2 * PP_BUF;
+  auto kern = gemm_pp_kernel<SWAP, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
+  hipLaunchKernelGGL(kern, dim3(ntm * ntn), dim3(512), SMEM, s, p);
+  return hipGetLastError();
+}
+
 template <bool AK, bool BKC, bool SWAP, int EPI>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   switch (p.tile_cfg) {
@@ -781,6 +1046,11 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     case 9: return launch_v3<256, 128, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 10: return launch_v3<128, 256, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 11: return launch_v3<256, 256, 2, 4, 3, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 12:
+      if constexpr (AK && BKC) {
+        if (p.K % PP_BK == 0 && p.k_split_len >= p.K) return launch_pp<SWAP, EPI>(p, s);
+      }
+      return launch_v3<256, 256, 2, 4, 4, 2, AK, BKC, SWAP, EPI>(p, s);
     default: return launch_cfg<128, 128, 2, 2, AK, BKC, SWAP, EPI>(p, s);
   }
 }

@@ -24,13 +24,14 @@ Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device
 
 
 def _tile(M: int, N: int, K: int, kind: str) -> int:
-    """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py):
-    k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave LDS-DMA ring (6); token-reduced
-    wgrad (both operands mn-contiguous, split-K atomics) -> 128x128 (0)."""
+    """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
+    k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave ping-pong (12; K % 64 == 0, else
+    the 4-stage BK=32 ring 6); token-reduced wgrad (both operands mn-contiguous, split-K
+    atomics) -> 128x128 (0)."""
     if _FORCE_TILE is not None:
         return int(_FORCE_TILE)
     if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
-        return 6
+        return 12 if K % 64 == 0 else 6
     return 0
 
 

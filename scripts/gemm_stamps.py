@@ -15,7 +15,7 @@ for (N, K) in [(2304, 768), (768, 3072)]:
     w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
     b = torch.randn(N, device="cuda")
     y = torch.empty(T, N, device="cuda", dtype=torch.bfloat16)
-    for tile, (BM, BN) in [(0, (128, 128)), (6, (256, 256))]:
+    for tile, (BM, BN) in [(6, (256, 256)), (12, (256, 256))]:
         nb = ((T + BM - 1) // BM) * ((N + BN - 1) // BN)
         dbg = torch.zeros(nb * 4, dtype=torch.int64, device="cuda")
         args = (x, True, w, True, y, T, N, K, 0, b, None, None, 0, None, 0, 0, 0, None, 0, 0.0, 0, tile)

@@ -104,10 +104,15 @@ def check_gemm_wgrad(T, N, K, tile=0):
     return (f"gemm_wgrad T{T} N{N} K{K} t{tile}", rel_err(out, ref), 5e-3)
 
 
-def check_gemm_dropout(M=512, N=256, K=128, p=0.1):
+def check_gemm_dropout(M=512, N=256, K=128, p=0.1, tile=None):
     x, w = bf(torch.ones(M, K, device=DEV)), bf(torch.full((N, K), 1.0 / K, device=DEV))
     seed = torch.tensor([12345], dtype=torch.int64, device=DEV)
-    y = G.linear_fwd(x, w, None, drop=(seed, 7 << 32, p))
+    old = G._FORCE_TILE
+    G._FORCE_TILE = None if tile is None else str(tile)
+    try:
+        y = G.linear_fwd(x, w, None, drop=(seed, 7 << 32, p))
+    finally:
+        G._FORCE_TILE = old
     keep = (y.float() != 0)
     rate = 1 - keep.float().mean().item()
     scale_ok = abs(y.float()[keep].mean().item() - 1.0 / (1 - p)) < 1e-2
@@ -117,7 +122,7 @@ def check_gemm_dropout(M=512, N=256, K=128, p=0.1):
     G.bias_grad(bf(torch.ones(M, N, device=DEV)), db, drop=(seed, 7 << 32, p), dz=dz)
     same = torch.equal(dz.float() != 0, keep)
     err = abs(rate - p) + (0 if scale_ok else 1) + (0 if same else 1)
-    return ("dropout rate/scale/fwd-bwd mask", err, 1e-2)
+    return (f"dropout rate/scale/fwd-bwd mask tile{tile}", err, 1e-2)
 
 
 # ----------------------------------------------------------------------------- LayerNorm
@@ -256,7 +261,7 @@ def check_vit_fused_vs_reference(B=4, train=False, **over):
 
 def all_checks() -> List[Callable]:
     c = []
-    for tile in (0, 6, 9, 10):
+    for tile in (0, 6, 12):
         c.append(lambda t=tile: check_gemm_fwd(50432 // 16, 768, 768, t))
         c.append(lambda t=tile: check_gemm_fwd(197 * 3, 2304, 768, t, True, True))
         c.append(lambda t=tile: check_gemm_gelu(197 * 2, 3072, 768, t))
@@ -264,11 +269,14 @@ def all_checks() -> List[Callable]:
         c.append(lambda t=tile: check_gemm_dgrad(197 * 3, 768, 2304, t, True))
         c.append(lambda t=tile: check_gemm_wgrad(197 * 5, 768, 3072, t))
     c += [
+        lambda: check_gemm_fwd(777, 2304, 3072, 12, True, True),
+        lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
         lambda: check_gemm_fwd(100, 64, 128, 0, True, True),
         lambda: check_gemm_dgelu(394, 768, 3072),
         lambda: check_gemm_dgelu(4096, 768, 3072, True),
         lambda: check_gemm_wgrad(17, 64, 128),
         lambda: check_gemm_dropout(),
+        lambda: check_gemm_dropout(1000, 768, 128, 0.1, 12),
         lambda: check_layernorm(394, 768),
         lambda: check_layernorm(100, 1024),
         lambda: check_layernorm(33, 1280),
