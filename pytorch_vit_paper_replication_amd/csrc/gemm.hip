@@ -947,9 +947,20 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
     }
   }
   if constexpr (EPI == EPI_DGELU) {
-    if (p.colsum && ncol) {
+    if (p.colsum) {
+      // the 8 waves hold partial sums of the same 256 columns (different rows): reduce them in LDS,
+      // then one atomic per column per workgroup (atomics on 3072 bias addresses from ~2400
+      // workgroups contend at L2, so their number matters more than their size)
+      __syncthreads();
+      float* red = (float*)smem;  // [8 waves][256 columns]
+      *(float4*)(red + (tid >> 6) * 256 + 4 * cq) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      __syncthreads();
+      if (tid < 256 && n0 + tid < p.N) {
+        float t = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) atomicAdd(p.colsum + n + q, csum[q]);
+        for (int w = 0; w < 8; ++w) t += red[w * 256 + tid];
+        atomicAdd(p.colsum + n0 + tid, t);
+      }
     }
   }
 }

@@ -105,7 +105,26 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) gw[i][j] = gb[i][j] = gs[i][j] = 0.f;
 
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  // Rows are software-pipelined: the x / dy / dres vectors of the wave's next row are loaded
+  // before the current row's two wave reductions, so HBM latency overlaps the shuffles.
+  const int stride = gridDim.x * 4;
+  uint4 cx[MAXCH], cdy[MAXCH], cr[MAXCH];
+  auto load_row = [&](int row, uint4 (&qx)[MAXCH], uint4 (&qd)[MAXCH], uint4 (&qr)[MAXCH]) {
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch && row < rows) {
+        qx[i] = *(const uint4*)(x + (int64_t)row * x_stride + c * 8);
+        qd[i] = *(const uint4*)(dy + (int64_t)row * dy_stride + c * 8);
+        if (dres) qr[i] = *(const uint4*)(dres + (int64_t)row * dres_stride + c * 8);
+      }
+    }
+  };
+  int row = blockIdx.x * 4 + wave;
+  load_row(row, cx, cdy, cr);
+  for (; row < rows; row += stride) {
+    uint4 nx[MAXCH], ndy[MAXCH], nr[MAXCH];
+    load_row(row + stride, nx, ndy, nr);
     const float mu = mean[row], rs = rstd[row];
     float xh[MAXCH][8], g[MAXCH][8];
     float s1 = 0.f, s2 = 0.f;
@@ -113,19 +132,20 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
     for (int i = 0; i < MAXCH; ++i) {
       const int c = lane + 64 * i;
       if (c < nch) {
-        float xv[8], dv[8];
-        load8(x + (int64_t)row * x_stride + c * 8, xv);
-        load8(dy + (int64_t)row * dy_stride + c * 8, dv);
+        const uint32_t ux[4] = {cx[i].x, cx[i].y, cx[i].z, cx[i].w};
+        const uint32_t ud[4] = {cdy[i].x, cdy[i].y, cdy[i].z, cdy[i].w};
         const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
         const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[i][j] = (xv[j] - mu) * rs;
-          g[i][j] = dv[j] * ww[j];
+          const float xv = bf2f(j & 1 ? ux[j >> 1] >> 16 : ux[j >> 1] & 0xFFFF);
+          const float dv = bf2f(j & 1 ? ud[j >> 1] >> 16 : ud[j >> 1] & 0xFFFF);
+          xh[i][j] = (xv - mu) * rs;
+          g[i][j] = dv * ww[j];
           s1 += g[i][j];
           s2 += g[i][j] * xh[i][j];
-          gw[i][j] += dv[j] * xh[i][j];
-          gb[i][j] += dv[j];
+          gw[i][j] += dv * xh[i][j];
+          gb[i][j] += dv;
         }
       }
     }
@@ -138,10 +158,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (g[i][j] - c1 - xh[i][j] * c2) * rs;
         if (dres) {
-          float r[8];
-          load8(dres + (int64_t)row * dres_stride + c * 8, r);
+          const uint32_t ur[4] = {cr[i].x, cr[i].y, cr[i].z, cr[i].w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) o[j] += bf2f(j & 1 ? ur[j >> 1] >> 16 : ur[j >> 1] & 0xFFFF);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) gs[i][j] += o[j];  // column sums of dx (a fused bias gradient)
@@ -150,6 +169,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
         q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
         *(uint4*)(dx + (int64_t)row * dx_stride + c * 8) = q;
       }
+    }
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      cx[i] = nx[i];
+      cdy[i] = ndy[i];
+      cr[i] = nr[i];
     }
   }
   // block reduction of the dgamma / dbeta / dsum partials, one quantity at a time through a
@@ -202,7 +227,7 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280) return hipErrorInvalidValue;
   int nblk = (rows + 3) / 4;
-  if (nblk > 1024) nblk = 1024;
+  if (nblk > 2048) nblk = 2048;  // 8 blocks (32 waves) per CU; each wave then pipelines ~6 rows
   const dim3 grid(nblk), block(256);
   const int maxch = (D / 8 + 63) / 64;
   switch (maxch) {
