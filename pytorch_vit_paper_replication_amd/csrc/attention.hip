@@ -106,8 +106,12 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
-  const int q0 = blockIdx.x * 64 + wave * 16;
+  // XCD-aware: the query blocks of one (batch, head) get consecutive logical ids on ONE XCD, so its
+  // K/V tiles are fetched into that XCD's L2 once instead of once per query block
+  const int nqb = (N + 63) / 64;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = L / nqb, b = bh / H, h = bh % H;
+  const int q0 = (L % nqb) * 64 + wave * 16;
 
   const uint16_t* base = qkv + (int64_t)b * N * ld;
   const int64_t extent = ((int64_t)(N - 1) * ld + DH) * 2;
@@ -134,6 +138,10 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  // Waves whose 16 queries all lie past N only help stage K/V (no math); the running max is kept
+  // in scaled log2 units so a score costs max + fma + exp + add; keys past N exist only in the last
+  // tile, whose all-invalid 16-key fragments are skipped outright.
+  const bool active = q0 < N;
   for (int t = 0; t < ntiles; ++t) {
     const char* kimg = smem + (t & 1) * 2 * TILE_BYTES;
     const char* vimg = kimg + TILE_BYTES;
@@ -142,50 +150,59 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
       dma_rows<C::NH>(krs, nk, KT, ld, (t + 1) * KT, wave, 4, lane);
       dma_rows<C::NH>(vrs, nk + TILE_BYTES, KT, ld, (t + 1) * KT, wave, 4, lane);
     }
-    // S^T[key][q] for 4 key fragments
-    v4f s[4];
+    if (active) {
+      const int kbase = t * KT;
+      const int nf = min(4, (N - kbase + 15) >> 4);  // 16-key fragments holding a valid key (uniform)
+      // S^T[key][q] for the key fragments
+      v4f s[4];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      s[f] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int f = 0; f < 4; ++f) {
+        s[f] = v4f{0.f, 0.f, 0.f, 0.f};
+        if (f < nf) {
 #pragma unroll
-      for (int ks = 0; ks < C::KS; ++ks) s[f] = mfma16(frag_rows(kimg, KT, 16 * f, ks, lane), qf[ks], s[f]);
-    }
-    const int kbase = t * KT;
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kbase + 16 * f + 4 * g + r;
-        const float v = key < N ? s[f][r] * c : -INFINITY;
-        s[f][r] = v;
-        tmax = fmaxf(tmax, v);
+          for (int ks = 0; ks < C::KS; ++ks) s[f] = mfma16(frag_rows(kimg, KT, 16 * f, ks, lane), qf[ks], s[f]);
+        }
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = exp2f(m_run - m_new);
-    float psum = 0.f;
+      if (kbase + KT > N) {  // tail tile: mask keys >= N
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+        for (int f = 0; f < 4; ++f)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(s[f][r] - m_new);
-        s[f][r] = pv;
-        psum += pv;
+          for (int r = 0; r < 4; ++r)
+            if (kbase + 16 * f + 4 * g + r >= N) s[f][r] = -INFINITY;
       }
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
+      float tmax = s[0][0];
 #pragma unroll
-    for (int e = 0; e < C::NE; ++e) o[e] *= alpha;
-    // O^T[d][q] += V^T[d][key] P^T[key][q]
+      for (int f = 0; f < 4; ++f)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[f][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_run, tmax * c);  // scaled log2 units (c > 0)
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      float psum = 0.f;
 #pragma unroll
-      for (int e = 0; e < C::NE; ++e) {
-        const v8s vf = frag_tr(vimg, KT, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane);
-        o[e] = mfma16(vf, pf, o[e]);
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(s[f][r], c, -m_new));
+          s[f][r] = pv;
+          psum += pv;
+        }
+      l_run = l_run * alpha + psum;
+      m_run = m_new;
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e) o[e] *= alpha;
+      // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk * 2 < nf) {
+          const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
+#pragma unroll
+          for (int e = 0; e < C::NE; ++e) {
+            const v8s vf = frag_tr(vimg, KT, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane);
+            o[e] = mfma16(vf, pf, o[e]);
+          }
+        }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -250,8 +267,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
-  const int kb0 = blockIdx.x * KB;
+  const int nkb = (N + KB - 1) / KB;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);  // key blocks of one (batch, head) share an XCD's L2
+  const int bh = L / nkb, b = bh / H, h = bh % H;
+  const int kb0 = (L % nkb) * KB;
   const int kw0 = kb0 + wave * 32;
 
   // LDS carve: K image [KB][dh] | Q blk [32][dh] | dO blk [32][dh] | dS [32][KB] | lse2[32] | delta[32]
@@ -341,7 +360,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         const float l2 = s_lse[ql], dl = s_del[ql];
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-          const float pv = exp2f(s[a][f][r] * c - l2);
+          const float pv = __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l2));
           s[a][f][r] = pv;
           dp[a][f][r] = pv * (dp[a][f][r] - dl);
         }
@@ -433,7 +452,8 @@ template <int DH>
 static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
                                   int D, float scale, hipStream_t s) {
   using namespace pvr;
-  hipLaunchKernelGGL(attn_fwd_kernel<DH>, dim3((N + 63) / 64, B * H), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
+  // 1-D grid of (B*H) x query blocks, XCD-remapped in-kernel
+  hipLaunchKernelGGL(attn_fwd_kernel<DH>, dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
   return hipGetLastError();
 }
 
@@ -478,7 +498,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb, B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
+  hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
                      nkb > 1 ? dq_acc : nullptr, N, H, D, scale);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
