@@ -788,7 +788,11 @@ hipError_t launch_v3(const GemmParams& p, hipStream_t s) {
 constexpr int PP_BK = 64;
 constexpr int PP_BUF = 2 * 256 * 128;  // A + B image of one K-tile
 
-template <int W>
+// k-contiguous operand half-tile: rows of a [256][64] image (128-B rows), see the layout above.
+// mn-contiguous operand half-tile (wgrad: dY / X are [tokens][features]): its own [64 k][128 col]
+// image (256-B rows, 16-B chunks XOR-swizzled by swz_mn for the transposed reads); image column c
+// is tile row (c >> 6) * 128 + hh * 64 + (c & 63) for A, (c >> 5) * 64 + hh * 32 + (c & 31) for B.
+template <int W, bool AK, bool BKC>
 PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem,
                       int64_t lda, int64_t ldb, int t, int nk, int wave, int lane) {
   char* buf = smem + (t & 1) * PP_BUF;
@@ -799,25 +803,32 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
     const int d = wave + 8 * x;  // 16 wave-instructions of 1 KiB per half-tile
     if constexpr (W == 0 || W == 3) {
       constexpr int hh = W == 3;
-      const int rowb = (2 * (d >> 3) + hh) * 64 + (d & 7) * 8;  // first image row of this instruction
-      const int row = rowb + (lane >> 3);
-      const int c = (lane & 7) ^ swz_k(row);
-      dma16(live ? ars : nul, to_lds(buf + rowb * 128), (uint32_t)(row * lda * 2 + (int64_t)(k0 + c * 8) * 2));
+      if constexpr (AK) {
+        const int rowb = (2 * (d >> 3) + hh) * 64 + (d & 7) * 8;  // first image row of this instruction
+        const int row = rowb + (lane >> 3);
+        const int c = (lane & 7) ^ swz_k(row);
+        dma16(live ? ars : nul, to_lds(buf + rowb * 128), (uint32_t)(row * lda * 2 + (int64_t)(k0 + c * 8) * 2));
+      } else {
+        const int kr = 4 * d + (lane >> 4);
+        const int cl = (lane & 15) ^ swz_mn(kr);  // logical chunk stored at this lane's LDS slot
+        const int m = (cl >> 3) * 128 + hh * 64 + (cl & 7) * 8;
+        dma16(live ? ars : nul, to_lds(buf + hh * 16384 + d * 1024), (uint32_t)(((int64_t)(k0 + kr) * lda + m) * 2));
+      }
     } else {
       constexpr int hh = W == 2;
-      const int rowb = (2 * (d >> 2) + hh) * 32 + (d & 3) * 8;
-      const int row = rowb + (lane >> 3);
-      const int c = (lane & 7) ^ swz_k(row);
-      dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * 2 + (int64_t)(k0 + c * 8) * 2));
+      if constexpr (BKC) {
+        const int rowb = (2 * (d >> 2) + hh) * 32 + (d & 3) * 8;
+        const int row = rowb + (lane >> 3);
+        const int c = (lane & 7) ^ swz_k(row);
+        dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * 2 + (int64_t)(k0 + c * 8) * 2));
+      } else {
+        const int kr = 4 * d + (lane >> 4);
+        const int cl = (lane & 15) ^ swz_mn(kr);
+        const int n = (cl >> 2) * 64 + hh * 32 + (cl & 3) * 8;
+        dma16(live ? brs : nul, to_lds(buf + 256 * 128 + hh * 16384 + d * 1024), (uint32_t)(((int64_t)(k0 + kr) * ldb + n) * 2));
+      }
     }
   }
-}
-
-// issue half-tile h (compile-time kind h & 3)
-template <int KIND>
-PVR_DEV void pp_issue_h(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem,
-                        int64_t lda, int64_t ldb, int t, int nk, int wave, int lane) {
-  pp_issue<KIND>(ars, brs, nul, smem, lda, ldb, t, nk, wave, lane);
 }
 
 PVR_DEV void pp_barrier() {
@@ -826,7 +837,7 @@ PVR_DEV void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int QM, int QN, int RD_A, int RD_B, int KIND, bool SWAP>
+template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool SWAP>
 PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
                       __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
                       int t_issue, int nk, int wave, int lane, int wm, int wn) {
@@ -835,15 +846,25 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (AK)
+          af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+        else
+          af[ii][ks] = read_frag<128, false>(buf + QM * 16384, wm * 64 + 16 * ii, ks, lane);
+      }
   }
   if constexpr (RD_B) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
+      for (int ks = 0; ks < 2; ++ks) {
+        if constexpr (BKC)
+          bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
+        else
+          bf[QN][jj][ks] = read_frag<128, false>(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, ks, lane);
+      }
   }
-  pp_issue_h<KIND>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
+  pp_issue<KIND, AK, BKC>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pp_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -965,7 +986,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   }
 }
 
-template <bool SWAP, int EPI>
+template <bool AK, bool BKC, bool SWAP, int EPI>
 __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -975,12 +996,31 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
   const int tt = xcd_remap(blockIdx.x, ntm * ntn);
   const int m0 = (tt / ntn) * 256, n0 = (tt % ntn) * 256;
-  const int nk = p.K / PP_BK;
+  // split-K (wgrad over tokens): this workgroup reduces k in [kbeg, kend)
+  const int kbeg = blockIdx.z * p.k_split_len;
+  const int kend = min(p.K, kbeg + p.k_split_len);
+  const int nk = (kend - kbeg + PP_BK - 1) / PP_BK;  // k-contiguous operands: K % 64 == 0 (host check)
 
-  const uint16_t* abase = p.A + (int64_t)m0 * p.lda;
-  const uint16_t* bbase = p.B + (int64_t)n0 * p.ldb;
-  const __amdgpu_buffer_rsrc_t ars = make_rsrc(abase, rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda));
-  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bbase, rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb));
+  const uint16_t* abase;
+  uint32_t abytes;
+  if constexpr (AK) {
+    abase = p.A + (int64_t)m0 * p.lda + kbeg;
+    abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg);
+  } else {  // rows past K and columns past M read as zero (range check of the last row)
+    abase = p.A + (int64_t)kbeg * p.lda + m0;
+    abytes = rsrc_bytes((int64_t)(kend - 1) * p.lda + p.M, (int64_t)kbeg * p.lda + m0);
+  }
+  const uint16_t* bbase;
+  uint32_t bbytes;
+  if constexpr (BKC) {
+    bbase = p.B + (int64_t)n0 * p.ldb + kbeg;
+    bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg);
+  } else {
+    bbase = p.B + (int64_t)kbeg * p.ldb + n0;
+    bbytes = rsrc_bytes((int64_t)(kend - 1) * p.ldb + p.N, (int64_t)kbeg * p.ldb + n0);
+  }
+  const __amdgpu_buffer_rsrc_t ars = make_rsrc(abase, abytes);
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bbase, bbytes);
   const __amdgpu_buffer_rsrc_t nul = make_rsrc(abase, 0);
 
   v4f acc[8][4];
@@ -992,12 +1032,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
 
   stamp(p, 0);
   // prologue: half-tiles 0..5 = all of K-tile 0, A0/B0 of K-tile 1
-  pp_issue<0>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<1>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<2>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<3>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<0>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
-  pp_issue<1>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
+  pp_issue<0, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<1, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<2, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<3, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<0, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
+  pp_issue<1, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0 of K-tile 0 landed
   pp_barrier();
   if (wm == 1) pp_barrier();  // group 1 runs one barrier behind
@@ -1006,10 +1046,10 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * PP_BUF;
     // phase P = 4t + ph issues half-tile P + 6 = 4(t+1) + ph + 2
-    pp_phase<0, 0, 1, 1, 2, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
-    pp_phase<0, 1, 0, 1, 3, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
-    pp_phase<1, 1, 1, 0, 0, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
-    pp_phase<1, 0, 0, 0, 1, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
+    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
+    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
@@ -1026,10 +1066,10 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   stamp(p, 3);
 }
 
-template <bool SWAP, int EPI>
+template <bool AK, bool BKC, bool SWAP, int EPI>
 hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
   constexpr int SMEM = 2 * PP_BUF;
-  auto kern = gemm_pp_kernel<SWAP, EPI>;
+  auto kern = gemm_pp_kernel<AK, BKC, SWAP, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -1037,7 +1077,8 @@ hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
     attr_set = true;
   }
   const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
-  hipLaunchKernelGGL(kern, dim3(ntm * ntn), dim3(512), SMEM, s, p);
+  const int nsplit = (p.K + p.k_split_len - 1) / p.k_split_len;
+  hipLaunchKernelGGL(kern, dim3(ntm * ntn, 1, nsplit), dim3(512), SMEM, s, p);
   return hipGetLastError();
 }
 
@@ -1058,8 +1099,9 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     case 10: return launch_v3<128, 256, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 11: return launch_v3<256, 256, 2, 4, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 12:
-      if constexpr (AK && BKC) {
-        if (p.K % PP_BK == 0 && p.k_split_len >= p.K) return launch_pp<SWAP, EPI>(p, s);
+      if constexpr (AK == BKC) {  // k-contiguous pair (fwd / dgrad with W^T) or mn pair (wgrad)
+        if ((!AK || (p.K % PP_BK == 0 && p.k_split_len % PP_BK == 0)) && (AK || p.k_split_len % PP_BK == 0))
+          return launch_pp<AK, BKC, SWAP, EPI>(p, s);
       }
       return launch_v3<256, 256, 2, 4, 4, 2, AK, BKC, SWAP, EPI>(p, s);
     default: return launch_cfg<128, 128, 2, 2, AK, BKC, SWAP, EPI>(p, s);

@@ -27,11 +27,14 @@ def _tile(M: int, N: int, K: int, kind: str) -> int:
     """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
     k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave ping-pong (12; K % 64 == 0, else
     the 4-stage BK=32 ring 6); token-reduced wgrad (both operands mn-contiguous, split-K
-    atomics) -> 128x128 (0)."""
+    atomics) -> the same ping-pong with transposed LDS reads when the token count is large,
+    128x128 (0) otherwise."""
     if _FORCE_TILE is not None:
         return int(_FORCE_TILE)
     if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
         return 12 if K % 64 == 0 else 6
+    if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
+        return 12
     return 0
 
 
@@ -83,7 +86,13 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
     return out
 
 
-def wgrad_splits(T: int, N: int, K: int) -> int:
+def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
+    """Token splits of a weight-gradient GEMM (each split accumulates into dW with f32 atomics).
+    256x256 ping-pong tiles (12): one resident workgroup per CU, so fill the 256 CUs once;
+    128x128 tiles (0): about 1024 workgroups."""
+    if tile == 12:
+        tiles = math.ceil(N / 256) * math.ceil(K / 256)
+        return max(1, min(256 // tiles, max(1, T // 256)))
     tiles = math.ceil(N / 128) * math.ceil(K / 128)
     target = 1024
     s = max(1, round(target / tiles))
@@ -95,10 +104,11 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.
     """out[N, K] += dy^T . x   (fp32, split over tokens with f32 atomics)."""
     T, N = dy.shape
     K = x.shape[1]
-    splits = wgrad_splits(T, N, K)
+    tile = _tile(N, K, T, "wgrad")
+    splits = wgrad_splits(T, N, K, tile)
     ksplit = math.ceil(math.ceil(T / splits) / 64) * 64
     _ext.ext().gemm(dy, False, x, False, out, N, K, T, EPI_F32_ATOMIC, None, None, None, 0, None, 0, 0, 0,
-                    None, 0, 0.0, ksplit, _tile(N, K, T, "wgrad"))
+                    None, 0, 0.0, ksplit, tile)
     return out
 
 

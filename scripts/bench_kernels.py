@@ -68,7 +68,7 @@ def main():
             out = torch.zeros(n, k, device=dev)
             t_lib = timeit(lambda: torch.matmul(dy.t(), x))
             print(f"wgrad {name:4s} N{n} K{k} T{T}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
-            for t in [t for t in tiles if t in (0, 6)]:
+            for t in [t for t in tiles if t in (0, 6, 12)]:
                 G._FORCE_TILE = str(t)
                 tt = timeit(lambda: G.linear_wgrad(dy, x, out))
                 print(f"wgrad {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)

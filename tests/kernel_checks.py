@@ -275,6 +275,8 @@ def all_checks() -> List[Callable]:
         lambda: check_gemm_dgelu(394, 768, 3072),
         lambda: check_gemm_dgelu(4096, 768, 3072, True),
         lambda: check_gemm_wgrad(17, 64, 128),
+        lambda: check_gemm_wgrad(3000, 768, 2304, 12),
+        lambda: check_gemm_wgrad(1000, 304, 200, 12),
         lambda: check_gemm_dropout(),
         lambda: check_gemm_dropout(1000, 768, 128, 0.1, 12),
         lambda: check_layernorm(394, 768),
