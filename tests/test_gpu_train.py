@@ -165,3 +165,29 @@ def test_native_communicator_collectives_world1():
         c.destroy()
     finally:
         dist.destroy_process_group()
+
+
+def test_feature_extractor_fused_gpu():
+    """Frozen backbone + new head on the fused path: only the head moves (MAIN.ipynb:4111-4130)."""
+    from pytorch_vit_paper_replication_amd.models import ViT, feature_extractor
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    m = feature_extractor(ViT(**CFG), num_classes=3, seed=0).cuda()
+    frozen = {n: p.detach().clone() for n, p in m.named_parameters() if not p.requires_grad}
+    head0 = m.classifier[0].weight.detach().clone()
+    opt = FusedAdam([p for p in m.parameters() if p.requires_grad], lr=1e-2)
+    x = torch.rand(8, 3, 64, 64, device="cuda")
+    y = torch.randint(0, 3, (8,), device="cuda")
+    for _ in range(3):
+        loss = cross_entropy(m(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step(clip_norm=1.0)
+    torch.cuda.synchronize()
+    assert getattr(m, "_pvr_store", None) is not None
+    assert not torch.equal(m.classifier[0].weight, head0)
+    for n, p in m.named_parameters():
+        if n in frozen:
+            assert torch.equal(p, frozen[n]), n
