@@ -141,7 +141,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (random [B,3,224,224] in [0,1), 1000 classes, random-init weights)",
+            "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
+                    "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
                        "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl,
                        "grad_transport": net.transport if use_ddp else "none",
