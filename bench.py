@@ -33,6 +33,8 @@ def parse():
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--num-classes", type=int, default=1000)
     p.add_argument("--impl", choices=["fused", "torch"], default="fused")
+    p.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                   help="fp8: encoder forward GEMMs in e4m3 with delayed scaling (ViT-H/14 fp8 config)")
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
     p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
     p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
@@ -66,6 +68,8 @@ def main():
     torch.manual_seed(1234)
 
     model = vit(args.model, image_size=args.image_size, num_classes=args.num_classes).to(device)
+    if args.dtype == "fp8":
+        model.enable_fp8()
     groups = param_groups_weight_decay(model, 0.03)
     total_steps = args.warmup + args.steps
     if args.impl == "fused":
@@ -129,8 +133,8 @@ def main():
     if rank == 0:
         out = {
             "metric": ("images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
-                       if (name, args.image_size) == ("ViT-B/16", 224)
-                       else f"images/sec (whole node) {name} {args.image_size}px bf16"),
+                       if (name, args.image_size, args.dtype) == ("ViT-B/16", 224, "bf16")
+                       else f"images/sec (whole node) {name} {args.image_size}px {args.dtype}"),
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -140,7 +144,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if args.dtype == "bf16" else "fp8 (e4m3 forward GEMMs; bf16 backward/attention/norms)",
             "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,

@@ -25,6 +25,8 @@ struct GemmParams {
   int tile_cfg;
   uint64_t* dbg;
   float* colsum;
+  const float* scale_a; const float* scale_b;
+  int elem8, fmt_a, fmt_b;
 };
 struct AdamGroup {
   float lr, beta1, beta2, eps, weight_decay;
@@ -48,6 +50,9 @@ int pvr_norm_partial_blocks();
 hipError_t pvr_grad_norm(const float*, int64_t, float, float*, float*, hipStream_t);
 hipError_t pvr_adam(float*, const float*, float*, float*, uint16_t*, int64_t, const int64_t*, const int*, int, const pvr::AdamGroup*, const float*, int, hipStream_t);
 hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
+hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, int, const float*, unsigned*, int, hipStream_t);
+hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
+hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
 }
@@ -269,6 +274,89 @@ void scale_by_clip(torch::Tensor g, torch::Tensor clip) {
   check(pvr_scale_by_clip(f32_mut(g, "g"), g.numel(), f32(clip, "clip"), stream()), "scale_by_clip");
 }
 
+const uint8_t* u8(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kUInt8, name, " must hold fp8 bytes (uint8), got ", t.scalar_type());
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.stride(0) % 16 == 0, name, " must be 2-D with a 16-byte multiple row stride");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+  return reinterpret_cast<const uint8_t*>(t.data_ptr());
+}
+
+// C[M][N] = epilogue(dscale_a * dscale_b * A[M][K] . B[N][K]^T), A/B OCP fp8 (fmt 0 e4m3, 1 e5m2)
+void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, torch::Tensor C, int64_t M, int64_t N, int64_t K,
+              int64_t epi, torch::Tensor scale_a, torch::Tensor scale_b, c10::optional<torch::Tensor> bias,
+              c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> seed, int64_t seed_offset,
+              double drop_p, c10::optional<torch::Tensor> colsum) {
+  pvr::GemmParams p{};
+  p.drop_scale = 1.f;
+  p.M = (int)M; p.N = (int)N; p.K = (int)K;
+  p.A = reinterpret_cast<const uint16_t*>(u8(A, "A")); p.lda = A.stride(0); p.a_kcontig = 1;
+  p.B = reinterpret_cast<const uint16_t*>(u8(B, "B")); p.ldb = B.stride(0); p.b_kcontig = 1;
+  TORCH_CHECK(A.size(0) >= M && A.size(1) >= K && B.size(0) >= N && B.size(1) >= K, "gemm_fp8: operand too small");
+  TORCH_CHECK(K % 128 == 0 && N % 8 == 0, "gemm_fp8: K must be a multiple of 128, N of 8");
+  TORCH_CHECK(C.is_cuda() && C.scalar_type() == torch::kBFloat16, "gemm_fp8: bf16 output");
+  p.C = C.data_ptr(); p.ldc = ld_of(C, "C");
+  p.scale_a = f32(scale_a, "scale_a"); p.scale_b = f32(scale_b, "scale_b");
+  p.elem8 = 1; p.fmt_a = (int)fmt_a; p.fmt_b = (int)fmt_b;
+  if (bias.has_value() && bias->defined()) { TORCH_CHECK(bias->numel() >= N && bias->is_contiguous(), "bias"); p.bias = f32(*bias, "bias"); }
+  if (resid.has_value() && resid->defined()) { p.resid = bf(*resid, "resid"); p.ld_resid = ld_of(*resid, "resid"); }
+  if (aux.has_value() && aux->defined()) { p.aux = const_cast<uint16_t*>(bf(*aux, "aux")); p.ld_aux = ld_of(*aux, "aux"); }
+  if (epi == 1 || epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm_fp8: GELU epilogues need aux");
+  if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
+  if (drop_p > 0.0) {
+    TORCH_CHECK(seed.has_value() && seed->defined() && seed->scalar_type() == torch::kInt64, "dropout needs an int64 seed tensor");
+    p.seed_ptr = reinterpret_cast<const uint64_t*>(seed->data_ptr());
+    p.seed_offset = (uint64_t)seed_offset;
+    uint32_t thr = (uint32_t)llround(drop_p * 65536.0);
+    if (thr > 65535) thr = 65535;
+    p.drop_thr = thr;
+    p.drop_scale = (float)(65536.0 / (65536.0 - thr));
+  }
+  p.k_split_len = (int)K;
+  p.epi = (int)epi;
+  p.tile_cfg = 12;
+  check(pvr_gemm(&p, stream()), "gemm_fp8");
+}
+
+// y[rows][cols] (uint8 fp8) = sat(x * qscale); amax (int32 holding float bits) = max(amax, max|x|).
+// y / qscale None: amax only.
+void fp8_quant(torch::Tensor x, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> qscale, torch::Tensor amax, int64_t fmt) {
+  const uint16_t* xp = bf(x, "x");
+  const int64_t ldx = ld_of(x, "x");
+  uint8_t* yp = nullptr;
+  int64_t ldy = 0;
+  if (y.has_value() && y->defined()) {
+    yp = const_cast<uint8_t*>(u8(*y, "y"));
+    ldy = y->stride(0);
+    TORCH_CHECK(y->size(0) == x.size(0) && y->size(1) == x.size(1), "fp8_quant: shape mismatch");
+  }
+  TORCH_CHECK(amax.is_cuda() && amax.scalar_type() == torch::kInt32 && amax.numel() >= 1, "fp8_quant: amax int32");
+  const float* qs = nullptr;
+  if (qscale.has_value() && qscale->defined()) qs = f32(*qscale, "qscale");
+  TORCH_CHECK(yp == nullptr || qs != nullptr, "fp8_quant: y needs qscale");
+  check(pvr_fp8_quant(xp, ldx, yp, ldy, x.size(0), (int)x.size(1), qs, reinterpret_cast<unsigned*>(amax.data_ptr()), (int)fmt, stream()),
+        "fp8_quant");
+}
+
+torch::Tensor fp8_dequant(torch::Tensor x, c10::optional<torch::Tensor> dscale, int64_t fmt) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous(), "fp8_dequant: contiguous uint8");
+  auto y = torch::empty(x.sizes(), x.options().dtype(torch::kFloat32));
+  const float* ds = nullptr;
+  if (dscale.has_value() && dscale->defined()) ds = f32(*dscale, "dscale");
+  check(pvr_fp8_dequant(x.data_ptr<uint8_t>(), y.data_ptr<float>(), x.numel(), ds, (int)fmt, stream()), "fp8_dequant");
+  return y;
+}
+
+void fp8_scale_update(torch::Tensor hist, torch::Tensor amax, torch::Tensor qscale, torch::Tensor dscale, torch::Tensor fmax, int64_t s0,
+                      int64_t s1, double margin_mul) {
+  TORCH_CHECK(hist.dim() == 2 && hist.is_contiguous(), "hist [n][H]");
+  TORCH_CHECK(amax.scalar_type() == torch::kInt32, "amax int32");
+  TORCH_CHECK(s0 >= 0 && s1 <= hist.size(0), "slot range");
+  check(pvr_fp8_scale_update(f32_mut(hist, "hist"), (int)hist.size(1), reinterpret_cast<unsigned*>(amax.data_ptr()), f32_mut(qscale, "qscale"),
+                             f32_mut(dscale, "dscale"), f32(fmax, "fmax"), (int)s0, (int)s1, (float)margin_mul, stream()),
+        "fp8_scale_update");
+}
+
 std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int64_t H, double scale) {
   const int64_t D = qkv.size(1) / 3;
   auto out = torch::empty({B * N, D}, qkv.options());
@@ -319,6 +407,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_partial_blocks", []() { return pvr_norm_partial_blocks(); });
   m.def("adam", &adam);
   m.def("scale_by_clip", &scale_by_clip);
+  m.def("gemm_fp8", &gemm_fp8, py::arg("A"), py::arg("fmt_a"), py::arg("B"), py::arg("fmt_b"), py::arg("C"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("scale_a"), py::arg("scale_b"), py::arg("bias") = py::none(),
+        py::arg("resid") = py::none(), py::arg("aux") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0,
+        py::arg("drop_p") = 0.0, py::arg("colsum") = py::none());
+  m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
+  m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
+  m.def("fp8_scale_update", &fp8_scale_update);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("arch", []() { return std::string("gfx950"); });

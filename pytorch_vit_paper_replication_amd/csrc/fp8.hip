@@ -1,0 +1,140 @@
+// fp8 quantization for the ViT-H/14 fp8 training config (BASELINE.json config 5, SURVEY.md §7.2
+// step 9): bf16 activations / weights -> OCP fp8 (e4m3 forward operands, e5m2 gradients) with
+// per-tensor scales, and the delayed-scaling bookkeeping (amax history -> scale) kept entirely on
+// the device so a training step never synchronises with the host.
+//
+//   quant:  y = sat(x * qscale) in fp8,  amax = max(amax, max|x|)   (one pass; qscale == null:
+//           amax only, used to calibrate a tensor the first time it is seen / for weights)
+//   update: per tensor slot, push amax into a history ring, qscale = fmax / max(history) / 2^margin,
+//           dscale = 1 / qscale (the GEMM epilogue's dequant factor), reset amax
+#include "common.h"
+
+namespace pvr {
+namespace {
+
+template <int FMT, bool HI>
+PVR_DEV int pack2_fp8(float a, float b, int old) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;  // OCP e4m3fn / e5m2 largest finite
+  a = fminf(fmaxf(a, -FMAX), FMAX);
+  b = fminf(fmaxf(b, -FMAX), FMAX);
+  if constexpr (FMT == 0)
+    return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
+  else
+    return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
+}
+
+// 16 elements (two 16-B bf16 loads, one 16-B fp8 store) per thread and grid-stride step.
+template <int FMT>
+__global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__ x, int64_t ldx, uint8_t* __restrict__ y, int64_t ldy,
+                                                    int64_t rows, int cols, const float* __restrict__ qscale,
+                                                    unsigned* __restrict__ amax) {
+  const int per_row = cols >> 4;
+  const int64_t n = rows * per_row;
+  const float qs = qscale ? *qscale : 1.f;
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / per_row;
+    const int c = (int)(i % per_row) * 16;
+    const uint16_t* src = x + r * ldx + c;
+    const uint4 u0 = *(const uint4*)src, u1 = *(const uint4*)(src + 8);
+    const uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[2 * j] = bf2f(w[j] & 0xFFFF);
+      v[2 * j + 1] = bf2f(w[j] >> 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[j]));
+    if (y) {
+      int o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int t = pack2_fp8<FMT, false>(v[4 * q] * qs, v[4 * q + 1] * qs, 0);
+        o[q] = pack2_fp8<FMT, true>(v[4 * q + 2] * qs, v[4 * q + 3] * qs, t);
+      }
+      *(int4*)(y + r * ldy + c) = make_int4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  // one same-address atomic per BLOCK: those serialise at L2 (~12 ns each), so the grid is capped
+  // at 256 blocks and the 4 waves reduce through LDS first
+  __shared__ float wm[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float b = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    if (b > 0.f) atomicMax(amax, __float_as_uint(b));  // |x| bits order like uints
+  }
+}
+
+// fp8 -> f32 (tests / debugging): y[i] = dscale * x[i]
+template <int FMT>
+__global__ void dequant_kernel(const uint8_t* __restrict__ x, float* __restrict__ y, int64_t n, const float* __restrict__ dscale) {
+  const float ds = dscale ? *dscale : 1.f;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int word = x[i];
+    float f;
+    if constexpr (FMT == 0)
+      f = __builtin_amdgcn_cvt_f32_fp8(word, 0);
+    else
+      f = __builtin_amdgcn_cvt_f32_bf8(word, 0);
+    y[i] = f * ds;
+  }
+}
+
+__global__ void scale_update_kernel(float* __restrict__ hist, int H, unsigned* __restrict__ amax, float* __restrict__ qscale,
+                                    float* __restrict__ dscale, const float* __restrict__ fmax, int s0, int s1, float margin_mul) {
+  const int i = s0 + blockIdx.x * 64 + threadIdx.x;
+  if (i >= s1) return;
+  float* h = hist + (int64_t)i * H;
+  const float cur = __uint_as_float(amax[i]);
+  float m = cur;
+  for (int k = H - 1; k > 0; --k) {
+    h[k] = h[k - 1];
+    m = fmaxf(m, h[k]);
+  }
+  h[0] = cur;
+  const float q = m > 0.f ? fmax[i] / m * margin_mul : 1.f;
+  qscale[i] = q;
+  dscale[i] = 1.f / q;
+  amax[i] = 0u;
+}
+
+}  // namespace
+}  // namespace pvr
+
+extern "C" hipError_t pvr_fp8_quant(const uint16_t* x, int64_t ldx, uint8_t* y, int64_t ldy, int64_t rows, int cols, const float* qscale,
+                                    unsigned* amax, int fmt, hipStream_t s) {
+  using namespace pvr;
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (cols % 16) return hipErrorInvalidValue;
+  int64_t blocks = (rows * (cols / 16) + 255) / 256;
+  if (blocks > 256) blocks = 256;  // one resident block per CU, grid-stride over the tensor
+  if (fmt == 0)
+    hipLaunchKernelGGL(quant_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, x, ldx, y, ldy, rows, cols, qscale, amax);
+  else
+    hipLaunchKernelGGL(quant_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, x, ldx, y, ldy, rows, cols, qscale, amax);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_fp8_dequant(const uint8_t* x, float* y, int64_t n, const float* dscale, int fmt, hipStream_t s) {
+  using namespace pvr;
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (fmt == 0)
+    hipLaunchKernelGGL(dequant_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, x, y, n, dscale);
+  else
+    hipLaunchKernelGGL(dequant_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, x, y, n, dscale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_fp8_scale_update(float* hist, int H, unsigned* amax, float* qscale, float* dscale, const float* fmax, int s0,
+                                           int s1, float margin_mul, hipStream_t s) {
+  using namespace pvr;
+  if (s1 <= s0) return hipSuccess;
+  hipLaunchKernelGGL(scale_update_kernel, dim3((s1 - s0 + 63) / 64), dim3(64), 0, s, hist, H, amax, qscale, dscale, fmax, s0, s1,
+                     margin_mul);
+  return hipGetLastError();
+}

@@ -46,6 +46,10 @@ struct GemmParams {
   int tile_cfg;
   uint64_t* dbg;  // diagnostic s_memtime stamps [block][4] (null in normal runs)
   float* colsum;  // optional: += column sums of the bf16-type output (a fused bias gradient)
+  // fp8 operands (elem8 = 1): A / B hold 1-byte OCP fp8 (fmt 0 = e4m3, 1 = e5m2), lda / ldb in
+  // bytes; the accumulator is multiplied by (*scale_a) * (*scale_b) (per-tensor dequant factors)
+  const float* scale_a; const float* scale_b;
+  int elem8, fmt_a, fmt_b;
 };
 
 namespace {
@@ -154,6 +158,7 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
   if constexpr (SWAP) {
     // lane holds C[m = mb + 16i + li][n = nb + 16j + 4g + r], r = 0..3 (4 consecutive columns)
     const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
+    const float deq = p.scale_a ? (*p.scale_a) * (*p.scale_b) : 1.f;
     float4 bias[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -178,7 +183,7 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
         for (int j = 0; j < FN; ++j) {
           const int n = nb + 16 * j + 4 * g;
           if (n >= p.N) continue;
-          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          float v[4] = {acc[i][j][0] * deq, acc[i][j][1] * deq, acc[i][j][2] * deq, acc[i][j][3] * deq};
           bool keep[4] = {true, true, true, true};
           if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
             if (p.drop_thr) {
@@ -792,11 +797,13 @@ constexpr int PP_BUF = 2 * 256 * 128;  // A + B image of one K-tile
 // mn-contiguous operand half-tile (wgrad: dY / X are [tokens][features]): its own [64 k][128 col]
 // image (256-B rows, 16-B chunks XOR-swizzled by swz_mn for the transposed reads); image column c
 // is tile row (c >> 6) * 128 + hh * 64 + (c & 63) for A, (c >> 5) * 64 + hh * 32 + (c & 31) for B.
-template <int W, bool AK, bool BKC>
+template <int W, bool AK, bool BKC, int ES>
 PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem,
                       int64_t lda, int64_t ldb, int t, int nk, int wave, int lane) {
+  static_assert(ES == 2 || (ES == 1 && AK && BKC), "fp8 operands: k-contiguous only");
   char* buf = smem + (t & 1) * PP_BUF;
-  const int k0 = t * PP_BK;
+  const int k0 = t * PP_BK;   // bf16 element offset (mn path)
+  const int kb = t * 128;     // byte offset of this K-tile within a k-contiguous row (64 bf16 / 128 fp8)
   const bool live = t < nk;
 #pragma unroll
   for (int x = 0; x < 2; ++x) {
@@ -807,7 +814,7 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
         const int rowb = (2 * (d >> 3) + hh) * 64 + (d & 7) * 8;  // first image row of this instruction
         const int row = rowb + (lane >> 3);
         const int c = (lane & 7) ^ swz_k(row);
-        dma16(live ? ars : nul, to_lds(buf + rowb * 128), (uint32_t)(row * lda * 2 + (int64_t)(k0 + c * 8) * 2));
+        dma16(live ? ars : nul, to_lds(buf + rowb * 128), (uint32_t)(row * lda * ES + kb + c * 16));
       } else {
         const int kr = 4 * d + (lane >> 4);
         const int cl = (lane & 15) ^ swz_mn(kr);  // logical chunk stored at this lane's LDS slot
@@ -820,7 +827,7 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
         const int rowb = (2 * (d >> 2) + hh) * 32 + (d & 3) * 8;
         const int row = rowb + (lane >> 3);
         const int c = (lane & 7) ^ swz_k(row);
-        dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * 2 + (int64_t)(k0 + c * 8) * 2));
+        dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * ES + kb + c * 16));
       } else {
         const int kr = 4 * d + (lane >> 4);
         const int cl = (lane & 15) ^ swz_mn(kr);
@@ -837,7 +844,28 @@ PVR_DEV void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool SWAP>
+// fp8 fragment half h of a 16 x 128 (k) operand tile: lane (row r0 + (l&15)) gets bytes
+// 32 (l>>4) + 16 h .. +15 of its 128-B row; A and B use the same read, so the k order the MFMA
+// assigns to the 32 bytes of a lane is the same for both operands.
+PVR_DEV v8s frag_fp8(const char* img, int r0, int h, int lane) {
+  const int row = r0 + (lane & 15);
+  const int c = 2 * (lane >> 4) + h;
+  return ds_read_b128(img + row * 128 + ((c ^ swz_k(row)) << 4));
+}
+
+template <int FA, int FB>
+PVR_DEV v4f mfma_fp8(const v8s& a0, const v8s& a1, const v8s& b0, const v8s& b1, v4f c) {
+  typedef int v8i __attribute__((ext_vector_type(8)));
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i x0 = __builtin_bit_cast(v4i, a0), x1 = __builtin_bit_cast(v4i, a1);
+  const v4i y0 = __builtin_bit_cast(v4i, b0), y1 = __builtin_bit_cast(v4i, b1);
+  const v8i a = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  const v8i b = {y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+  // scale operands 127 = 2^0 in E8M0: per-tensor dequant happens in the epilogue
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, 127, 0, 127);
+}
+
+template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool SWAP, int ES = 2, int FA = 0, int FB = 0>
 PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
                       __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
                       int t_issue, int nk, int wave, int lane, int wm, int wn) {
@@ -847,7 +875,9 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        if constexpr (AK)
+        if constexpr (ES == 1)
+          af[ii][ks] = frag_fp8(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+        else if constexpr (AK)
           af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
         else
           af[ii][ks] = read_frag<128, false>(buf + QM * 16384, wm * 64 + 16 * ii, ks, lane);
@@ -858,17 +888,34 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        if constexpr (BKC)
+        if constexpr (ES == 1)
+          bf[QN][jj][ks] = frag_fp8(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
+        else if constexpr (BKC)
           bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
         else
           bf[QN][jj][ks] = read_frag<128, false>(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, ks, lane);
       }
   }
-  pp_issue<KIND, AK, BKC>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
+  pp_issue<KIND, AK, BKC, ES>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pp_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_setprio(1);
+  if constexpr (ES == 1) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        v4f& c = acc[QM * 4 + ii][QN * 2 + jj];
+        if constexpr (SWAP)
+          c = mfma_fp8<FB, FA>(bf[QN][jj][0], bf[QN][jj][1], af[ii][0], af[ii][1], c);
+        else
+          c = mfma_fp8<FA, FB>(af[ii][0], af[ii][1], bf[QN][jj][0], bf[QN][jj][1], c);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+    return;
+  }
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -904,6 +951,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
     if (p.bias && ncol) bias = *(const float4*)(p.bias + n);
   }
   const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
+  const float deq = p.scale_a ? (*p.scale_a) * (*p.scale_b) : 1.f;
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -925,7 +973,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
       const int m = m0 + half * 128 + r;
       const v4f a = *(const v4f*)(smem + r * 1024 + ((cq ^ (r & 63)) << 4));
       if (m >= p.M || !ncol) continue;
-      float v[4] = {a[0], a[1], a[2], a[3]};
+      float v[4] = {a[0] * deq, a[1] * deq, a[2] * deq, a[3] * deq};
       if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
         v[0] += bias.x; v[1] += bias.y; v[2] += bias.z; v[3] += bias.w;
         bool keep[4] = {true, true, true, true};
@@ -986,7 +1034,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   }
 }
 
-template <bool AK, bool BKC, bool SWAP, int EPI>
+template <bool AK, bool BKC, bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
 __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -999,20 +1047,29 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   // split-K (wgrad over tokens): this workgroup reduces k in [kbeg, kend)
   const int kbeg = blockIdx.z * p.k_split_len;
   const int kend = min(p.K, kbeg + p.k_split_len);
-  const int nk = (kend - kbeg + PP_BK - 1) / PP_BK;  // k-contiguous operands: K % 64 == 0 (host check)
+  constexpr int BKE = 128 / ES;  // K-tile depth in elements (64 bf16 / 128 fp8)
+  const int nk = (kend - kbeg + BKE - 1) / BKE;  // k-contiguous operands: K % BKE == 0 (host check)
 
-  const uint16_t* abase;
+  const void* abase;
   uint32_t abytes;
-  if constexpr (AK) {
+  if constexpr (ES == 1) {
+    const uint8_t* a8 = (const uint8_t*)p.A;
+    abase = a8 + (int64_t)m0 * p.lda + kbeg;
+    abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg) / 2;
+  } else if constexpr (AK) {
     abase = p.A + (int64_t)m0 * p.lda + kbeg;
     abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg);
   } else {  // rows past K and columns past M read as zero (range check of the last row)
     abase = p.A + (int64_t)kbeg * p.lda + m0;
     abytes = rsrc_bytes((int64_t)(kend - 1) * p.lda + p.M, (int64_t)kbeg * p.lda + m0);
   }
-  const uint16_t* bbase;
+  const void* bbase;
   uint32_t bbytes;
-  if constexpr (BKC) {
+  if constexpr (ES == 1) {
+    const uint8_t* b8 = (const uint8_t*)p.B;
+    bbase = b8 + (int64_t)n0 * p.ldb + kbeg;
+    bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg) / 2;
+  } else if constexpr (BKC) {
     bbase = p.B + (int64_t)n0 * p.ldb + kbeg;
     bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg);
   } else {
@@ -1032,12 +1089,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
 
   stamp(p, 0);
   // prologue: half-tiles 0..5 = all of K-tile 0, A0/B0 of K-tile 1
-  pp_issue<0, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<1, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<2, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<3, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
-  pp_issue<0, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
-  pp_issue<1, AK, BKC>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
+  pp_issue<0, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<1, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<2, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<3, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
+  pp_issue<0, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
+  pp_issue<1, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 1, nk, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0 of K-tile 0 landed
   pp_barrier();
   if (wm == 1) pp_barrier();  // group 1 runs one barrier behind
@@ -1046,10 +1103,10 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * PP_BUF;
     // phase P = 4t + ph issues half-tile P + 6 = 4(t+1) + ph + 2
-    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
-    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
-    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
-    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
+    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
+    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
@@ -1066,10 +1123,10 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   stamp(p, 3);
 }
 
-template <bool AK, bool BKC, bool SWAP, int EPI>
+template <bool AK, bool BKC, bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
 hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
   constexpr int SMEM = 2 * PP_BUF;
-  auto kern = gemm_pp_kernel<AK, BKC, SWAP, EPI>;
+  auto kern = gemm_pp_kernel<AK, BKC, SWAP, EPI, ES, FA, FB>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -1118,6 +1175,23 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
   const GemmParams& p = *pp;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return hipSuccess;
   const bool ak = p.a_kcontig, bk = p.b_kcontig;
+  if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad e5m2 x e4m3)
+    if (!ak || !bk || p.K % 128 != 0 || p.k_split_len < p.K || (p.N & 3) || !p.scale_a || !p.scale_b) return hipErrorInvalidValue;
+    const int f = p.fmt_a * 2 + p.fmt_b;
+    switch (p.epi) {
+      case EPI_BF16:
+        if (f == 0) return launch_pp<true, true, true, EPI_BF16, 1, 0, 0>(p, s);
+        if (f == 2) return launch_pp<true, true, true, EPI_BF16, 1, 1, 0>(p, s);
+        break;
+      case EPI_GELU:
+        if (f == 0) return launch_pp<true, true, true, EPI_GELU, 1, 0, 0>(p, s);
+        break;
+      case EPI_DGELU:
+        if (f == 2) return launch_pp<true, true, true, EPI_DGELU, 1, 1, 0>(p, s);
+        break;
+    }
+    return hipErrorInvalidValue;
+  }
   switch (p.epi) {
     case EPI_BF16:
       if (ak && bk) return launch_tile<true, true, true, EPI_BF16>(p, s);

@@ -259,6 +259,9 @@ class ViT(nn.Module):
                                     conv.weight, conv.bias, pe.class_token, pe.position_embedding)
         B = x.shape[0]
         N = pe.number_of_patches + 1
+        f8 = self._fp8_state(dev, B * N)
+        if f8 is not None:
+            f8.begin_step(training)
         for i, blk in enumerate(self.transformer_encoder):
             ln1 = blk.msa_block.layer_norm
             ln2 = blk.mlp_block.layer_norm
@@ -266,10 +269,34 @@ class ViT(nn.Module):
             p2 = blk.mlp_block.mlp[4].p
             tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads, ln1.eps, ln2.eps,
                                           store, site_drop(seed, 1 + 2 * i, p1, training),
-                                          site_drop(seed, 2 + 2 * i, p2, training), *blk.fused_params())
+                                          site_drop(seed, 2 + 2 * i, p2, training),
+                                          None if f8 is None else (f8, i), *blk.fused_params())
         head = self.classifier[0]
         return HeadFn.apply(tokens, B, N, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias,
                             head.weight, head.bias)
+
+    # ------------------------------------------------------------------ fp8
+    def enable_fp8(self, enabled: bool = True, history: int = 16, margin: int = 0) -> "ViT":
+        """Run the encoder's forward GEMMs in fp8 (e4m3, per-tensor delayed scaling) on the fused
+        MI355X path (ops/fp8.py). The constructor signature stays the reference's; this is opt-in."""
+        object.__setattr__(self, "_fp8_cfg", (history, margin) if enabled else None)
+        object.__setattr__(self, "_fp8", None)
+        return self
+
+    def _fp8_state(self, device, tokens: int):
+        cfg = getattr(self, "_fp8_cfg", None)
+        if cfg is None:
+            return None
+        from ..ops import fp8 as F8
+
+        c = self.config
+        if not F8.supported(tokens, c["embedding_dim"], c["mlp_size"]):
+            return None
+        st = getattr(self, "_fp8", None)
+        if st is None or st.device != device:
+            st = F8.Fp8State(c["num_transformer_layer"], device, history=cfg[0], margin=cfg[1])
+            object.__setattr__(self, "_fp8", st)
+        return st
 
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())

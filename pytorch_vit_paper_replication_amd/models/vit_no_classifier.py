@@ -51,11 +51,14 @@ class ViT(_FullViT):
         tokens = PatchEmbedFn.apply(x, c["patch_size"], store, seed, pe.dropout.p, training,
                                     conv.weight, conv.bias, pe.class_token, pe.position_embedding)
         B, N = x.shape[0], pe.number_of_patches + 1
+        f8 = self._fp8_state(dev, B * N)
+        if f8 is not None:
+            f8.begin_step(training)
         for i, blk in enumerate(self.transformer_encoder):
             tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads,
                                           blk.msa_block.layer_norm.eps, blk.mlp_block.layer_norm.eps, store,
                                           site_drop(seed, 1 + 2 * i, blk.mlp_block.mlp[2].p, training),
                                           site_drop(seed, 2 + 2 * i, blk.mlp_block.mlp[4].p, training),
-                                          *blk.fused_params())
+                                          None if f8 is None else (f8, i), *blk.fused_params())
         y = TokenLayerNormFn.apply(tokens, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias)
         return y.float().view(B, N, -1)

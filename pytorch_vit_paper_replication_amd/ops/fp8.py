@@ -1,0 +1,133 @@
+"""fp8 (OCP e4m3 / e5m2) GEMM path with per-tensor delayed scaling (SURVEY.md §7.2 step 9,
+BASELINE.json config 5: ViT-H/14 fp8).
+
+Recipe (the usual delayed-scaling scheme, all state on the device):
+  * every quantized tensor has a slot: amax history (ring of ``history`` steps), quant scale
+    ``qscale = fmax / max(history) * 2^-margin`` and dequant scale ``dscale = 1 / qscale``;
+  * activations are quantized with the scale derived from PREVIOUS steps while the same pass
+    records this step's amax; ``Fp8Meta.step()`` (once per training step, one kernel launch)
+    rolls the histories. A slot seen for the first time is calibrated with one amax pass;
+  * weights use current scaling (amax pass, then quantize) once per optimizer step, from the bf16
+    shadow the fused Adam kernel already writes;
+  * GEMMs run ``v_mfma_scale_f32_16x16x128_f8f6f4`` in the ping-pong kernel; the epilogue
+    multiplies by ``dscale_a * dscale_b`` before bias / GELU / dropout / residual (csrc/gemm.hip).
+
+Forward GEMMs use e4m3 x e4m3; LayerNorm, softmax, attention, residual adds, the optimizer and the
+backward pass stay in bf16 / fp32 (fp8 dgrad e5m2 x e4m3 is available via ``linear_dgrad_fp8``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .. import _ext
+from . import gemm
+
+E4M3, E5M2 = 0, 1
+FMAX = {E4M3: 448.0, E5M2: 57344.0}
+
+
+class Fp8Meta:
+    """Delayed-scaling state of ``n`` tensor slots."""
+
+    def __init__(self, n: int, device, history: int = 16, margin: int = 0, fmt: int = E4M3):
+        self.n = n
+        self.fmt = fmt
+        self.hist = torch.zeros(n, history, dtype=torch.float32, device=device)
+        self.amax = torch.zeros(n, dtype=torch.int32, device=device)
+        self.qscale = torch.ones(n, dtype=torch.float32, device=device)
+        self.dscale = torch.ones(n, dtype=torch.float32, device=device)
+        self.fmax = torch.full((n,), FMAX[fmt], dtype=torch.float32, device=device)
+        self.margin_mul = 2.0 ** (-margin)
+        self.calibrated = [False] * n
+
+    def _update(self, s0: int, s1: int) -> None:
+        _ext.ext().fp8_scale_update(self.hist, self.amax, self.qscale, self.dscale, self.fmax, s0, s1, self.margin_mul)
+
+    def step(self) -> None:
+        """Roll every slot's amax history into new scales (start of a training step)."""
+        self._update(0, self.n)
+
+    def quantize(self, x: torch.Tensor, slot: int, current: bool = False,
+                 out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """fp8 copy of a 2-D bf16 tensor -> (uint8 [rows, cols], dscale [1])."""
+        ext = _ext.ext()
+        am = self.amax[slot:slot + 1]
+        if current or not self.calibrated[slot]:
+            ext.fp8_quant(x, None, None, am, self.fmt)
+            self._update(slot, slot + 1)
+            self.calibrated[slot] = True
+        y = out if out is not None else torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+        ext.fp8_quant(x, y, self.qscale[slot:slot + 1], am, self.fmt)
+        return y, self.dscale[slot:slot + 1]
+
+
+class Fp8State:
+    """Per-model fp8 state: activation slots (4 per encoder block) + weight cache."""
+
+    ACT_PER_BLOCK = 4  # xn1 (qkv input), o (out-proj input), xn2 (fc1 input), h (fc2 input)
+
+    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0):
+        self.act = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E4M3)
+        self.n_blocks = n_blocks
+        self._wmeta: Optional[Fp8Meta] = None
+        self._wslot: Dict[int, int] = {}
+        self._wcache: Dict[int, Tuple[int, torch.Tensor, torch.Tensor]] = {}
+        self.device = device
+
+    def begin_step(self, training: bool) -> None:
+        if training:
+            self.act.step()
+
+    def act_quant(self, x: torch.Tensor, block: int, which: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        return self.act.quantize(x, block * self.ACT_PER_BLOCK + which)
+
+    def weight(self, w16: torch.Tensor, key: int, generation: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """fp8 (e4m3, current scaling) copy of a bf16 weight shadow, cached per store generation."""
+        hit = self._wcache.get(key)
+        if hit is not None and hit[0] == generation:
+            return hit[1], hit[2]
+        if key not in self._wslot:
+            self._wslot[key] = len(self._wslot)
+            if self._wmeta is None or self._wslot[key] >= self._wmeta.n:
+                old = self._wmeta
+                self._wmeta = Fp8Meta(max(64, 2 * len(self._wslot)), self.device, history=1, fmt=E4M3)
+                if old is not None:  # grow: keep nothing (weights are re-scaled from scratch anyway)
+                    self._wcache.clear()
+        slot = self._wslot[key]
+        out = hit[1] if hit is not None else None
+        q, ds = self._wmeta.quantize(w16, slot, current=True, out=out)
+        self._wcache[key] = (generation, q, ds)
+        return q, ds
+
+
+def linear_fwd_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
+                   bias: Optional[torch.Tensor] = None, *, resid: Optional[torch.Tensor] = None, drop=None,
+                   gelu_aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = resid + dropout(dequant(xq . wq^T) + bias), or the GELU variant (see gemm.linear_fwd)."""
+    T, K = xq.shape
+    N = wq.shape[0]
+    if out is None:
+        out = torch.empty(T, N, dtype=torch.bfloat16, device=xq.device)
+    seed, soff, p = gemm._drop_args(drop)
+    epi = gemm.EPI_GELU if gelu_aux is not None else gemm.EPI_BF16
+    _ext.ext().gemm_fp8(xq, E4M3, wq, E4M3, out, T, N, K, epi, xs, ws, bias, resid, gelu_aux, seed, soff, p)
+    return out
+
+
+def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts: torch.Tensor, *,
+                     dgelu_aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dequant(gq (e5m2) . wtq^T (e4m3, W^T rows)) [* dgelu_aux]."""
+    T, N = gq.shape
+    K = wtq.shape[0]
+    if out is None:
+        out = torch.empty(T, K, dtype=torch.bfloat16, device=gq.device)
+    epi = gemm.EPI_DGELU if dgelu_aux is not None else gemm.EPI_BF16
+    _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum)
+    return out
+
+
+def supported(T: int, D: int, M: int) -> bool:
+    return D % 128 == 0 and M % 128 == 0 and T >= 256

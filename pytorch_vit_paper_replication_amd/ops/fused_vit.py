@@ -87,20 +87,39 @@ class EncoderBlockFn(torch.autograd.Function):
     """One pre-LN transformer encoder block, forward and hand-written backward."""
 
     @staticmethod
-    def forward(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, *params):
+    def forward(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, f8, *params):
         ext = _ext.ext()
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
         T, D = x.shape
         M = w1.shape[0]
         scale = 1.0 / math.sqrt(D // H)
-        xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
-        qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
-        o, lse = ext.attn_fwd(qkv, B, N, H, scale)
-        x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=x)
-        xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
         u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
-        h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=drop1)
-        x2 = gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=drop2)
+        xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
+        if f8 is None:
+            qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
+            o, lse = ext.attn_fwd(qkv, B, N, H, scale)
+            x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=x)
+            xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
+            h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=drop1)
+            x2 = gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=drop2)
+        else:
+            # fp8 forward GEMMs (e4m3 x e4m3, per-tensor delayed scaling); everything the backward
+            # saves stays bf16, so the backward below is unchanged
+            from . import fp8 as F8
+
+            st, blk = f8
+            gen = store.generation
+            wq = [st.weight(store.bf16(w), id(w), gen) for w in (wqkv, wo, w1, w2)]
+            a, s_ = st.act_quant(xn1, blk, 0)
+            qkv = F8.linear_fwd_fp8(a, s_, *wq[0], bqkv)
+            o, lse = ext.attn_fwd(qkv, B, N, H, scale)
+            a, s_ = st.act_quant(o, blk, 1)
+            x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
+            xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
+            a, s_ = st.act_quant(xn2, blk, 2)
+            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1)
+            a, s_ = st.act_quant(h, blk, 3)
+            x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
         ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
         ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
         return x2
@@ -156,7 +175,7 @@ class EncoderBlockFn(torch.autograd.Function):
         dx = torch.empty_like(dx2)
         ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])
-        return (dx,) + (None,) * (8 + len(params))
+        return (dx,) + (None,) * (9 + len(params))
 
 
 class HeadFn(torch.autograd.Function):

@@ -85,6 +85,7 @@ class ParamStore:
         self._t_dirty = True
         self.shadow_t: Optional[torch.Tensor] = None
         self._listeners: List[Callable[[List[torch.nn.Parameter]], None]] = []
+        self.generation = 0  # bumped whenever the bf16 shadow changes (derived caches key on it)
         # weight-gradient side stream (see on_side): created lazily on GPU stores
         self._side: Optional[torch.cuda.Stream] = None
         self._side_pending = False
@@ -118,11 +119,13 @@ class ParamStore:
                     self.shadow.copy_(self.flat)
             self._shadow_key = key
             self._t_dirty = True
+            self.generation += 1
 
     def mark_shadow_fresh(self) -> None:
         """Called by the fused optimizer after it rewrote master + shadow in one pass."""
         self._shadow_key = self._version_key()
         self._t_dirty = True
+        self.generation += 1
 
     # ------------------------------------------------------------------ transposed bf16 weights
     def register_transposed(self, params: Iterable[torch.nn.Parameter]) -> None:

@@ -73,6 +73,28 @@ def main():
                 tt = timeit(lambda: G.linear_wgrad(dy, x, out))
                 print(f"wgrad {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
             G._FORCE_TILE = None
+    if "fp8" in a.only:
+        from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+        for (T8, n, k, name) in [(T, 2304, 768, "B qkv"), (T, 3072, 768, "B fc1"), (T, 768, 3072, "B fc2"),
+                                 (128 * 257, 3840, 1280, "H qkv"), (128 * 257, 5120, 1280, "H fc1"),
+                                 (128 * 257, 1280, 5120, "H fc2")]:
+            x = torch.randn(T8, k, device=dev, dtype=torch.bfloat16)
+            w = (torch.randn(n, k, device=dev) * 0.02).to(torch.bfloat16)
+            b = torch.randn(n, device=dev)
+            fl = 2.0 * T8 * n * k
+            meta = F8.Fp8Meta(2, dev, history=1)
+            xq, xs = meta.quantize(x, 0, current=True)
+            wq, ws = meta.quantize(w, 1, current=True)
+            G._FORCE_TILE = "12"
+            t16 = timeit(lambda: G.linear_fwd(x, w, b))
+            G._FORCE_TILE = None
+            t8 = timeit(lambda: F8.linear_fwd_fp8(xq, xs, wq, ws, b))
+            tq = timeit(lambda: meta.quantize(x, 0))
+            t_lib = timeit(lambda: torch.matmul(x, w.t()))
+            print(f"fp8 fwd {name:6s} T{T8} N{n} K{k}: bf16 {t16:.3f} ms {fl / t16 / 1e9:6.1f} TF | fp8 {t8:.3f} ms "
+                  f"{fl / t8 / 1e9:6.1f} TF (x{t16 / t8:.2f}) | act quant {tq:.3f} ms | hipblaslt bf16 {t_lib:.3f} ms",
+                  flush=True)
     if "attn" in a.only:
         ext = _ext.ext()
         B, N, H = a.batch, 197, 12

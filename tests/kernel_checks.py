@@ -181,6 +181,108 @@ def check_attn_bwd(B, N, H, dh=64):
     return (f"attn_bwd B{B} N{N} H{H} dh{dh}", rel_err(dqkv, qr.grad), 3e-2)
 
 
+# ----------------------------------------------------------------------------- fp8
+def check_fp8_format(fmt=0):
+    """Our quantizer must produce OCP fp8 (torch float8_e4m3fn / float8_e5m2 decode of the bytes)."""
+    ext = _ext.ext()
+    x = bf(rnd(64, 256) * 3)
+    qs = torch.tensor([7.0], device=DEV)
+    am = torch.zeros(1, dtype=torch.int32, device=DEV)
+    y = torch.empty(64, 256, dtype=torch.uint8, device=DEV)
+    ext.fp8_quant(x, y, qs, am, fmt)
+    tdt = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
+    fmax = 448.0 if fmt == 0 else 57344.0
+    ref = (x.float().cpu() * 7.0).clamp(-fmax, fmax).to(tdt)
+    got = y.cpu().view(tdt)
+    mism = (got.float() != ref.float()).float().mean().item()
+    amax_ok = abs(am.view(torch.float32).item() - x.float().abs().max().item()) < 1e-6
+    dq = ext.fp8_dequant(y, None, fmt).cpu()
+    dq_ok = torch.equal(dq, got.float())
+    return (f"fp8 quant format fmt{fmt} (byte mismatch frac {mism:.2e})", mism + (0 if amax_ok else 1) + (0 if dq_ok else 1), 1e-3)
+
+
+def _fp8_operand(x, fmt=0):
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=fmt)
+    q, ds = meta.quantize(x, 0, current=True)
+    deq = _ext.ext().fp8_dequant(q.contiguous(), ds, fmt)
+    return q, ds, deq
+
+
+def check_gemm_fp8(M, N, K, resid=False, gelu=False):
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    x, w = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05))
+    b = rnd(N)
+    r = bf(rnd(M, N)) if resid else None
+    xq, xs, xd = _fp8_operand(x)
+    wq, ws, wd = _fp8_operand(w)
+    u = torch.empty(M, N, dtype=torch.bfloat16, device=DEV) if gelu else None
+    y = F8.linear_fwd_fp8(xq, xs, wq, ws, b, resid=r, gelu_aux=u)
+    ref = xd @ wd.t() + b
+    if gelu:
+        ref = F.gelu(ref)
+    if r is not None:
+        ref = ref + r.float()
+    e_q = rel_err(y, ref)                    # vs the exact product of the quantized operands
+    ref_b = x.float() @ w.float().t() + b
+    if gelu:
+        ref_b = F.gelu(ref_b)
+    if r is not None:
+        ref_b = ref_b + r.float()
+    e_b = rel_err(y, ref_b)                  # vs the unquantized bf16 operands (fp8 rounding included)
+    return (f"gemm_fp8 e4m3 M{M} N{N} K{K} r{int(resid)} g{int(gelu)} (vs bf16 {e_b:.2e})", max(e_q, e_b / 5), 2e-2)
+
+
+def check_dgrad_fp8(M, N, K):
+    """dX = dequant(g (e5m2) . W (e4m3)) with the dGELU epilogue and the fused bias-grad column sum."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    g, wt = bf(rnd(M, N)), bf(rnd(K, N, scale=0.05))
+    aux = bf(rnd(M, K))
+    gq, gs, gd = _fp8_operand(g, 1)
+    wq, ws, wd = _fp8_operand(wt, 0)
+    cs = torch.zeros(K, device=DEV)
+    y = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=aux, colsum=cs)
+    ref = (gd @ wd.t()) * aux.float()
+    return (f"dgrad_fp8 e5m2 x e4m3 dGELU M{M} N{N} K{K}", max(rel_err(y, ref), rel_err(cs, ref.sum(0))), 2e-2)
+
+
+def check_vit_fp8(B=4):
+    """fp8-forward ViT vs the fp32 PyTorch model: logits and gradients close, training decreases loss."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=256, mlp_size=512,
+               num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0)
+    mf = ViT(**cfg).to(DEV).enable_fp8()
+    mr = ViT(**cfg).to(DEV)
+    mr.load_state_dict(mf.state_dict())
+    x = torch.rand(B * 4, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B * 4,), device=DEV)
+    lf = mf(x)
+    assert mf._fp8 is not None, "fp8 path did not engage"
+    os.environ["PVR_DISABLE_FUSED"] = "1"
+    try:
+        lr = mr(x)
+    finally:
+        os.environ["PVR_DISABLE_FUSED"] = "0"
+    e = rel_err(lf, lr)
+    opt = FusedAdam(mf.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(6):
+        loss = cross_entropy(mf(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step(clip_norm=1.0)
+        losses.append(loss.item())
+    ok = losses[-1] < losses[0] and all(math.isfinite(v) for v in losses)
+    return (f"vit fp8 fwd vs fp32 ({e:.2e}), loss {losses[0]:.3f}->{losses[-1]:.3f}", e / 3 + (0 if ok else 1), 5e-2)
+
+
 # ----------------------------------------------------------------------------- misc
 def check_xent(B, C):
     ext = _ext.ext()
@@ -297,6 +399,13 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_fwd(1, 197, 2, 128),
         lambda: check_attn_bwd(1, 300, 2, 128),
         lambda: check_attn_bwd(1, 100, 2, 96),
+        lambda: check_fp8_format(0),
+        lambda: check_fp8_format(1),
+        lambda: check_gemm_fp8(3000, 768, 1280),
+        lambda: check_gemm_fp8(700, 2304, 768, True, False),
+        lambda: check_gemm_fp8(520, 3072, 384, False, True),
+        lambda: check_dgrad_fp8(1030, 1280, 768),
+        lambda: check_vit_fp8(),
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
         lambda: check_adam(),
