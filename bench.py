@@ -39,6 +39,7 @@ def parse():
     p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
     p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
     p.add_argument("--bucket-mb", type=float, default=28.0)
+    p.add_argument("--graph", action="store_true", help="replay the whole training step as one captured hipGraph")
     return p.parse_args()
 
 
@@ -103,6 +104,15 @@ def main():
         sched.step()
         return loss
 
+    if args.graph:
+        if args.impl != "fused" or use_ddp:
+            raise SystemExit("--graph: single-process fused path only")
+        from pytorch_vit_paper_replication_amd.runtime.graph import GraphedTrainStep
+
+        graphed = GraphedTrainStep(model, opt, cross_entropy, x, y, clip_norm=1.0, warmup=max(1, args.warmup),
+                                   scheduler=sched)
+        step = graphed  # noqa: F811  (each call: graph_prepare + hipGraphLaunch + LR schedule step)
+        args.warmup = 0
     for _ in range(args.warmup):
         loss = step()
     torch.cuda.synchronize()
@@ -148,7 +158,7 @@ def main():
             "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
-                       "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl,
+                       "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl + ("+hipgraph" if args.graph else ""),
                        "grad_transport": net.transport if use_ddp else "none",
                        "optimizer": "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
                        "dropout": "0.1 (mlp, embedding)", "final_loss": round(final_loss, 4)},

@@ -273,13 +273,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int kb0 = (L % nkb) * KB;
   const int kw0 = kb0 + wave * 32;
 
-  // LDS carve: K image [KB][dh] | Q blk [32][dh] | dO blk [32][dh] | dS [32][KB] | lse2[32] | delta[32]
+  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh]) | dS [32][KB] | 2 x (lse2[32] | delta[32])
+  // Q / dO / lse / delta of query block qb+1 are staged while block qb is processed.
   char* kimg = smem;
-  char* qimg = kimg + KB * RB;
-  char* doimg = qimg + QB * RB;
-  char* dsimg = doimg + QB * RB;
-  float* s_lse = (float*)(dsimg + QB * KB * 2);
-  float* s_del = s_lse + QB;
+  char* qdo = kimg + KB * RB;
+  char* dsimg = qdo + 4 * QB * RB;
+  float* s_ld = (float*)(dsimg + QB * KB * 2);
   const int ds_cpr = KB / 8;  // 16-B chunks per dS row (power of two)
 
   const uint16_t* base = qkv + (int64_t)b * N * ld;
@@ -319,17 +318,35 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 
   const float c = scale * LOG2E;
   const int nqb = (N + QB - 1) / QB;
+  auto stage = [&](int qb) {  // Q / dO rows (LDS-DMA) and lse / delta of query block qb into slot qb & 1
+    // lse / delta are loaded BEFORE the DMAs: vmcnt retires in order, so their ds_write then waits
+    // only for these two loads, not for the DMAs that must stay in flight
+    const int q = qb * QB + (threadIdx.x & (QB - 1));
+    float l2 = INFINITY, dl = 0.f;
+    if (threadIdx.x < QB && q < N) {
+      l2 = lse[(int64_t)bh * N + q] * LOG2E;
+      dl = delta[(int64_t)bh * N + q];
+    }
+    char* qi = qdo + (qb & 1) * 2 * QB * RB;
+    dma_rows<C::NH>(qrs, qi, QB, ld, qb * QB, wave, NW, lane);
+    dma_rows<C::NH>(dors, qi + QB * RB, QB, ld_do, qb * QB, wave, NW, lane);
+    if (threadIdx.x < QB) {
+      float* sl = s_ld + (qb & 1) * 2 * QB;
+      sl[threadIdx.x] = l2;
+      sl[QB + threadIdx.x] = dl;
+    }
+  };
+  stage(0);
   for (int qb = 0; qb < nqb; ++qb) {
     const int q0 = qb * QB;
-    dma_rows<C::NH>(qrs, qimg, QB, ld, q0, wave, NW, lane);
-    dma_rows<C::NH>(dors, doimg, QB, ld_do, q0, wave, NW, lane);
-    if (threadIdx.x < QB) {
-      const int q = q0 + threadIdx.x;
-      s_lse[threadIdx.x] = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
-      s_del[threadIdx.x] = q < N ? delta[(int64_t)bh * N + q] : 0.f;
-    }
+    // block qb landed (issued one iteration ago); every wave is done with slot (qb+1)&1 and with dS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (qb + 1 < nqb) stage(qb + 1);
+    const char* qimg = qdo + (qb & 1) * 2 * QB * RB;
+    const char* doimg = qimg + QB * RB;
+    const float* s_lse = s_ld + (qb & 1) * 2 * QB;
+    const float* s_del = s_lse + QB;
 
     if (active) {
     // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]
@@ -391,7 +408,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
           *(uint16_t*)(dsimg + ql * KB * 2 + chunk * 16 + (kl & 7) * 2) = f2bf(dp[a][f][r]);
         }
     }  // active
-    __syncthreads();
+    // dS visible to every wave; a raw barrier, so the next block's DMAs stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 2*NE output fragments split over the waves
     for (int fr = wave; fr < 2 * C::NE; fr += NW) {
       const int a = fr / C::NE, e = fr % C::NE;
@@ -490,11 +510,11 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   const int nkb = (N + KB - 1) / KB;
   if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
   const int RB = 128 * Hd<DH>::NH;
-  const size_t smem = (size_t)KB * RB + 2 * 32 * RB + 32 * KB * 2 + 2 * 32 * 4;
+  const size_t smem = (size_t)KB * RB + 4 * 32 * RB + 32 * KB * 2 + 4 * 32 * 4;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)(8 * 32 * RB + 2 * 32 * RB + 32 * 8 * 32 * 2 + 2 * 32 * 4));
+                                             (int)(8 * 32 * RB + 4 * 32 * RB + 32 * 8 * 32 * 2 + 4 * 32 * 4));
     if (e != hipSuccess) return e;
     attr = true;
   }

@@ -48,6 +48,12 @@ class FusedAdam(torch.optim.Optimizer):
         self._fused = None  # (store, m, v, seg_start, seg_group, ws, clip)
         self.last_grad_norm: Optional[torch.Tensor] = None
         self.step_count = 0
+        # hipGraph mode: the per-step hyper-parameter table lives in a persistent device tensor that
+        # graph_prepare() refreshes (outside the graph) before each replay
+        self._graph = False
+        self._table_dev: Optional[torch.Tensor] = None
+        self._table_ring = []  # pinned host buffers + events (host may run a few steps ahead)
+        self._ring_i = 0
 
     # ------------------------------------------------------------------ helpers
     def _all_params(self):
@@ -99,9 +105,10 @@ class FusedAdam(torch.optim.Optimizer):
         self._fused = (store, m, v, seg_start, seg_group, ws, clip)
         return self._fused
 
-    def _group_table(self, step: int, device) -> torch.Tensor:
+    def _group_array(self, step: int, arr: Optional[np.ndarray] = None) -> np.ndarray:
         G = len(self.param_groups)
-        arr = np.zeros((G, 8), dtype=np.float32)
+        if arr is None:
+            arr = np.zeros((G, 8), dtype=np.float32)
         for i, g in enumerate(self.param_groups):
             b1, b2 = g["betas"]
             arr[i, 0] = float(g["lr"])
@@ -112,7 +119,37 @@ class FusedAdam(torch.optim.Optimizer):
             arr[i, 5] = 1.0 - b1 ** step
             arr[i, 6] = math.sqrt(1.0 - b2 ** step)
         arr.view(np.int32)[:, 7] = [int(bool(g["decoupled_weight_decay"])) for g in self.param_groups]
-        return torch.from_numpy(arr).to(device, non_blocking=True)
+        return arr
+
+    def _group_table(self, step: int, device) -> torch.Tensor:
+        if self._graph:
+            return self._table_dev
+        return torch.from_numpy(self._group_array(step)).to(device, non_blocking=True)
+
+    # ------------------------------------------------------------------ hipGraph support
+    def graph_mode(self, enabled: bool = True, ring: int = 4) -> None:
+        """Capture-safe stepping: ``step()`` reads the group table from a persistent device tensor and
+        does not advance the step counter; call ``graph_prepare()`` before every graph replay."""
+        fz = self._setup_fused()
+        if enabled and fz is None:
+            raise RuntimeError("graph mode needs the fused (single-store, GPU) optimizer path")
+        self._graph = enabled
+        if enabled and self._table_dev is None:
+            G = len(self.param_groups)
+            self._table_dev = torch.zeros(G, 8, dtype=torch.float32, device=fz[0].device)
+            self._table_ring = [(torch.zeros(G, 8, dtype=torch.float32).pin_memory(), torch.cuda.Event()) for _ in range(ring)]
+            self.graph_prepare(advance=False)
+
+    def graph_prepare(self, advance: bool = True) -> None:
+        """Advance the step counter and upload this step's lr / bias corrections (stream-ordered)."""
+        if advance:
+            self.step_count += 1
+        host, ev = self._table_ring[self._ring_i % len(self._table_ring)]
+        self._ring_i += 1
+        ev.synchronize()  # the copy that last used this pinned buffer has executed
+        self._group_array(max(self.step_count, 1), host.numpy())
+        self._table_dev.copy_(host, non_blocking=True)
+        ev.record()
 
     # ------------------------------------------------------------------ public
     def zero_grad(self, set_to_none: bool = True):
@@ -148,7 +185,8 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         fz = self._setup_fused()
-        self.step_count += 1
+        if not self._graph:
+            self.step_count += 1
         step = self.step_count
         if fz is not None:
             store, m, v, seg_start, seg_group, ws, clip = fz
@@ -166,9 +204,6 @@ class FusedAdam(torch.optim.Optimizer):
                             clip if use_clip else None, self.skip_nonfinite)
             store.mark_shadow_fresh()
             self._pending_clip = False
-            for st in self.state.values():
-                if "step" in st:
-                    st["step"] = torch.tensor(float(step))
             return loss
         # ---------------- reference math (torch.optim.Adam, single-tensor, maximize=False)
         if clip_norm is not None:
@@ -199,6 +234,13 @@ class FusedAdam(torch.optim.Optimizer):
                 denom = (st["exp_avg_sq"].sqrt() / math.sqrt(bc2)).add_(eps)
                 p.addcdiv_(st["exp_avg"], denom, value=-step_size)
         return loss
+
+    def state_dict(self):
+        if self._fused is not None:  # per-tensor step counters are materialised lazily
+            for st in self.state.values():
+                if "step" in st:
+                    st["step"] = torch.tensor(float(self.step_count))
+        return super().state_dict()
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)

@@ -1,0 +1,19 @@
+"""Run the attention kernels at ViT-B/16 b256 shapes a few times (for rocprofv3 counter collection)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
+
+ext = _ext.ext()
+B, N, H, D = 256, 197, 12, 768
+qkv = torch.randn(B * N, 3 * D, device="cuda", dtype=torch.bfloat16)
+o, lse = ext.attn_fwd(qkv, B, N, H, 0.125)
+do = torch.randn_like(o)
+for _ in range(3):
+    ext.attn_fwd(qkv, B, N, H, 0.125)
+    ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125)
+torch.cuda.synchronize()
+print("ok")
