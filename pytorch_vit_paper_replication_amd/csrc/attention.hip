@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
                                                         const uint16_t* __restrict__ dout, int64_t ld_do,
                                                         const float* __restrict__ lse, const float* __restrict__ delta,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
-                                                        int N, int H, int D, float scale) {
+                                                        float* __restrict__ dbias, int N, int H, int D, float scale) {
   using C = Hd<DH>;
   constexpr int QB = 32;
   constexpr int RB = 128 * C::NH;  // LDS bytes per staged head row
@@ -337,6 +337,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     }
   };
   stage(0);
+  float dqb0 = 0.f, dqb1 = 0.f;  // q-bias gradient partials (column sums of this wave's dQ fragments)
   for (int qb = 0; qb < nqb; ++qb) {
     const int q0 = qb * QB;
     // block qb landed (issued one iteration ago); every wave is done with slot (qb+1)&1 and with dS
@@ -413,7 +414,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 2*NE output fragments split over the waves
-    for (int fr = wave; fr < 2 * C::NE; fr += NW) {
+    int kfr = 0;
+    for (int fr = wave; fr < 2 * C::NE; fr += NW, ++kfr) {
       const int a = fr / C::NE, e = fr % C::NE;
       v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
       for (int ks = 0; ks < nks_dq; ++ks) {
@@ -423,17 +425,71 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         const v8s bf = frag_tr(kimg, KB, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane);
         acc = mfma16(af, bf, acc);
       }
+      float cs = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int q = q0 + 16 * a + 4 * g + r;
         if (q < N) {
           const float val = acc[r] * scale;
+          cs += val;
           if (dq_acc)
             atomicAdd(dq_acc + ((int64_t)b * N + q) * D + h * DH + 16 * e + li, val);
           else
             dqkv[((int64_t)b * N + q) * ld_dq + h * DH + 16 * e + li] = f2bf(val);
         }
       }
+      if (kfr == 0) dqb0 += cs;  // q-bias gradient: this fragment's column sums across query blocks
+      else dqb1 += cs;           // (at most two fragments per wave: host guarantees 2*NE <= 2*NW)
+    }
+  }
+  // in_proj bias gradient partials of this (batch, key block, head): column sums of dQ | dK | dV,
+  // reduced across the waves in LDS and written once (no atomics) to dbias[(b * nkb + kb)][3D];
+  // the host then sums over the (batch, key block) rows
+  if (dbias) {
+    __syncthreads();  // every wave is past its last LDS read
+    float* red = (float*)smem;  // [2 (dQ row halves)][DH] q sums | [NW][DH] k | [NW][DH] v
+    float* rq = red;
+    float* rk = red + 2 * DH;
+    float* rv = rk + NW * DH;
+    int kfr = 0;
+    for (int fr = wave; fr < 2 * C::NE && kfr < 2; fr += NW, ++kfr) {
+      float cs = kfr == 0 ? dqb0 : dqb1;
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (g == 0) rq[(fr / C::NE) * DH + 16 * (fr % C::NE) + li] = cs;
+    }
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sk = 0.f, sv = 0.f;
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+          if (kw0 + 16 * f + li < N) {
+            sk += dk[e][f][r];
+            sv += dv[e][f][r];
+          }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          sk += __shfl_xor(sk, o, 64);
+          sv += __shfl_xor(sv, o, 64);
+        }
+        if (li == 0) {
+          rk[wave * DH + 16 * e + 4 * g + r] = sk * scale;
+          rv[wave * DH + 16 * e + 4 * g + r] = sv;
+        }
+      }
+    __syncthreads();
+    float* dst = dbias + ((int64_t)b * nkb + kb0 / KB) * 3 * D + h * DH;
+    for (int d = threadIdx.x; d < DH; d += blockDim.x) {
+      float tk = 0.f, tv = 0.f;
+      for (int w = 0; w < NW; ++w) {
+        tk += rk[w * DH + d];
+        tv += rv[w * DH + d];
+      }
+      dst[d] = rq[d] + rq[DH + d];
+      dst[D + d] = tk;
+      dst[2 * D + d] = tv;
     }
   }
   // dK, dV stores: lane holds X^T[d = 16e + 4g + r][key = kw0 + 16f + li]
@@ -492,6 +548,12 @@ extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* ou
 
 extern "C" int pvr_attn_head_dim_supported(int dh) { return dh == 64 || dh == 80 || dh == 96 || dh == 128; }
 
+extern "C" int pvr_attn_bwd_waves(int N);
+extern "C" int pvr_attn_bwd_key_blocks(int N) {
+  const int kb = 32 * pvr_attn_bwd_waves(N);
+  return (N + kb - 1) / kb;
+}
+
 extern "C" int pvr_attn_bwd_waves(int N) {
   const int need = (N + 31) / 32;
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
@@ -500,7 +562,7 @@ extern "C" int pvr_attn_bwd_waves(int N) {
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                  int B, int N, int H, int D, float scale, hipStream_t s) {
+                                  float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
   const int64_t nrows = (int64_t)B * N * H;
   hipLaunchKernelGGL(attn_bwd_delta_kernel<DH>, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, dout, ld_do, out, ld_o, delta,
@@ -509,6 +571,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
   if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
+  if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   const int RB = 128 * Hd<DH>::NH;
   const size_t smem = (size_t)KB * RB + 4 * 32 * RB + 32 * KB * 2 + 4 * 32 * 4;
   static bool attr = false;
@@ -519,7 +582,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     attr = true;
   }
   hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
-                     nkb > 1 ? dq_acc : nullptr, N, H, D, scale);
+                     nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
     int64_t blocks = (rows * D + 255) / 256;
@@ -530,15 +593,17 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
 }
 
 // dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
+// dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
+// every element is written), whose row sum is the in_proj bias gradient.
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                    int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                   int B, int N, int H, int D, float scale, hipStream_t s) {
+                                   float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
   switch (D / H) {
-    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
-    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
-    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
-    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, B, N, H, D, scale, s);
+    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
     default: return hipErrorInvalidValue;
   }
 }

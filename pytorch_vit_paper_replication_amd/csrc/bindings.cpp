@@ -53,8 +53,10 @@ hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
 hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, int, const float*, unsigned*, int, hipStream_t);
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
+int pvr_attn_bwd_key_blocks(int);
+int pvr_attn_bwd_waves(int);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
-hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, float*, int, int, int, int, float, hipStream_t);
 }
 
 namespace {
@@ -369,16 +371,33 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int
 }
 
 torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
-                       double scale) {
+                       double scale, c10::optional<torch::Tensor> dbias) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
   auto delta = torch::empty_like(lse);
   torch::Tensor dq_acc;
   if (N > 256) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
+  // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
+  torch::Tensor dbias_part;
+  const bool want_db = dbias.has_value() && dbias->defined();
+  if (want_db) {
+    TORCH_CHECK(dbias->numel() == 3 * D && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous(), "dbias [3D] f32");
+    const int dh = (int)(D / H);
+    if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
+      dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
+  }
   check(pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"), ld_of(dout, "dout"),
                      f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"), ld_of(dqkv, "dqkv"),
-                     dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D, (float)scale, stream()),
+                     dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr,
+                     dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
+                     (float)scale, stream()),
         "attn_bwd");
+  if (want_db) {
+    if (dbias_part.defined())
+      dbias->add_(dbias_part.sum(0));
+    else
+      dbias->add_(dqkv.sum(0, false, torch::kFloat32));
+  }
   return dqkv;
 }
 
@@ -415,6 +434,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
+        py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none());
   m.def("arch", []() { return std::string("gfx950"); });
 }

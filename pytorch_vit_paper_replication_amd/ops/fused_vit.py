@@ -15,6 +15,7 @@ Reference semantics (models/vit.py):
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -24,6 +25,7 @@ from .. import _ext
 from . import gemm
 
 SITE_SHIFT = 32
+_FUSE_QKV_DBIAS = os.environ.get("PVR_ATTN_DBIAS", "1") != "0"
 
 
 def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
@@ -159,9 +161,14 @@ class EncoderBlockFn(torch.autograd.Function):
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
         do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
-        dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
-        if bqkv.requires_grad:
-            gemm.bias_grad(dqkv, g(bqkv))
+        # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
+        gbqkv = g(bqkv)
+        if _FUSE_QKV_DBIAS:
+            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None if gbqkv is None else gbqkv.view(-1))
+        else:
+            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
+            if gbqkv is not None:
+                gemm.bias_grad(dqkv, gbqkv)
         gwo, gwqkv = g(wo), g(wqkv)
 
         def attn_wgrads():

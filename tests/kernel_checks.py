@@ -174,11 +174,13 @@ def check_attn_bwd(B, N, H, dh=64):
     qkv = bf(rnd(B * N, 3 * D))
     o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / math.sqrt(dh))
     do = bf(rnd(B * N, D))
-    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh))
+    dbias = torch.zeros(3 * D, device=DEV)
+    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
     qr = qkv.float().requires_grad_(True)
     oref, _ = _attn_ref(qr, B, N, H)
     oref.backward(do.float())
-    return (f"attn_bwd B{B} N{N} H{H} dh{dh}", rel_err(dqkv, qr.grad), 3e-2)
+    e_b = rel_err(dbias, qr.grad.sum(0))  # fused in_proj bias gradient
+    return (f"attn_bwd B{B} N{N} H{H} dh{dh} (dbias {e_b:.1e})", max(rel_err(dqkv, qr.grad), e_b), 3e-2)
 
 
 # ----------------------------------------------------------------------------- fp8
