@@ -939,8 +939,11 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
 // coalesced instead of 16 rows x 32 B per instruction. The math is the per-element epilogue above,
 // in fp32, unchanged. Row images are 1 KiB (256 fp32) with the 16-B chunk index XOR-swizzled by
 // the row (ds_write_b128 2-way, ds_read_b128 conflict-free).
-template <int EPI>
+// RP = tile rows per staging pass (128: the two K-tile buffers, 128 KiB; 32: the persistent
+// kernel's separate 32 KiB region, while the next tile's K-tiles stream into the buffers).
+template <int EPI, int RP = 128>
 PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, int m0, int n0, int wm, int wn, int lane) {
+  static_assert(RP == 128 || RP == 64 || RP == 32, "rows per pass");
   const int tid = threadIdx.x;
   const int g = lane >> 4, li = lane & 15;
   const int cq = tid & 63;           // this thread's 4-column group within the tile row
@@ -953,24 +956,26 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
   const float deq = p.scale_a ? (*p.scale_a) * (*p.scale_b) : 1.f;
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NPASS = 256 / RP, FPP = RP / 16;  // passes; fragment rows (of 8 per wave) per pass
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    __syncthreads();  // previous half's LDS reads (or the main loop's) are done
-    if (wm == half) {
+  for (int half = 0; half < NPASS; ++half) {
+    __syncthreads();  // previous pass's LDS reads (or the main loop's) are done
+    if (wm == (half * RP) / 128) {
+      const int i0 = ((half * RP) % 128) / 16;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int ii = 0; ii < FPP; ++ii)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int r = 16 * i + li;                 // row within the half
+          const int r = 16 * ii + li;                // row within the pass
           const int ch = wn * 16 + 4 * j + g;        // 16-B chunk (4 fp32 columns) within the row
-          *(v4f*)(smem + r * 1024 + ((ch ^ (r & 63)) << 4)) = acc[i][j];
+          *(v4f*)(smem + r * 1024 + ((ch ^ (r & 63)) << 4)) = acc[i0 + ii][j];
         }
     }
     __syncthreads();
 #pragma unroll 4
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < RP / 8; ++k) {
       const int r = (tid >> 6) + 8 * k;
-      const int m = m0 + half * 128 + r;
+      const int m = m0 + half * RP + r;
       const v4f a = *(const v4f*)(smem + r * 1024 + ((cq ^ (r & 63)) << 4));
       if (m >= p.M || !ncol) continue;
       float v[4] = {a[0] * deq, a[1] * deq, a[2] * deq, a[3] * deq};
@@ -1139,6 +1144,182 @@ hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ===================================================================================== persistent ping-pong
+// One resident 8-wave workgroup per CU walks tiles v = blockIdx.x, +gridDim.x, ... (XCD-remapped as
+// above). The half-tile LDS-DMA stream is continuous across a workgroup's tiles: the last phases
+// of tile i already stage K-tiles 0 and 1 of tile i+1 into the two buffers, so the next tile starts
+// with its operands landed and its prologue latency is hidden under tile i's tail and epilogue.
+// The epilogue stages through a separate 32 KiB LDS region (8 passes of 32 rows) so it never
+// touches the K-tile buffers the in-flight DMAs are writing. k-contiguous bf16 operands, K >= 128.
+PVR_DEV void ppp_issue_kind(int kind, __amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, char* buf, int64_t lda, int64_t ldb,
+                            int kb, int wave, int lane) {
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int d = wave + 8 * x;
+    if (kind == 0 || kind == 3) {
+      const int hh = kind == 3;
+      const int rowb = (2 * (d >> 3) + hh) * 64 + (d & 7) * 8;
+      const int row = rowb + (lane >> 3);
+      const int c = (lane & 7) ^ swz_k(row);
+      dma16(ars, to_lds(buf + rowb * 128), (uint32_t)(row * lda * 2 + kb + c * 16));
+    } else {
+      const int hh = kind == 2;
+      const int rowb = (2 * (d >> 2) + hh) * 32 + (d & 3) * 8;
+      const int row = rowb + (lane >> 3);
+      const int c = (lane & 7) ^ swz_k(row);
+      dma16(brs, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * 2 + kb + c * 16));
+    }
+  }
+}
+
+struct PppTile {
+  int m0, n0;
+  __amdgpu_buffer_rsrc_t ars, brs;
+};
+
+PVR_DEV PppTile ppp_tile(const GemmParams& p, int v, int ntiles, int ntn) {
+  PppTile t;
+  if (v >= ntiles) {  // past this workgroup's last tile: every DMA reads as out of range
+    t.m0 = t.n0 = 0;
+    t.ars = make_rsrc(p.A, 0);
+    t.brs = make_rsrc(p.B, 0);
+    return t;
+  }
+  const int tt = xcd_remap(v, ntiles);
+  t.m0 = (tt / ntn) * 256;
+  t.n0 = (tt % ntn) * 256;
+  t.ars = make_rsrc(p.A + (int64_t)t.m0 * p.lda, rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)t.m0 * p.lda));
+  t.brs = make_rsrc(p.B + (int64_t)t.n0 * p.ldb, rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)t.n0 * p.ldb));
+  return t;
+}
+
+// Phase of the continuous stream: reads / MFMAs of K-tile (current buffer) and the DMA of global
+// half-tile `h_issue`, which belongs to this tile (K-tile kt_i) or to the next one.
+template <int QM, int QN, int RD_A, int RD_B, bool SWAP>
+PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, char* smem, const PppTile& cur,
+                       const PppTile& nxt, int G_issue, int kind, int tile_first_G, int nk, const GemmParams& p, int wave, int lane,
+                       int wm, int wn) {
+  if constexpr (RD_A) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+  }
+  if constexpr (RD_B) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
+  }
+  {
+    const int rel = G_issue - tile_first_G;  // K-tile index relative to the current tile
+    const bool same = rel < nk;
+    const PppTile& t = same ? cur : nxt;
+    const int kt = same ? rel : rel - nk;
+    ppp_issue_kind(kind, t.ars, t.brs, smem + (G_issue & 1) * PP_BUF, p.lda, p.ldb, kt * 128, wave, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  pp_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        v4f& c = acc[QM * 4 + ii][QN * 2 + jj];
+        if constexpr (SWAP)
+          c = mfma16(bf[QN][jj][ks], af[ii][ks], c);
+        else
+          c = mfma16(af[ii][ks], bf[QN][jj][ks], c);
+      }
+  __builtin_amdgcn_s_setprio(0);
+  pp_barrier();
+}
+
+template <bool SWAP, int EPI>
+__global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256, ntiles = ntm * ntn;
+  const int nk = p.K / PP_BK;  // >= 2 (host check)
+  int v = blockIdx.x;
+  if (v >= ntiles) return;
+
+  PppTile cur = ppp_tile(p, v, ntiles, ntn);
+  PppTile nxt = ppp_tile(p, v + gridDim.x, ntiles, ntn);
+  // prologue of the first tile: half-tiles 0..5 (global K-tiles 0 and 1 of the stream)
+  ppp_issue_kind(0, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind(1, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind(2, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind(3, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind(0, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
+  ppp_issue_kind(1, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  pp_barrier();
+
+  int G0 = 0;  // global index (in this workgroup's K-tile stream) of the current tile's K-tile 0
+  for (;;) {
+    v4f acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    v8s af[4][2], bf[2][2][2];
+    if (wm == 1) pp_barrier();  // group 1 runs one barrier behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const int G = G0 + kt;
+      const char* buf = smem + (G & 1) * PP_BUF;
+      ppp_phase<0, 0, 1, 1, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 1, 2, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<0, 1, 0, 1, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 1, 3, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<1, 1, 1, 0, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 2, 0, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<1, 0, 0, 0, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
+    }
+    if (wm == 0) pp_barrier();  // re-align the groups for the epilogue
+    // The next tile's first DMAs are in flight into the K-tile buffers; the epilogue stages in the
+    // separate region behind them.
+    epilogue_staged<EPI, 32>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+    v += gridDim.x;
+    if (v >= ntiles) break;
+    G0 += nk;
+    cur = nxt;
+    nxt = ppp_tile(p, v + gridDim.x, ntiles, ntn);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step 1: drain (stores + the K-tiles already issued)
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
+template <bool SWAP, int EPI>
+hipError_t launch_ppp(const GemmParams& p, hipStream_t s) {
+  constexpr int SMEM = 2 * PP_BUF + 32 * 1024;
+  auto kern = gemm_ppp_kernel<SWAP, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int ntiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  int cus = 256;
+  {
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      hipDeviceProp_t prop;
+      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) n_cu = prop.multiProcessorCount;
+      if (n_cu <= 0) n_cu = 256;
+    }
+    cus = n_cu;
+  }
+  const int grid = ntiles < cus ? ntiles : cus;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, s, p);
+  return hipGetLastError();
+}
+
 template <bool AK, bool BKC, bool SWAP, int EPI>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   switch (p.tile_cfg) {
@@ -1155,6 +1336,12 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     case 9: return launch_v3<256, 128, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 10: return launch_v3<128, 256, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 11: return launch_v3<256, 256, 2, 4, 3, 2, AK, BKC, SWAP, EPI>(p, s);
+    case 13:  // persistent ping-pong (k-contiguous bf16, bf16-output epilogues, no split-K)
+      if constexpr (AK && BKC && SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
+        if (p.K % PP_BK == 0 && p.K >= 2 * PP_BK && p.k_split_len >= p.K && !p.addend && !p.row_group && (p.N & 3) == 0)
+          return launch_ppp<SWAP, EPI>(p, s);
+      }
+      [[fallthrough]];
     case 12:
       if constexpr (AK == BKC) {  // k-contiguous pair (fwd / dgrad with W^T) or mn pair (wgrad)
         if ((!AK || (p.K % PP_BK == 0 && p.k_split_len % PP_BK == 0)) && (AK || p.k_split_len % PP_BK == 0))

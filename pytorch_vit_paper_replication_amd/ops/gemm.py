@@ -19,20 +19,25 @@ EPI_BF16, EPI_GELU, EPI_DGELU, EPI_F32_ATOMIC, EPI_F32_STORE = range(5)
 
 # tile configs: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves), 2 = 128x256 (8 waves)
 _FORCE_TILE = os.environ.get("PVR_GEMM_TILE")
+_PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "1") != "0"
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
 
 def _tile(M: int, N: int, K: int, kind: str) -> int:
     """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
-    k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave ping-pong (12; K % 64 == 0, else
-    the 4-stage BK=32 ring 6); token-reduced wgrad (both operands mn-contiguous, split-K
+    k-contiguous forward/dgrad at ViT sizes -> persistent 256x256 8-wave ping-pong (13; K % 64 == 0,
+    else the 4-stage BK=32 ring 6); token-reduced wgrad (both operands mn-contiguous, split-K
     atomics) -> the same ping-pong with transposed LDS reads when the token count is large,
     128x128 (0) otherwise."""
     if _FORCE_TILE is not None:
         return int(_FORCE_TILE)
     if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
-        return 12 if K % 64 == 0 else 6
+        if K % 64:
+            return 6
+        # persistent ping-pong (13) where a CU gets several tiles; the kernel itself falls back to
+        # the one-tile-per-workgroup form (12) for epilogues it does not stage
+        return 13 if K >= 128 and _PERSISTENT else 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
         return 12
     return 0

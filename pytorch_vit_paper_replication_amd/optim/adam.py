@@ -122,9 +122,26 @@ class FusedAdam(torch.optim.Optimizer):
         return arr
 
     def _group_table(self, step: int, device) -> torch.Tensor:
-        if self._graph:
-            return self._table_dev
-        return torch.from_numpy(self._group_array(step)).to(device, non_blocking=True)
+        if not self._graph:
+            # same pinned-ring upload as the graph path: a pageable H2D copy would block the host until
+            # the GPU queue drains (a ~0.3 ms bubble per step)
+            if self._table_dev is None:
+                self._alloc_table(device)
+            self._upload_table(step)
+        return self._table_dev
+
+    def _alloc_table(self, device, ring: int = 4) -> None:
+        G = len(self.param_groups)
+        self._table_dev = torch.zeros(G, 8, dtype=torch.float32, device=device)
+        self._table_ring = [(torch.zeros(G, 8, dtype=torch.float32).pin_memory(), torch.cuda.Event()) for _ in range(ring)]
+
+    def _upload_table(self, step: int) -> None:
+        host, ev = self._table_ring[self._ring_i % len(self._table_ring)]
+        self._ring_i += 1
+        ev.synchronize()  # the copy that last used this pinned buffer has executed
+        self._group_array(max(step, 1), host.numpy())
+        self._table_dev.copy_(host, non_blocking=True)
+        ev.record()
 
     # ------------------------------------------------------------------ hipGraph support
     def graph_mode(self, enabled: bool = True, ring: int = 4) -> None:
@@ -134,22 +151,16 @@ class FusedAdam(torch.optim.Optimizer):
         if enabled and fz is None:
             raise RuntimeError("graph mode needs the fused (single-store, GPU) optimizer path")
         self._graph = enabled
-        if enabled and self._table_dev is None:
-            G = len(self.param_groups)
-            self._table_dev = torch.zeros(G, 8, dtype=torch.float32, device=fz[0].device)
-            self._table_ring = [(torch.zeros(G, 8, dtype=torch.float32).pin_memory(), torch.cuda.Event()) for _ in range(ring)]
+        if enabled:
+            if self._table_dev is None:
+                self._alloc_table(fz[0].device, ring)
             self.graph_prepare(advance=False)
 
     def graph_prepare(self, advance: bool = True) -> None:
         """Advance the step counter and upload this step's lr / bias corrections (stream-ordered)."""
         if advance:
             self.step_count += 1
-        host, ev = self._table_ring[self._ring_i % len(self._table_ring)]
-        self._ring_i += 1
-        ev.synchronize()  # the copy that last used this pinned buffer has executed
-        self._group_array(max(self.step_count, 1), host.numpy())
-        self._table_dev.copy_(host, non_blocking=True)
-        ev.record()
+        self._upload_table(self.step_count)
 
     # ------------------------------------------------------------------ public
     def zero_grad(self, set_to_none: bool = True):

@@ -365,7 +365,7 @@ def check_vit_fused_vs_reference(B=4, train=False, **over):
 
 def all_checks() -> List[Callable]:
     c = []
-    for tile in (0, 6, 12):
+    for tile in (0, 6, 12, 13):
         c.append(lambda t=tile: check_gemm_fwd(50432 // 16, 768, 768, t))
         c.append(lambda t=tile: check_gemm_fwd(197 * 3, 2304, 768, t, True, True))
         c.append(lambda t=tile: check_gemm_gelu(197 * 2, 3072, 768, t))
@@ -374,6 +374,10 @@ def all_checks() -> List[Callable]:
         c.append(lambda t=tile: check_gemm_wgrad(197 * 5, 768, 3072, t))
     c += [
         lambda: check_gemm_fwd(777, 2304, 3072, 12, True, True),
+        lambda: check_gemm_fwd(5000, 2304, 768, 13, True, True),   # persistent: several tiles per CU
+        lambda: check_gemm_fwd(9000, 768, 128, 13, True, False),   # nk = 2: next-tile DMAs start at phase 3
+        lambda: check_gemm_gelu(6000, 3072, 768, 13),
+        lambda: check_gemm_dropout(3000, 768, 128, 0.1, 13),
         lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
         lambda: check_gemm_fwd(100, 64, 128, 0, True, True),
         lambda: check_gemm_dgelu(394, 768, 3072),
