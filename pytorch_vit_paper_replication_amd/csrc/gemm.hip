@@ -941,7 +941,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
 // the row (ds_write_b128 2-way, ds_read_b128 conflict-free).
 // RP = tile rows per staging pass (128: the two K-tile buffers, 128 KiB; 32: the persistent
 // kernel's separate 32 KiB region, while the next tile's K-tiles stream into the buffers).
-template <int EPI, int RP = 128>
+template <int EPI, int RP = 128, bool RES = false>
 PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, int m0, int n0, int wm, int wn, int lane) {
   static_assert(RP == 128 || RP == 64 || RP == 32, "rows per pass");
   const int tid = threadIdx.x;
@@ -972,12 +972,28 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         }
     }
     __syncthreads();
-#pragma unroll 4
-    for (int k = 0; k < RP / 8; ++k) {
+    // Per-row inputs of this pass (residual / dGELU factor) are loaded up front and unconditionally
+    // (rows / columns clamped into range): a load under a per-row branch makes the compiler wait
+    // vmcnt(0) after each one, serialising them and draining every in-flight LDS-DMA.
+    constexpr int RPT = RP / 8;  // rows per thread per pass
+    constexpr bool HAS_IN = EPI == EPI_DGELU || (EPI == EPI_BF16 && RES);
+    uint2 pin[HAS_IN ? RPT : 1];
+    if constexpr (HAS_IN) {
+      const uint16_t* src = EPI == EPI_DGELU ? p.aux : p.resid;
+      const int64_t lsrc = EPI == EPI_DGELU ? p.ld_aux : p.ld_resid;
+      const int nn = ncol ? n : 0;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int mc = min(m0 + half * RP + (tid >> 6) + 8 * k, p.M - 1);
+        pin[k] = *(const uint2*)(src + (int64_t)mc * lsrc + nn);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
       const int r = (tid >> 6) + 8 * k;
       const int m = m0 + half * RP + r;
       const v4f a = *(const v4f*)(smem + r * 1024 + ((cq ^ (r & 63)) << 4));
-      if (m >= p.M || !ncol) continue;
+      const bool ok = m < p.M && ncol;
       float v[4] = {a[0] * deq, a[1] * deq, a[2] * deq, a[3] * deq};
       if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
         v[0] += bias.x; v[1] += bias.y; v[2] += bias.z; v[3] += bias.w;
@@ -992,8 +1008,8 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = keep[q] ? v[q] * p.drop_scale : 0.f;
           }
-          if (p.resid) {
-            const uint2 rr = *(const uint2*)(p.resid + (int64_t)m * p.ld_resid + n);
+          if constexpr (RES) {
+            const uint2 rr = pin[k];
             v[0] += bf2f(rr.x & 0xFFFF); v[1] += bf2f(rr.x >> 16);
             v[2] += bf2f(rr.y & 0xFFFF); v[3] += bf2f(rr.y >> 16);
           }
@@ -1008,16 +1024,18 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
             gp[q] = gd * sc;
           }
           uint2 ax; ax.x = pack2bf(gp[0], gp[1]); ax.y = pack2bf(gp[2], gp[3]);
-          *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = ax;
+          if (ok) *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = ax;
         }
       } else {  // EPI_DGELU
-        const uint2 gg = *(const uint2*)(p.aux + (int64_t)m * p.ld_aux + n);
+        const uint2 gg = pin[k];
         v[0] *= bf2f(gg.x & 0xFFFF); v[1] *= bf2f(gg.x >> 16);
         v[2] *= bf2f(gg.y & 0xFFFF); v[3] *= bf2f(gg.y >> 16);
-        csum[0] += v[0]; csum[1] += v[1]; csum[2] += v[2]; csum[3] += v[3];
+        if (ok) {
+          csum[0] += v[0]; csum[1] += v[1]; csum[2] += v[2]; csum[3] += v[3];
+        }
       }
       uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-      *(uint2*)((uint16_t*)p.C + (int64_t)m * p.ldc + n) = o;
+      if (ok) *(uint2*)((uint16_t*)p.C + (int64_t)m * p.ldc + n) = o;
     }
   }
   if constexpr (EPI == EPI_DGELU) {
@@ -1117,8 +1135,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
   stamp(p, 2);
   if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
-    if (!p.addend && !p.row_group && (p.N & 3) == 0)
-      epilogue_staged<EPI>(p, acc, smem, m0, n0, wm, wn, lane);
+    if (!p.addend && !p.row_group && (p.N & 3) == 0) {
+      if (p.resid)
+        epilogue_staged<EPI, 128, true>(p, acc, smem, m0, n0, wm, wn, lane);
+      else
+        epilogue_staged<EPI, 128, false>(p, acc, smem, m0, n0, wm, wn, lane);
+    }
     else
       epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
   } else {
@@ -1281,7 +1303,10 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
     if (wm == 0) pp_barrier();  // re-align the groups for the epilogue
     // The next tile's first DMAs are in flight into the K-tile buffers; the epilogue stages in the
     // separate region behind them.
-    epilogue_staged<EPI, 32>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+    if (p.resid)
+      epilogue_staged<EPI, 32, true>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+    else
+      epilogue_staged<EPI, 32, false>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
     v += gridDim.x;
     if (v >= ntiles) break;
     G0 += nk;

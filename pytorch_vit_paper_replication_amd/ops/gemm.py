@@ -19,7 +19,7 @@ EPI_BF16, EPI_GELU, EPI_DGELU, EPI_F32_ATOMIC, EPI_F32_STORE = range(5)
 
 # tile configs: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves), 2 = 128x256 (8 waves)
 _FORCE_TILE = os.environ.get("PVR_GEMM_TILE")
-_PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "1") != "0"
+_PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "0") == "1"  # A/B: 12 faster once its epilogue loads were fixed
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
