@@ -35,28 +35,43 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
   const uint64_t seed = thr ? (*seed_ptr + seed_off) : 0ull;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (act) {
-    for (int r = blockIdx.y * 4 + wave; r < rows; r += gridDim.y * 4) {
-      const uint4 q = *(const uint4*)(dy + (int64_t)r * ld + c * 8);
-      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
-      float v[8];
+    // 4 rows per trip with their loads issued together (clamped rows, so the loads are
+    // unconditional and the compiler counts them instead of draining vmcnt per row)
+    constexpr int U = 4;
+    const int stride = gridDim.y * 4;
+    for (int r0 = blockIdx.y * 4 + wave; r0 < rows; r0 += U * stride) {
+      uint4 q[U];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[2 * j] = bf2f(u[j] & 0xFFFF);
-        v[2 * j + 1] = bf2f(u[j] >> 16);
-      }
-      if (thr) {
+      for (int u = 0; u < U; ++u) q[u] = *(const uint4*)(dy + (int64_t)min(r0 + u * stride, rows - 1) * ld + c * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[j] = rng_keep(seed, (uint64_t)r * N + c * 8 + j, thr) ? v[j] * scale : 0.f;
-      }
-      if (dz) {
-        uint4 o;
-        o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-        o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
-        *(uint4*)(dz + (int64_t)r * ld_dz + c * 8) = o;
-      }
+      for (int u = 0; u < U; ++u) {
+        const int r = r0 + u * stride;
+        if (r >= rows) break;
+        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+        float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+        for (int j = 0; j < 4; ++j) {
+          v[2 * j] = bf2f(w[j] & 0xFFFF);
+          v[2 * j + 1] = bf2f(w[j] >> 16);
+        }
+        if (thr) {
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            bool k0, k1;
+            rng_keep2(seed, (uint64_t)r * N + c * 8 + j, thr, k0, k1);
+            v[j] = k0 ? v[j] * scale : 0.f;
+            v[j + 1] = k1 ? v[j + 1] * scale : 0.f;
+          }
+        }
+        if (dz) {
+          uint4 o;
+          o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+          o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+          *(uint4*)(dz + (int64_t)r * ld_dz + c * 8) = o;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
     }
   }
 #pragma unroll

@@ -109,23 +109,36 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
   // before the current row's two wave reductions, so HBM latency overlaps the shuffles.
   const int stride = gridDim.x * 4;
   uint4 cx[MAXCH], cdy[MAXCH], cr[MAXCH];
+  // unconditional (clamped) loads: the compiler can then count them instead of waiting vmcnt(0)
   auto load_row = [&](int row, uint4 (&qx)[MAXCH], uint4 (&qd)[MAXCH], uint4 (&qr)[MAXCH]) {
+    const int rr = min(row, rows - 1);
 #pragma unroll
     for (int i = 0; i < MAXCH; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nch && row < rows) {
-        qx[i] = *(const uint4*)(x + (int64_t)row * x_stride + c * 8);
-        qd[i] = *(const uint4*)(dy + (int64_t)row * dy_stride + c * 8);
-        if (dres) qr[i] = *(const uint4*)(dres + (int64_t)row * dres_stride + c * 8);
-      }
+      const int c = min(lane + 64 * i, nch - 1);
+      qx[i] = *(const uint4*)(x + (int64_t)rr * x_stride + c * 8);
+      qd[i] = *(const uint4*)(dy + (int64_t)rr * dy_stride + c * 8);
+      qr[i] = dres ? *(const uint4*)(dres + (int64_t)rr * dres_stride + c * 8) : make_uint4(0, 0, 0, 0);
     }
   };
+  // gamma is loop-invariant: keep this lane's columns in registers (a per-row reload would be
+  // waited with vmcnt(0), which also drains the next row's prefetch)
+  float wreg[MAXCH][8];
+#pragma unroll
+  for (int i = 0; i < MAXCH; ++i) {
+    const int c = min(lane + 64 * i, nch - 1);
+    const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
+    wreg[i][0] = w0.x; wreg[i][1] = w0.y; wreg[i][2] = w0.z; wreg[i][3] = w0.w;
+    wreg[i][4] = w1.x; wreg[i][5] = w1.y; wreg[i][6] = w1.z; wreg[i][7] = w1.w;
+  }
   int row = blockIdx.x * 4 + wave;
   load_row(row, cx, cdy, cr);
+  float cmu = row < rows ? mean[row] : 0.f, crs = row < rows ? rstd[row] : 0.f;
   for (; row < rows; row += stride) {
     uint4 nx[MAXCH], ndy[MAXCH], nr[MAXCH];
     load_row(row + stride, nx, ndy, nr);
-    const float mu = mean[row], rs = rstd[row];
+    const int rn = min(row + stride, rows - 1);
+    const float nmu = mean[rn], nrs = rstd[rn];
+    const float mu = cmu, rs = crs;
     float xh[MAXCH][8], g[MAXCH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -134,8 +147,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
       if (c < nch) {
         const uint32_t ux[4] = {cx[i].x, cx[i].y, cx[i].z, cx[i].w};
         const uint32_t ud[4] = {cdy[i].x, cdy[i].y, cdy[i].z, cdy[i].w};
-        const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
-        const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float* ww = wreg[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float xv = bf2f(j & 1 ? ux[j >> 1] >> 16 : ux[j >> 1] & 0xFFFF);
@@ -176,6 +188,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
       cdy[i] = ndy[i];
       cr[i] = nr[i];
     }
+    cmu = nmu;
+    crs = nrs;
   }
   // block reduction of the dgamma / dbeta / dsum partials, one quantity at a time through a
   // [4][D] LDS buffer (keeps LDS at 4*D*4 bytes so occupancy is register-, not LDS-, bound),
