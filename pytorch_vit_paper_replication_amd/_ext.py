@@ -22,8 +22,12 @@ def load():
     if _TRIED:
         return _C
     _TRIED = True
+    debug = os.environ.get("PVR_DEBUG_KERNELS", "0") == "1"
     try:
-        from . import _C as mod  # noqa: F401  (built in-tree)
+        if debug:  # kernels with device-side invariant checks (build_extension(debug=True))
+            from . import _C_debug as mod  # noqa: F401
+        else:
+            from . import _C as mod  # noqa: F401  (built in-tree)
 
         _C = mod
     except BaseException as e:  # pragma: no cover - depends on build state
@@ -32,8 +36,11 @@ def load():
             try:
                 from .build import build_extension
 
-                build_extension()
-                from . import _C as mod2
+                build_extension(debug=debug)
+                if debug:
+                    from . import _C_debug as mod2
+                else:
+                    from . import _C as mod2
 
                 _C = mod2
                 _ERR = None

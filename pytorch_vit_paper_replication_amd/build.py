@@ -25,8 +25,8 @@ if ARCH != "gfx950":  # this framework is written for CDNA4 only
     ARCH = "gfx950"
 
 
-def ext_path() -> Path:
-    return PKG_DIR / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+def ext_path(debug: bool = False) -> Path:
+    return PKG_DIR / (("_C_debug" if debug else "_C") + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
 def _torch_dirs():
@@ -55,9 +55,15 @@ def _run(cmd):
     return r.stdout
 
 
-def build_extension(verbose: bool = False, force: bool = False, jobs: int | None = None) -> Path:
-    """Compile every HIP kernel for gfx950 and link the torch extension. Returns the .so path."""
-    BUILD_DIR.mkdir(exist_ok=True)
+def build_extension(verbose: bool = False, force: bool = False, jobs: int | None = None, debug: bool = False) -> Path:
+    """Compile every HIP kernel for gfx950 and link the torch extension. Returns the .so path.
+
+    ``debug=True`` builds ``_C_debug`` (separate objects) with ``-DPVR_DEBUG``: device-side
+    ``PVR_ASSERT`` invariant checks in the kernels; load it with ``PVR_DEBUG_KERNELS=1``."""
+    build_dir = BUILD_DIR.with_name("_build_debug") if debug else BUILD_DIR
+    build_dir.mkdir(exist_ok=True)
+    ext_name = "_C_debug" if debug else "_C"
+    dbg_flags = ["-DPVR_DEBUG"] if debug else []
     inc, lib = _torch_dirs()
     py_inc = sysconfig.get_paths()["include"]
     headers = list(CSRC.glob("*.h"))
@@ -69,22 +75,22 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
         "-munsafe-fp-atomics", "-Wno-unused-result",
     ]
     for src in hip_srcs:
-        obj = BUILD_DIR / (src.stem + ".o")
+        obj = build_dir / (src.stem + ".o")
         objs.append(obj)
         if force or _newer([src, *headers], obj):
-            jobs_list.append([_hipcc(), *hip_flags, "-c", str(src), "-o", str(obj)])
+            jobs_list.append([_hipcc(), *hip_flags, *dbg_flags, "-c", str(src), "-o", str(obj)])
     import torch
 
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     cxx = os.environ.get("CXX", "g++")
     for cpp in sorted(CSRC.glob("*.cpp")):  # host-only translation units (ATen / pybind11 / RCCL)
-        obj = BUILD_DIR / (cpp.stem + ".o")
+        obj = build_dir / (cpp.stem + ".o")
         objs.append(obj)
         if force or _newer([cpp, *headers], obj):
             jobs_list.append([
                 cxx, "-O2", "-std=c++17", "-fPIC", "-c", str(cpp), "-o", str(obj),
                 "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                f"-DTORCH_EXTENSION_NAME={ext_name}", "-DTORCH_API_INCLUDE_EXTENSION_H", *dbg_flags,
                 f"-I{inc}", f"-I{inc / 'torch' / 'csrc' / 'api' / 'include'}", "-I/opt/rocm/include", f"-I{py_inc}",
                 "-w",
             ])
@@ -94,7 +100,7 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
             for out in ex.map(_run, jobs_list):
                 if verbose and out.strip():
                     print(out)
-    so = ext_path()
+    so = ext_path(debug)
     if force or jobs_list or not so.exists():
         link = [
             _hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(so),
@@ -109,5 +115,5 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
 
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    p = build_extension(verbose=True, force=force)
+    p = build_extension(verbose=True, force=force, debug="--debug" in sys.argv)
     print(p)

@@ -272,6 +272,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int bh = L / nkb, b = bh / H, h = bh % H;
   const int kb0 = (L % nkb) * KB;
   const int kw0 = kb0 + wave * 32;
+  PVR_ASSERT(kb0 < N && L < (int)gridDim.x && (KB & (KB - 1)) == 0);
 
   // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh]) | dS [32][KB] | 2 x (lse2[32] | delta[32])
   // Q / dO / lse / delta of query block qb+1 are staged while block qb is processed.

@@ -17,6 +17,24 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Debug builds (build_extension(debug=True) -> _C_debug, loaded with PVR_DEBUG_KERNELS=1) check
+// kernel invariants on the device: a violated one prints its location and traps, so the failing
+// launch is reported by the HIP runtime instead of corrupting memory silently.
+#ifdef PVR_DEBUG
+#define PVR_ASSERT(cond)                                                                     \
+  do {                                                                                       \
+    if (!(cond)) {                                                                           \
+      printf("PVR_ASSERT failed %s:%d (block %d thread %d): %s\n", __FILE__, __LINE__,        \
+             (int)blockIdx.x, (int)threadIdx.x, #cond);                                      \
+      __builtin_trap();                                                                      \
+    }                                                                                        \
+  } while (0)
+#else
+#define PVR_ASSERT(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace pvr {
 
 PVR_DEV float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }

@@ -1065,6 +1065,8 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   const int wm = wave >> 2, wn = wave & 3;  // group = wm
 
   const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
+  PVR_ASSERT(blockDim.x == 512 && (int)blockIdx.x < ntm * ntn);
+  PVR_ASSERT(ES == 2 || (p.K % 128 == 0 && p.scale_a && p.scale_b));
   const int tt = xcd_remap(blockIdx.x, ntm * ntn);
   const int m0 = (tt / ntn) * 256, n0 = (tt % ntn) * 256;
   // split-K (wgrad over tokens): this workgroup reduces k in [kbeg, kend)
@@ -1072,6 +1074,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   const int kend = min(p.K, kbeg + p.k_split_len);
   constexpr int BKE = 128 / ES;  // K-tile depth in elements (64 bf16 / 128 fp8)
   const int nk = (kend - kbeg + BKE - 1) / BKE;  // k-contiguous operands: K % BKE == 0 (host check)
+  PVR_ASSERT(!(AK || BKC) || (p.K % BKE == 0 && kbeg % BKE == 0));
 
   const void* abase;
   uint32_t abytes;

@@ -17,6 +17,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const uint16_t* __restrict_
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int nch = D >> 3;
+  PVR_ASSERT((D & 7) == 0 && nch <= 64 * MAXCH);
   const uint16_t* xr = x + (int64_t)row * x_stride;
   float v[MAXCH][8];
   float s = 0.f;

@@ -29,6 +29,7 @@ except Exception:  # pragma: no cover
         return x
 
 from .ops.fused_vit import cross_entropy
+from .utils.profiling import range_push
 
 
 def _is_dist() -> bool:
@@ -79,11 +80,14 @@ def train_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, opt
     nb = 0
     for X, y in dataloader:
         X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
-        y_pred = model(X)
-        loss = lf(y_pred, y)
+        with range_push("forward"):  # ROCTX ranges (PVR_ROCTX=1, rocprofv3 --marker-trace)
+            y_pred = model(X)
+            loss = lf(y_pred, y)
         optimizer.zero_grad()
-        loss.backward()
-        _clip_and_step(model, optimizer, max_grad_norm)
+        with range_push("backward"):
+            loss.backward()
+        with range_push("optimizer"):
+            _clip_and_step(model, optimizer, max_grad_norm)
         lr_scheduler.step()
         with torch.no_grad():
             acc = (y_pred.argmax(dim=1) == y).sum().float() / y_pred.shape[0]
