@@ -5,29 +5,13 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include "gemm_params.h"
+
 namespace pybind11 { class module_; }
 namespace pvr_comm { void register_comm(pybind11::module_& m); }
 
 namespace pvr {
-struct GemmParams {
-  int M, N, K;
-  const uint16_t* A; int64_t lda; int a_kcontig;
-  const uint16_t* B; int64_t ldb; int b_kcontig;
-  void* C; int64_t ldc;
-  const float* bias;
-  const uint16_t* resid; int64_t ld_resid;
-  const float* addend; int addend_period;
-  uint16_t* aux; int64_t ld_aux;
-  int row_group, row_stride_group, row_offset;
-  const uint64_t* seed_ptr; uint64_t seed_offset; uint32_t drop_thr; float drop_scale;
-  int k_split_len;
-  int epi;
-  int tile_cfg;
-  uint64_t* dbg;
-  float* colsum;
-  const float* scale_a; const float* scale_b;
-  int elem8, fmt_a, fmt_b;
-};
+
 struct AdamGroup {
   float lr, beta1, beta2, eps, weight_decay;
   float bc1, bc2_sqrt;
@@ -40,6 +24,7 @@ hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
+hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
@@ -122,7 +107,15 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   }
   const bool f32out = epi >= 3;
   TORCH_CHECK(C.is_cuda() && C.scalar_type() == (f32out ? torch::kFloat32 : torch::kBFloat16), "gemm: C dtype mismatch for epilogue");
-  p.C = C.data_ptr(); p.ldc = ld_of(C, "C");
+  if (C.dim() == 3) {  // split-K partials [splits, M, N] (EPI_F32_STORE, tile 14)
+    TORCH_CHECK(epi == 4 && tile_cfg == 14, "gemm: a 3-D C is the split-K workspace of EPI_F32_STORE / tile 14");
+    TORCH_CHECK(C.stride(2) == 1 && C.size(1) >= M && C.size(2) >= N, "gemm: workspace shape");
+    const int64_t ks = k_split > 0 ? ((k_split + 63) / 64) * 64 : ((K + 63) / 64) * 64;
+    TORCH_CHECK(C.size(0) >= (K + ks - 1) / ks, "gemm: workspace has fewer slices than K splits");
+    p.C = C.data_ptr(); p.ldc = C.stride(1); p.split_stride = C.stride(0);
+  } else {
+    p.C = C.data_ptr(); p.ldc = ld_of(C, "C");
+  }
   if (bias.has_value() && bias->defined()) { TORCH_CHECK(bias->numel() >= N && bias->is_contiguous(), "bias"); p.bias = f32(*bias, "bias"); }
   if (resid.has_value() && resid->defined()) { p.resid = bf(*resid, "resid"); p.ld_resid = ld_of(*resid, "resid"); }
   if (addend.has_value() && addend->defined()) { p.addend = f32(*addend, "addend"); p.addend_period = (int)addend_period; TORCH_CHECK(addend_period > 0, "addend_period"); }
@@ -166,6 +159,15 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
                           opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
                           opt_ptr<float>(db), opt_ptr<float>(dsum), (int)rows, (int)D, stream()),
         "layernorm_bwd");
+}
+
+// out (+)= ws.sum(0) for a split-K workspace ws [S, rows, cols] (out: contiguous [rows, cols])
+void splitk_reduce(torch::Tensor ws, int64_t S, torch::Tensor out, bool accumulate) {
+  TORCH_CHECK(ws.dim() == 3 && ws.size(0) >= S && S >= 1, "splitk_reduce: ws must be [S, rows, cols]");
+  TORCH_CHECK(out.is_contiguous() && ws.stride(2) == 1 && ws.stride(1) == ws.size(2) && out.numel() == ws.size(1) * ws.size(2),
+              "splitk_reduce: layouts");
+  check(pvr_splitk_reduce(f32(ws, "ws"), (int)S, ws.stride(0), f32_mut(out, "out"), out.numel(), accumulate ? 1 : 0, stream()),
+        "splitk_reduce");
 }
 
 void cast_f32_bf16(torch::Tensor in, torch::Tensor out) {
@@ -416,6 +418,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),
         py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none());
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("splitk_reduce", &splitk_reduce);
   m.def("transpose_batched", &transpose_batched);
   m.def("colsum", &colsum);
   m.def("im2col", &im2col);

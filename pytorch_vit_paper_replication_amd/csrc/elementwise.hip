@@ -170,8 +170,44 @@ __global__ void __launch_bounds__(256) transpose_batched_kernel(const uint16_t* 
   }
 }
 
+// out (+)= sum over S split-K partial slices ws[s][i] (i < n, n % 4 == 0): the second half of the
+// store-then-reduce wgrad (tile 14); fixed slice order, so the result is deterministic
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t stride,
+                                                            float* __restrict__ out, int64_t n4, int accumulate) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 a = accumulate ? ((const float4*)out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* src = ws + 4 * i;
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {  // 4 independent loads in flight per trip
+      const float4 b0 = *(const float4*)(src + (int64_t)s * stride);
+      const float4 b1 = *(const float4*)(src + (int64_t)(s + 1) * stride);
+      const float4 b2 = *(const float4*)(src + (int64_t)(s + 2) * stride);
+      const float4 b3 = *(const float4*)(src + (int64_t)(s + 3) * stride);
+      a.x += (b0.x + b1.x) + (b2.x + b3.x);
+      a.y += (b0.y + b1.y) + (b2.y + b3.y);
+      a.z += (b0.z + b1.z) + (b2.z + b3.z);
+      a.w += (b0.w + b1.w) + (b2.w + b3.w);
+    }
+    for (; s < S; ++s) {
+      const float4 b = *(const float4*)(src + (int64_t)s * stride);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    ((float4*)out)[i] = a;
+  }
+}
+
 }  // namespace
 }  // namespace pvr
+
+extern "C" hipError_t pvr_splitk_reduce(const float* ws, int S, int64_t stride, float* out, int64_t n, int accumulate, hipStream_t s) {
+  using namespace pvr;
+  if (n <= 0) return hipSuccess;
+  if (n % 4 || stride % 4) return hipErrorInvalidValue;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, S, stride, out, n / 4, accumulate);
+  return hipGetLastError();
+}
 
 // meta: int64 [nmat][5] = {src_off, dst_off, rows, cols, tile_prefix}; total_tiles = sum of tiles
 extern "C" hipError_t pvr_transpose_batched(const uint16_t* src, uint16_t* dst, const int64_t* meta, int nmat, int total_tiles,

@@ -18,6 +18,7 @@
 // ds_read_b64_tr_b16 hardware transpose for mn-contig). Two LDS stages: the DMA for tile t+1 is in
 // flight while the MFMAs of tile t run.
 #include "common.h"
+#include "gemm_params.h"
 #include <type_traits>
 
 namespace pvr {
@@ -30,27 +31,7 @@ enum GemmEpi : int {
   EPI_F32_STORE = 4,   // out = acc                                              (f32)
 };
 
-struct GemmParams {
-  int M, N, K;
-  const uint16_t* A; int64_t lda; int a_kcontig;
-  const uint16_t* B; int64_t ldb; int b_kcontig;
-  void* C; int64_t ldc;
-  const float* bias;
-  const uint16_t* resid; int64_t ld_resid;
-  const float* addend; int addend_period;
-  uint16_t* aux; int64_t ld_aux;
-  int row_group, row_stride_group, row_offset;
-  const uint64_t* seed_ptr; uint64_t seed_offset; uint32_t drop_thr; float drop_scale;
-  int k_split_len;
-  int epi;
-  int tile_cfg;
-  uint64_t* dbg;  // diagnostic s_memtime stamps [block][4] (null in normal runs)
-  float* colsum;  // optional: += column sums of the bf16-type output (a fused bias gradient)
-  // fp8 operands (elem8 = 1): A / B hold 1-byte OCP fp8 (fmt 0 = e4m3, 1 = e5m2), lda / ldb in
-  // bytes; the accumulator is multiplied by (*scale_a) * (*scale_b) (per-tensor dequant factors)
-  const float* scale_a; const float* scale_b;
-  int elem8, fmt_a, fmt_b;
-};
+
 
 namespace {
 
@@ -959,6 +940,33 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   constexpr int NPASS = 256 / RP, FPP = RP / 16;  // passes; fragment rows (of 8 per wave) per pass
 #pragma unroll
   for (int half = 0; half < NPASS; ++half) {
+    if constexpr (EPI == EPI_F32_ATOMIC) {
+      // split-K partial sums: each wave instruction adds one dense 256-B run of a row (thread =
+      // column), two cache lines per request instead of 4 rows x 64 B
+      __syncthreads();
+      if (wm == (half * RP) / 128) {
+        const int i0 = ((half * RP) % 128) / 16;
+#pragma unroll
+        for (int ii = 0; ii < FPP; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 16 * ii + li;
+            const int ch = wn * 16 + 4 * j + g;
+            *(v4f*)(smem + r * 1024 + ((ch ^ (r & 63)) << 4)) = acc[i0 + ii][j];
+          }
+      }
+      __syncthreads();
+      const int c = tid & 255;
+      const bool okc = n0 + c < p.N;
+#pragma unroll 8
+      for (int k = 0; k < RP / 2; ++k) {
+        const int r = (tid >> 8) + 2 * k;
+        const int m = m0 + half * RP + r;
+        const float a = *(const float*)(smem + r * 1024 + (((c >> 2) ^ (r & 63)) << 4) + 4 * (c & 3));
+        if (okc && m < p.M) atomicAdd((float*)p.C + (int64_t)m * p.ldc + n0 + c, a * deq);
+      }
+      continue;
+    }
     __syncthreads();  // previous pass's LDS reads (or the main loop's) are done
     if (wm == (half * RP) / 128) {
       const int i0 = ((half * RP) % 128) / 16;
@@ -1026,7 +1034,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
           uint2 ax; ax.x = pack2bf(gp[0], gp[1]); ax.y = pack2bf(gp[2], gp[3]);
           if (ok) *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = ax;
         }
-      } else {  // EPI_DGELU
+      } else if constexpr (EPI == EPI_DGELU) {
         const uint2 gg = pin[k];
         v[0] *= bf2f(gg.x & 0xFFFF); v[1] *= bf2f(gg.x >> 16);
         v[2] *= bf2f(gg.y & 0xFFFF); v[3] *= bf2f(gg.y >> 16);
@@ -1034,8 +1042,12 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
           csum[0] += v[0]; csum[1] += v[1]; csum[2] += v[2]; csum[3] += v[3];
         }
       }
-      uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-      if (ok) *(uint2*)((uint16_t*)p.C + (int64_t)m * p.ldc + n) = o;
+      if constexpr (EPI == EPI_F32_STORE) {
+        if (ok) *(float4*)((float*)p.C + (int64_t)blockIdx.z * p.split_stride + (int64_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+        if (ok) *(uint2*)((uint16_t*)p.C + (int64_t)m * p.ldc + n) = o;
+      }
     }
   }
   if constexpr (EPI == EPI_DGELU) {
@@ -1137,7 +1149,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
   stamp(p, 2);
-  if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
+  if constexpr (SWAP && (EPI == EPI_F32_ATOMIC || EPI == EPI_F32_STORE)) {
+    if ((p.N & 3) == 0 && !p.row_group)
+      epilogue_staged<EPI, 128, false>(p, acc, smem, m0, n0, wm, wn, lane);
+    else
+      epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+  } else if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
     if (!p.addend && !p.row_group && (p.N & 3) == 0) {
       if (p.resid)
         epilogue_staged<EPI, 128, true>(p, acc, smem, m0, n0, wm, wn, lane);
@@ -1420,10 +1437,17 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
       if (ak && !bk) return launch_tile<true, false, true, EPI_DGELU>(p, s);
       break;
     case EPI_F32_ATOMIC:
+      // tile 14: ping-pong with the LDS-staged f32 epilogue (split-K wgrad)
+      if (p.tile_cfg == 14 && ak == bk && p.k_split_len % PP_BK == 0 && (!ak || p.K % PP_BK == 0))
+        return ak ? launch_pp<true, true, true, EPI_F32_ATOMIC>(p, s) : launch_pp<false, false, true, EPI_F32_ATOMIC>(p, s);
       if (!ak && !bk) return launch_tile<false, false, false, EPI_F32_ATOMIC>(p, s);
       if (ak && bk) return launch_tile<true, true, false, EPI_F32_ATOMIC>(p, s);
       break;
     case EPI_F32_STORE:
+      // tile 14: per-split partials C + z * split_stride (split_stride 0: one K range only)
+      if (p.tile_cfg == 14 && ak == bk && p.k_split_len % PP_BK == 0 && (!ak || p.K % PP_BK == 0))
+        return ak ? launch_pp<true, true, true, EPI_F32_STORE>(p, s) : launch_pp<false, false, true, EPI_F32_STORE>(p, s);
+      if (p.split_stride) return hipErrorInvalidValue;
       if (!ak && !bk) return launch_tile<false, false, false, EPI_F32_STORE>(p, s);
       if (ak && bk) return launch_tile<true, true, false, EPI_F32_STORE>(p, s);
       break;

@@ -1,0 +1,32 @@
+// Launch parameters of the GEMM kernels (csrc/gemm.hip), shared with the host bindings
+// (bindings.cpp, compiled by g++): plain C++, no HIP headers.
+#pragma once
+#include <stdint.h>
+
+namespace pvr {
+
+struct GemmParams {
+  int M, N, K;
+  const uint16_t* A; int64_t lda; int a_kcontig;
+  const uint16_t* B; int64_t ldb; int b_kcontig;
+  void* C; int64_t ldc;
+  const float* bias;
+  const uint16_t* resid; int64_t ld_resid;
+  const float* addend; int addend_period;
+  uint16_t* aux; int64_t ld_aux;
+  int row_group, row_stride_group, row_offset;
+  const uint64_t* seed_ptr; uint64_t seed_offset; uint32_t drop_thr; float drop_scale;
+  int k_split_len;
+  int epi;
+  int tile_cfg;
+  uint64_t* dbg;  // diagnostic s_memtime stamps [block][4] (null in normal runs)
+  float* colsum;  // optional: += column sums of the bf16-type output (a fused bias gradient)
+  // fp8 operands (elem8 = 1): A / B hold 1-byte OCP fp8 (fmt 0 = e4m3, 1 = e5m2), lda / ldb in
+  // bytes; the accumulator is multiplied by (*scale_a) * (*scale_b) (per-tensor dequant factors)
+  const float* scale_a; const float* scale_b;
+  int elem8, fmt_a, fmt_b;
+  // EPI_F32_STORE with split-K (tile 14): split z writes its partial to C + z * split_stride
+  int64_t split_stride;
+};
+
+}  // namespace pvr

@@ -105,15 +105,44 @@ def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
     return s
 
 
+_SPLITK_REDUCE = os.environ.get("PVR_WGRAD_REDUCE", "1") == "1"
+_workspaces = {}  # (device index, stream id) -> flat f32 split-K workspace
+
+
+def _workspace(numel: int, device: torch.device) -> torch.Tensor:
+    """Split-K partial buffer, one per (device, stream): weight-gradient GEMMs on one stream are
+    serialised, so they can share it; grown (never shrunk) to the largest request."""
+    key = (device.index, torch.cuda.current_stream(device).stream_id)
+    ws = _workspaces.get(key)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(numel, dtype=torch.float32, device=device)
+        _workspaces[key] = ws
+    return ws
+
+
 def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    """out[N, K] += dy^T . x   (fp32, split over tokens with f32 atomics)."""
+    """out[N, K] += dy^T . x   (fp32, split over tokens).
+
+    Large token counts (tile 12/14 ping-pong) write each split's partial product to a workspace with
+    LDS-staged coalesced stores, then one reduction pass adds the slices into ``out`` in a fixed
+    order. That is 8-25 % faster than f32 atomics at ViT-B/16 shapes (the L2 executes atomics one
+    element at a time, profiles/wgrad_epilogue_ab.log) and makes the weight gradients deterministic.
+    Small GEMMs accumulate with f32 atomics."""
     T, N = dy.shape
     K = x.shape[1]
     tile = _tile(N, K, T, "wgrad")
     splits = wgrad_splits(T, N, K, tile)
     ksplit = math.ceil(math.ceil(T / splits) / 64) * 64
-    _ext.ext().gemm(dy, False, x, False, out, N, K, T, EPI_F32_ATOMIC, None, None, None, 0, None, 0, 0, 0,
-                    None, 0, 0.0, ksplit, tile)
+    ext = _ext.ext()
+    nsplit = math.ceil(T / ksplit)
+    if tile == 12 and _SPLITK_REDUCE and nsplit > 1 and out.is_contiguous() and N % 4 == 0:
+        ws = _workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
+        ext.gemm(dy, False, x, False, ws, N, K, T, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0,
+                 None, 0, 0.0, ksplit, 14)
+        ext.splitk_reduce(ws, nsplit, out, True)
+        return out
+    ext.gemm(dy, False, x, False, out, N, K, T, EPI_F32_ATOMIC, None, None, None, 0, None, 0, 0, 0,
+             None, 0, 0.0, ksplit, tile)
     return out
 
 
