@@ -17,6 +17,7 @@ elapsed time, where the timed region is bracketed by barrier + device synchroniz
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -40,6 +41,8 @@ def parse():
     p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
     p.add_argument("--bucket-mb", type=float, default=28.0)
     p.add_argument("--graph", action="store_true", help="replay the whole training step as one captured hipGraph")
+    p.add_argument("--main-prio", type=int, default=int(os.environ.get("PVR_MAIN_PRIO", "-1")),
+                   help="run the step on a stream of this priority: -1 (default) puts the dgrad chain above the weight-gradient side stream; 0 = default stream")
     return p.parse_args()
 
 
@@ -113,14 +116,21 @@ def main():
                                    scheduler=sched)
         step = graphed  # noqa: F811  (each call: graph_prepare + hipGraphLaunch + LR schedule step)
         args.warmup = 0
-    for _ in range(args.warmup):
-        loss = step()
+    stream_ctx = contextlib.nullcontext()
+    if args.main_prio != 0:
+        main_stream = torch.cuda.Stream(device=device, priority=args.main_prio)
+        main_stream.wait_stream(torch.cuda.current_stream(device))
+        stream_ctx = torch.cuda.stream(main_stream)
+    with stream_ctx:
+        for _ in range(args.warmup):
+            loss = step()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
+    with stream_ctx:
+        for _ in range(args.steps):
+            loss = step()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

@@ -75,6 +75,15 @@ PVR_DEV v8s frag_tr(const char* img, int rows, int rowA, int rowB, int c0, int l
   return cat44(lo, hi);
 }
 
+// frag_tr through ds_read_tr_async (no compiler drain of in-flight LDS-DMA in front of it); the
+// caller combines the halves with cat44 after lds_wait().
+PVR_DEV void frag_tr_async(const char* img, int rows, int rowA, int rowB, int c0, int lane, v4s& lo, v4s& hi) {
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const int chunk = (c0 >> 3) + (p >> 1);
+  lo = ds_read_tr_async(img + lds_off(rows, rowA + q, chunk) + 8 * (p & 1));
+  hi = ds_read_tr_async(img + lds_off(rows, rowB + q, chunk) + 8 * (p & 1));
+}
+
 // Global 8-element fragment at head-dim offset d0, zero past the head dim.
 template <int DH>
 PVR_DEV v8s load_frag(const uint16_t* p, int d0) {
@@ -196,12 +205,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         if (kk * 2 < nf) {
-          const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
+          // asm transpose reads: the next tile's K/V DMA stays in flight under them
+          v4s vlo[C::NE], vhi[C::NE];
 #pragma unroll
-          for (int e = 0; e < C::NE; ++e) {
-            const v8s vf = frag_tr(vimg, KT, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane);
-            o[e] = mfma16(vf, pf, o[e]);
-          }
+          for (int e = 0; e < C::NE; ++e) frag_tr_async(vimg, KT, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, vlo[e], vhi[e]);
+          const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
+          lds_wait();
+#pragma unroll
+          for (int e = 0; e < C::NE; ++e) o[e] = mfma16(cat44(vlo[e], vhi[e]), pf, o[e]);
         }
       }
     }
@@ -225,37 +236,169 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   }
 }
 
-// ------------------------------------------------------------------------- backward: delta
-// delta[bh][q] = sum_d dO[q][h*dh + d] * O[q][h*dh + d]
-template <int DH>
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                              const uint16_t* __restrict__ o, int64_t ld_o,
-                                                              float* __restrict__ delta, int B, int N, int H) {
-  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= (int64_t)B * N * H) return;
-  const int h = (int)(i % H);
-  const int64_t tok = i / H;
-  const int b = (int)(tok / N), q = (int)(tok % N);
-  const uint16_t* a = dout + tok * ld_do + h * DH;
-  const uint16_t* bb = o + tok * ld_o + h * DH;
-  float s = 0.f;
+// ------------------------------------------------------------- forward: whole head in LDS
+// N <= 256 and dh = 64 (ViT-B/16 and ViT-L/16 at 224 px: N = 197). One persistent workgroup per
+// CU walks a contiguous range of (batch, head) pairs with ceil(N/16) waves of 16 queries. Every
+// key of a head fits in LDS, so
+//   * each query row's softmax is exact in one pass (no running max, no rescaling of O);
+//   * the head's K/V are staged once instead of once per 64-query workgroup;
+//   * the next pair's K/V LDS-DMA (second buffer) and Q fragments are in flight under this pair's
+//     math, and its O rows are stored one pair late, so no store sits in front of a DMA wait.
+// Key rows past N (padding to a multiple of 32 for the P.V k-steps) read as zero.
+template <int NF>
+__global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                              uint16_t* __restrict__ out, int64_t ld_o,
+                                                              float* __restrict__ lse, int N, int H, int D,
+                                                              int npairs, float scale) {
+  constexpr int DH = 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NP = 32 * ((NF + 1) / 2);  // staged key rows
+  constexpr int BUF = 2 * NP * 128;         // K | V images of one (batch, head)
+  constexpr int NW = NF;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  constexpr int nf = NF;  // 16-key fragments holding a valid key, one wave each
+  PVR_ASSERT((N + 15) / 16 == NF && blockDim.x == NF * 64 && (int)gridDim.x <= npairs);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
+  const int p0 = L * per + min(L, rem);
+  const int p1 = p0 + per + (L < rem ? 1 : 0);
+  const int qrow = min(wave * 16 + li, N - 1);
+  const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
+  const float c = scale * LOG2E;
+
+  auto issue = [&](int pr, char* buf) {
+    const uint16_t* base = qkv + (int64_t)(pr / H) * N * ld + (pr % H) * DH;
+    dma_rows<1>(make_rsrc(base + D, extent), buf, NP, ld, 0, wave, NW, lane);
+    dma_rows<1>(make_rsrc(base + 2 * D, extent), buf + NP * 128, NP, ld, 0, wave, NW, lane);
+  };
+  auto load_q = [&](int pr, v8s (&qf)[2]) {
+    const uint16_t* qp = qkv + ((int64_t)(pr / H) * N + qrow) * ld + (pr % H) * DH + 8 * g;
+    qf[0] = *(const v8s*)qp;
+    qf[1] = *(const v8s*)(qp + 32);
+  };
+  // O^T layout: lane holds O[q = 16 wave + li][d = 16e + 4g + r]. Stores go through range-checked
+  // buffer resources: a lane with nothing to write gets an offset past the extent and its store is
+  // dropped, so every wave issues exactly STORES store instructions per pair and the loop's wait
+  // below can retire the DMAs issued before them without waiting for the stores.
+  constexpr int STORES = 5;
+  const uint32_t o_extent = clamp_bytes(((int64_t)(N - 1) * ld_o + DH) * 2);
+  auto store_o = [&](int pr, const v4f (&o)[4], float m, float l) {
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    const int q = wave * 16 + li;
+    const bool ok = q < N;
+    const float inv = 1.f / l;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(out + (int64_t)(pr / H) * N * ld_o + (pr % H) * DH, o_extent);
+    const uint32_t vo = ok ? (uint32_t)((q * ld_o + 4 * g) * 2) : 0x80000000u;
 #pragma unroll
-  for (int c = 0; c < DH / 8; ++c) {
-    const uint4 x = *(const uint4*)(a + c * 8), y = *(const uint4*)(bb + c * 8);
-    const uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+    for (int e = 0; e < 4; ++e) {
+      const v2u w = {pack2bf(o[e][0] * inv, o[e][1] * inv), pack2bf(o[e][2] * inv, o[e][3] * inv)};
+      __builtin_amdgcn_raw_buffer_store_b64(w, rs, vo + 32 * e, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t ls = make_rsrc(lse + (int64_t)pr * N, (uint32_t)N * 4);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((m + __log2f(l)) * LN2), ls,
+                                          ok && g == 0 ? (uint32_t)q * 4 : 0x80000000u, 0, 0);
+  };
+
+  if (p0 >= p1) return;  // uniform: the host launches at most npairs workgroups
+  v8s qf[2], qn[2];
+  issue(p0, smem);
+  load_q(p0, qf);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  asm volatile("" : "+v"(qf[0]), "+v"(qf[1]));
+  for (int pr = p0; pr < p1; ++pr) {
+    const int it = pr - p0;
+    const char* kimg = smem + (it & 1) * BUF;
+    const char* vimg = kimg + NP * 128;
+    if (pr + 1 < p1) {
+      issue(pr + 1, smem + ((it + 1) & 1) * BUF);
+      load_q(pr + 1, qn);
+    }
+    // S^T[key][q] = K . Q^T: the query on the MFMA lane, keys down the accumulator rows
+    v4f s[16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      s += bf2f(xa[j] & 0xFFFF) * bf2f(ya[j] & 0xFFFF) + bf2f(xa[j] >> 16) * bf2f(ya[j] >> 16);
+    for (int f = 0; f < 16; ++f) {
+      s[f] = v4f{0.f, 0.f, 0.f, 0.f};
+      if (f < nf) {
+        s[f] = mfma16(frag_rows(kimg, NP, 16 * f, 0, lane), qf[0], s[f]);
+        s[f] = mfma16(frag_rows(kimg, NP, 16 * f, 1, lane), qf[1], s[f]);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      if (f == nf - 1) {  // keys >= N live only in the last valid fragment
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * f + 4 * g + r >= N) s[f][r] = -INFINITY;
+      }
+      if (f < nf) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[f][r]);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m = mx * c;  // scaled log2 units (c > 0)
+    float l = 0.f;
+    v4f o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
+    // O^T[d][q] += V^T[d][key] P^T[key][q], 32 keys per k-step
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      if (2 * kk < nf) {
+        // V^T fragments first (asm reads: the next pair's DMA stays in flight), softmax under them
+        v4s vlo[4], vhi[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) frag_tr_async(vimg, NP, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, vlo[e], vhi[e]);
+        v4f pa, pb = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pa[r] = __builtin_amdgcn_exp2f(fmaf(s[2 * kk][r], c, -m));
+          l += pa[r];
+        }
+        if (2 * kk + 1 < nf) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            pb[r] = __builtin_amdgcn_exp2f(fmaf(s[2 * kk + 1][r], c, -m));
+            l += pb[r];
+          }
+        }
+        const v8s pf = pack_p(pa, pb);
+        lds_wait();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = mfma16(cat44(vlo[e], vhi[e]), pf, o[e]);
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    store_o(pr, o, m, l);
+    // everything but this pair's stores has landed (the next pair's K/V images and Q fragments),
+    // and every wave is done reading this buffer before the pair after next restages it
+    static_assert(STORES == 5, "the vmcnt below counts store_o's store instructions");
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    __syncthreads();
+    qf[0] = qn[0];
+    qf[1] = qn[1];
+    // re-define qf through an empty asm: the compiler's own wait for these loads then sits here
+    // (already satisfied) instead of in front of the next pair's first MFMA, where it would also
+    // wait for that pair's K/V prefetch
+    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]));
   }
-  delta[((int64_t)b * H + h) * N + q] = s;
 }
 
-// ------------------------------------------------------------------------- backward: main
+// ------------------------------------------------------------------------- backward
 // grid (nkb, B*H), block NW*64 (NW in {1,2,4,8}); workgroup keys [kb*KB, kb*KB + KB), KB = 32*NW.
+// delta = rowsum(dO * O) of each query block is formed in-kernel from the staged dO and O rows
+// (no separate pass over dO and O, no delta round trip through HBM).
 template <int DH>
 __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                         const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                        const float* __restrict__ lse, const float* __restrict__ delta,
+                                                        const uint16_t* __restrict__ o, int64_t ld_o,
+                                                        const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
                                                         float* __restrict__ dbias, int N, int H, int D, float scale) {
   using C = Hd<DH>;
@@ -274,11 +417,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int kw0 = kb0 + wave * 32;
   PVR_ASSERT(kb0 < N && L < (int)gridDim.x && (KB & (KB - 1)) == 0);
 
-  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh]) | dS [32][KB] | 2 x (lse2[32] | delta[32])
-  // Q / dO / lse / delta of query block qb+1 are staged while block qb is processed.
+  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh] | O blk [32][dh]) | dS [32][KB] | 2 x lse [256]
+  // Q / dO / O / lse of query block qb+1 are staged while block qb is processed.
   char* kimg = smem;
   char* qdo = kimg + KB * RB;
-  char* dsimg = qdo + 4 * QB * RB;
+  char* dsimg = qdo + 6 * QB * RB;
   float* s_ld = (float*)(dsimg + QB * KB * 2);
   const int ds_cpr = KB / 8;  // 16-B chunks per dS row (power of two)
 
@@ -288,6 +431,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const __amdgpu_buffer_rsrc_t krs = make_rsrc(base + D + h * DH, clamp_bytes(extent));
   const uint16_t* dobase = dout + (int64_t)b * N * ld_do;
   const __amdgpu_buffer_rsrc_t dors = make_rsrc(dobase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2));
+  const uint16_t* obase = o + (int64_t)b * N * ld_o;
+  const __amdgpu_buffer_rsrc_t ors = make_rsrc(obase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_o + DH) * 2));
 
   // own keys' K and V fragments (B operands): lane holds X[kw0 + 16f + li][32ks + 8g + j]
   v8s kf[2][C::KS], vf[2][C::KS];
@@ -319,22 +464,17 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 
   const float c = scale * LOG2E;
   const int nqb = (N + QB - 1) / QB;
-  auto stage = [&](int qb) {  // Q / dO rows (LDS-DMA) and lse / delta of query block qb into slot qb & 1
-    // lse / delta are loaded BEFORE the DMAs: vmcnt retires in order, so their ds_write then waits
-    // only for these two loads, not for the DMAs that must stay in flight
-    const int q = qb * QB + (threadIdx.x & (QB - 1));
-    float l2 = INFINITY, dl = 0.f;
-    if (threadIdx.x < QB && q < N) {
-      l2 = lse[(int64_t)bh * N + q] * LOG2E;
-      dl = delta[(int64_t)bh * N + q];
-    }
-    char* qi = qdo + (qb & 1) * 2 * QB * RB;
+  auto stage = [&](int qb) {  // Q / dO / O rows and the lse of query block qb into slot qb & 1
+    // everything by LDS-DMA: a plain load of lse here would make hipcc wait vmcnt(0) at its first
+    // use, draining these DMAs right after issuing them. lse of queries past N reads as 0; their
+    // Q and dO rows are zero, so their P = 1 meets dO = 0 and dS = 0 and contributes nothing.
+    char* qi = qdo + (qb & 1) * 3 * QB * RB;
     dma_rows<C::NH>(qrs, qi, QB, ld, qb * QB, wave, NW, lane);
     dma_rows<C::NH>(dors, qi + QB * RB, QB, ld_do, qb * QB, wave, NW, lane);
-    if (threadIdx.x < QB) {
-      float* sl = s_ld + (qb & 1) * 2 * QB;
-      sl[threadIdx.x] = l2;
-      sl[QB + threadIdx.x] = dl;
+    dma_rows<C::NH>(ors, qi + 2 * QB * RB, QB, ld_o, qb * QB, wave, NW, lane);
+    if (wave == NW - 1) {
+      const __amdgpu_buffer_rsrc_t lrs = make_rsrc(lse + (int64_t)bh * N + qb * QB, (uint32_t)(N - qb * QB) * 4);
+      dma16(lrs, to_lds(s_ld + (qb & 1) * 256), (uint32_t)lane * 16);  // 1 KiB slot, first QB floats used
     }
   };
   stage(0);
@@ -345,14 +485,15 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (qb + 1 < nqb) stage(qb + 1);
-    const char* qimg = qdo + (qb & 1) * 2 * QB * RB;
+    const char* qimg = qdo + (qb & 1) * 3 * QB * RB;
     const char* doimg = qimg + QB * RB;
-    const float* s_lse = s_ld + (qb & 1) * 2 * QB;
-    const float* s_del = s_lse + QB;
+    const char* oimg = doimg + QB * RB;
+    const float* s_lse = s_ld + (qb & 1) * 256;
 
     if (active) {
     // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]
     v4f s[2][2], dp[2][2];
+    float dsum[2] = {0.f, 0.f};  // delta partials: query 16a + li, head dims 32ks + 8g .. +7
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -363,6 +504,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       for (int a = 0; a < 2; ++a) {
         const v8s qa = frag_rows(qimg, QB, 16 * a, ks, lane);
         const v8s da = frag_rows(doimg, QB, 16 * a, ks, lane);
+        if (DH % 32 == 0 || 32 * ks + 8 * g < DH) {  // staged dims past dh belong to the next head
+          const v8s oa = frag_rows(oimg, QB, 16 * a, ks, lane);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dsum[a] = fmaf(bf2f((uint16_t)da[j]), bf2f((uint16_t)oa[j]), dsum[a]);
+        }
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           s[a][f] = mfma16(qa, kf[f][ks], s[a][f]);
@@ -370,13 +516,18 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         }
       }
     }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      dsum[a] += __shfl_xor(dsum[a], 16, 64);
+      dsum[a] += __shfl_xor(dsum[a], 32, 64);  // every lane li: delta of query 16a + li
+    }
     // P and dS
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * a + 4 * g + r;
-        const float l2 = s_lse[ql], dl = s_del[ql];
+        const float l2 = s_lse[ql] * LOG2E, dl = __shfl(dsum[a], 4 * g + r, 64);
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const float pv = __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l2));
@@ -385,16 +536,24 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         }
       }
     // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+    // (asm transpose reads: the next query block's DMA stays in flight under this phase)
+    v8s pf[2], sf[2];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      const v8s pf = pack_p(s[0][f], s[1][f]);
-      const v8s sf = pack_p(dp[0][f], dp[1][f]);
+      pf[f] = pack_p(s[0][f], s[1][f]);
+      sf[f] = pack_p(dp[0][f], dp[1][f]);
+    }
 #pragma unroll
-      for (int e = 0; e < C::NE; ++e) {
-        const v8s dot = frag_tr(doimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane);
-        const v8s qt = frag_tr(qimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane);
-        dv[e][f] = mfma16(dot, pf, dv[e][f]);
-        dk[e][f] = mfma16(qt, sf, dk[e][f]);
+    for (int e = 0; e < C::NE; ++e) {
+      v4s dlo, dhi, qlo, qhi;
+      frag_tr_async(doimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane, dlo, dhi);
+      frag_tr_async(qimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane, qlo, qhi);
+      lds_wait();
+      const v8s dot = cat44(dlo, dhi), qt = cat44(qlo, qhi);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
+        dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
       }
     }
     // dS -> LDS (bf16) [q][key_local], chunk-swizzled by row for the dQ row reads
@@ -419,12 +578,18 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     for (int fr = wave; fr < 2 * C::NE; fr += NW, ++kfr) {
       const int a = fr / C::NE, e = fr % C::NE;
       v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-      for (int ks = 0; ks < nks_dq; ++ks) {
-        const int ql = 16 * a + li;
-        const int chunk = (ks * 4 + g) ^ (ql & (ds_cpr - 1) & 15);
-        const v8s af = ds_read_b128(dsimg + ql * KB * 2 + chunk * 16);
-        const v8s bf = frag_tr(kimg, KB, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane);
-        acc = mfma16(af, bf, acc);
+      const int ql = 16 * a + li;
+      for (int ks = 0; ks < nks_dq; ks += 2) {  // two key slices per LDS wait
+        const bool two = ks + 1 < nks_dq;
+        v4s lo0, hi0, lo1, hi1;
+        frag_tr_async(kimg, KB, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane, lo0, hi0);
+        if (two) frag_tr_async(kimg, KB, 32 * (ks + 1) + 8 * g, 32 * (ks + 1) + 8 * g + 4, 16 * e, lane, lo1, hi1);
+        const v8s af0 = ds_read_b128(dsimg + ql * KB * 2 + (((ks * 4 + g) ^ (ql & (ds_cpr - 1) & 15)) * 16));
+        const v8s af1 = two ? ds_read_b128(dsimg + ql * KB * 2 + ((((ks + 1) * 4 + g) ^ (ql & (ds_cpr - 1) & 15)) * 16))
+                            : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+        lds_wait();
+        acc = mfma16(af0, cat44(lo0, hi0), acc);
+        if (two) acc = mfma16(af1, cat44(lo1, hi1), acc);
       }
       float cs = 0.f;
 #pragma unroll
@@ -525,10 +690,61 @@ __global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict
 }  // namespace
 }  // namespace pvr
 
+static int device_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+
+// PVR_ATTN_FWD_TILED=1 forces the tiled (online-softmax) forward everywhere (A/B switch)
+static bool fwd_tiled_forced() {
+  static const bool f = [] {
+    const char* e = getenv("PVR_ATTN_FWD_TILED");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
+// whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take up to
+// 128 KiB of LDS), ceil(N/16) waves
+template <int NF>
+static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
+                                       int H, int D, float scale, hipStream_t s) {
+  using namespace pvr;
+  constexpr int SMEM = 2 * 2 * 32 * ((NF + 1) / 2) * 128;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_fwd_head_kernel<NF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int npairs = B * H;
+  const int grid = npairs < device_cus() ? npairs : device_cus();
+  hipLaunchKernelGGL(attn_fwd_head_kernel<NF>, dim3(grid), dim3(NF * 64), SMEM, s, qkv, ld, out, ld_o, lse, N, H, D, npairs, scale);
+  return hipGetLastError();
+}
+
 template <int DH>
 static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
                                   int D, float scale, hipStream_t s) {
   using namespace pvr;
+  if (DH == 64 && N <= 256 && !fwd_tiled_forced()) {
+    // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take
+    // up to 128 KiB of LDS), ceil(N/16) waves
+    switch ((N + 15) / 16) {
+#define PVR_FWD_HEAD(NF) \
+  case NF: return attn_fwd_head_launch<NF>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
+      PVR_FWD_HEAD(1) PVR_FWD_HEAD(2) PVR_FWD_HEAD(3) PVR_FWD_HEAD(4) PVR_FWD_HEAD(5) PVR_FWD_HEAD(6)
+      PVR_FWD_HEAD(7) PVR_FWD_HEAD(8) PVR_FWD_HEAD(9) PVR_FWD_HEAD(10) PVR_FWD_HEAD(11) PVR_FWD_HEAD(12)
+      PVR_FWD_HEAD(13) PVR_FWD_HEAD(14) PVR_FWD_HEAD(15) PVR_FWD_HEAD(16)
+#undef PVR_FWD_HEAD
+      default: break;
+    }
+  }
   // 1-D grid of (B*H) x query blocks, XCD-remapped in-kernel
   hipLaunchKernelGGL(attn_fwd_kernel<DH>, dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
   return hipGetLastError();
@@ -562,27 +778,25 @@ extern "C" int pvr_attn_bwd_waves(int N) {
 
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                  int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                  int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                   float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
-  const int64_t nrows = (int64_t)B * N * H;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel<DH>, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, dout, ld_do, out, ld_o, delta,
-                     B, N, H);
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
   if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   const int RB = 128 * Hd<DH>::NH;
-  const size_t smem = (size_t)KB * RB + 4 * 32 * RB + 32 * KB * 2 + 4 * 32 * 4;
+  // K image | 2 x (Q | dO | O) blocks | dS | 2 x 1 KiB lse DMA slots
+  const size_t smem = (size_t)KB * RB + 6 * 32 * RB + 32 * KB * 2 + 2 * 1024;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)(8 * 32 * RB + 4 * 32 * RB + 32 * 8 * 32 * 2 + 4 * 32 * 4));
+                                             (int)(8 * 32 * RB + 6 * 32 * RB + 32 * 8 * 32 * 2 + 2 * 1024));
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
+  hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq,
                      nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
@@ -597,14 +811,14 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
 // dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
 // every element is written), whose row sum is the in_proj bias gradient.
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                   int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                    float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
   switch (D / H) {
-    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -72,6 +72,24 @@ PVR_DEV v4s ds_read_tr(const void* lds_ptr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)lds_ptr);
 }
 
+// The same read as inline asm. hipcc models the ds_read_tr builtin as possibly writing LDS, so it
+// drains every in-flight LDS-DMA (s_waitcnt vmcnt(0)) in front of it, which defeats a prefetch of
+// the next tile into the other buffer. The asm form is invisible to the compiler's wait insertion:
+// the caller waits for it with lds_wait() before the first use of the result.
+PVR_DEV v4s ds_read_tr_async(const void* lds_ptr) {
+  v4s r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_ptr;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// Wait for every outstanding LDS read (including ds_read_tr_async) and keep the compiler from
+// scheduling their consumers above the wait (an MFMA has no memory operand, so the asm's "memory"
+// clobber alone does not order it).
+PVR_DEV void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 PVR_DEV v8s ds_read_b128(const void* lds_ptr) {
   return *(const __attribute__((address_space(3))) v8s*)lds_ptr;
 }

@@ -96,6 +96,20 @@ PVR_DEV v8s read_frag(const char* lds, int r0, int ks, int lane) {
   }
 }
 
+// read_frag<R, false> as two ds_read_tr_async halves (no compiler-inserted drain of in-flight
+// LDS-DMA); the caller combines them with cat44 after lds_wait()
+template <int R>
+PVR_DEV void read_frag_mn_async(const char* lds, int r0, int ks, int lane, v4s& lo, v4s& hi) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = (r0 >> 3) + (p >> 1);
+  const int kr0 = ks * 32 + 8 * g + q;
+  const int kr1 = kr0 + 4;
+  const int pc0 = (c & ~15) | ((c & 15) ^ swz_mn(kr0));
+  const int pc1 = (c & ~15) | ((c & 15) ^ swz_mn(kr1));
+  lo = ds_read_tr_async(lds + kr0 * (R * 2) + pc0 * 16 + 8 * (p & 1));
+  hi = ds_read_tr_async(lds + kr1 * (R * 2) + pc1 * 16 + 8 * (p & 1));
+}
+
 PVR_DEV uint32_t rsrc_bytes(int64_t extent_elems, int64_t base_elems) {
   int64_t b = (extent_elems - base_elems) * 2;
   if (b < 0) b = 0;
@@ -850,7 +864,10 @@ template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool 
 PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
                       __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
                       int t_issue, int nk, int wave, int lane, int wm, int wn) {
-  // R: register subtile for this quadrant
+  // R: register subtile for this quadrant. mn-contiguous operands are read with the asm transpose
+  // read (halves combined after the wait below): the builtin would make hipcc drain the in-flight
+  // half-tile DMAs (vmcnt(0)) in front of the read.
+  v4s alo[4][2], ahi[4][2], blo[2][2], bhi[2][2];
   if constexpr (RD_A) {
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
@@ -861,7 +878,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
         else if constexpr (AK)
           af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
         else
-          af[ii][ks] = read_frag<128, false>(buf + QM * 16384, wm * 64 + 16 * ii, ks, lane);
+          read_frag_mn_async<128>(buf + QM * 16384, wm * 64 + 16 * ii, ks, lane, alo[ii][ks], ahi[ii][ks]);
       }
   }
   if constexpr (RD_B) {
@@ -874,13 +891,28 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
         else if constexpr (BKC)
           bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
         else
-          bf[QN][jj][ks] = read_frag<128, false>(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, ks, lane);
+          read_frag_mn_async<128>(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, ks, lane, blo[jj][ks], bhi[jj][ks]);
       }
   }
   pp_issue<KIND, AK, BKC, ES>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pp_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (AK && BKC)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else
+    lds_wait();  // asm reads in flight: the wait must also fence their consumers
+  if constexpr (RD_A && !AK && ES == 2) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) af[ii][ks] = cat44(alo[ii][ks], ahi[ii][ks]);
+  }
+  if constexpr (RD_B && !BKC && ES == 2) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = cat44(blo[jj][ks], bhi[jj][ks]);
+  }
   __builtin_amdgcn_s_setprio(1);
   if constexpr (ES == 1) {
 #pragma unroll

@@ -393,6 +393,13 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_fwd(2, 197, 3),
         lambda: check_attn_fwd(1, 17, 2),
         lambda: check_attn_fwd(1, 577, 2),
+        # whole-head forward (dh 64, N <= 256): one pair per workgroup, several pairs per
+        # workgroup (B*H > CUs), N = 256 (16 waves), N = 1
+        lambda: check_attn_fwd(16, 197, 12),
+        lambda: check_attn_fwd(40, 197, 12),
+        lambda: check_attn_fwd(3, 256, 5),
+        lambda: check_attn_fwd(300, 33, 2),
+        lambda: check_attn_fwd(4, 1, 3),
         lambda: check_attn_bwd(2, 197, 3),
         lambda: check_attn_bwd(1, 17, 2),
         lambda: check_attn_bwd(1, 64, 1),
