@@ -22,7 +22,7 @@ struct AdamGroup {
 extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
-hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, int, int, hipStream_t);
+hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
 hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
@@ -150,14 +150,46 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor w, torch
   return {y, mean, rstd};
 }
 
+// Dropout parameters shared by every kernel that recomputes a mask: keep iff the element's 16-bit
+// hash >= thr16 = round(p * 65536); kept values scale by 65536 / (65536 - thr16).
+struct DropArgs {
+  const uint64_t* seed = nullptr;
+  uint32_t thr = 0;
+  float scale = 1.f;
+};
+DropArgs drop_args(const c10::optional<torch::Tensor>& seed, double drop_p, const char* what) {
+  DropArgs d;
+  if (drop_p > 0.0) {
+    TORCH_CHECK(seed.has_value() && seed->defined(), what, ": dropout needs a seed");
+    d.seed = reinterpret_cast<const uint64_t*>(seed->data_ptr());
+    d.thr = (uint32_t)llround(drop_p * 65536.0);
+    if (d.thr > 65535) d.thr = 65535;
+    d.scale = (float)(65536.0 / (65536.0 - d.thr));
+  }
+  return d;
+}
+
+// dz (optional, needs drop_p > 0): dropout backward of the layer that produced x's residual stream,
+// dz = mask(seed + seed_offset) * scale * dx; dsum then receives the column sums of dz instead of dx.
 void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t x_stride, torch::Tensor mean, torch::Tensor rstd,
                    torch::Tensor w, c10::optional<torch::Tensor> dres, int64_t dres_stride, torch::Tensor dx, int64_t dx_stride,
                    c10::optional<torch::Tensor> dw, c10::optional<torch::Tensor> db, int64_t rows,
-                   c10::optional<torch::Tensor> dsum) {
+                   c10::optional<torch::Tensor> dsum, c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> seed,
+                   int64_t seed_offset, double drop_p) {
   const int64_t D = w.numel();
+  uint16_t* dzp = nullptr;
+  int64_t ldz = 0;
+  DropArgs d;
+  if (dz.has_value() && dz->defined()) {
+    TORCH_CHECK(drop_p > 0.0, "layernorm_bwd: dz is the dropout backward, it needs drop_p > 0");
+    dzp = const_cast<uint16_t*>(bf(*dz, "dz"));
+    ldz = ld_of(*dz, "dz");
+    d = drop_args(seed, drop_p, "layernorm_bwd");
+  }
   check(pvr_layernorm_bwd(bf(dy, "dy"), dy_stride, bf(x, "x"), x_stride, f32(mean, "mean"), f32(rstd, "rstd"), f32(w, "w"),
                           opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
-                          opt_ptr<float>(db), opt_ptr<float>(dsum), (int)rows, (int)D, stream()),
+                          opt_ptr<float>(db), opt_ptr<float>(dsum), dzp, ldz, d.seed, (uint64_t)seed_offset, d.thr, d.scale,
+                          (int)rows, (int)D, stream()),
         "layernorm_bwd");
 }
 
@@ -184,21 +216,12 @@ void transpose_batched(torch::Tensor src, torch::Tensor dst, torch::Tensor meta,
 
 void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tensor> db, c10::optional<torch::Tensor> dz,
             c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p) {
-  uint32_t thr = 0;
-  float scale = 1.f;
-  const uint64_t* sp = nullptr;
-  if (drop_p > 0.0) {
-    TORCH_CHECK(seed.has_value() && seed->defined(), "colsum: dropout needs a seed");
-    sp = reinterpret_cast<const uint64_t*>(seed->data_ptr());
-    thr = (uint32_t)llround(drop_p * 65536.0);
-    if (thr > 65535) thr = 65535;
-    scale = (float)(65536.0 / (65536.0 - thr));
-  }
+  const DropArgs d = drop_args(seed, drop_p, "colsum");
   int64_t ldz = 0;
   uint16_t* dzp = nullptr;
   if (dz.has_value() && dz->defined()) { dzp = const_cast<uint16_t*>(bf(*dz, "dz")); ldz = ld_of(*dz, "dz"); }
-  check(pvr_colsum(bf(dy, "dy"), ld_of(dy, "dy"), (int)rows, (int)N, opt_ptr<float>(db), dzp, ldz, sp, (uint64_t)seed_offset, thr,
-                   scale, stream()),
+  check(pvr_colsum(bf(dy, "dy"), ld_of(dy, "dy"), (int)rows, (int)N, opt_ptr<float>(db), dzp, ldz, d.seed, (uint64_t)seed_offset,
+                   d.thr, d.scale, stream()),
         "colsum");
 }
 
@@ -415,7 +438,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("dy_stride"), py::arg("x"), py::arg("x_stride"),
         py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),
-        py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none());
+        py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none(),
+        py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("transpose_batched", &transpose_batched);

@@ -1,7 +1,10 @@
 // LayerNorm forward/backward for the pre-LN ViT blocks (reference models/vit.py:83, :115, :216;
 // SURVEY.md K5). One wave per token row, bf16 I/O with 16-B vector accesses, fp32 statistics.
 // The backward fuses the residual-branch gradient add (dx = dres + LN'(dy)) and reduces
-// d(gamma)/d(beta) per block in LDS before one f32 atomic per column per block.
+// d(gamma)/d(beta) per block in LDS before one f32 atomic per column per block. It can also emit
+// the dropout backward of the layer that PRODUCED x's residual stream (dz = mask * scale * dx, the
+// previous encoder block's fc2 dropout, mask recomputed from the same counter hash) together with
+// that layer's bias gradient (column sums of dz), so no separate pass re-reads dx for them.
 #include "common.h"
 
 namespace pvr {
@@ -96,7 +99,9 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       const uint16_t* __restrict__ dres, int64_t dres_stride,
                                                       uint16_t* __restrict__ dx, int64_t dx_stride,
                                                       float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dsum,
-                                                      int rows, int D) {
+                                                      uint16_t* __restrict__ dz, int64_t dz_stride,
+                                                      const uint64_t* __restrict__ seed_ptr, uint64_t seed_off, uint32_t thr,
+                                                      float dscale, int rows, int D) {
   __shared__ float red[4][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];  // one partial at a time
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = D >> 3;
@@ -131,6 +136,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
     wreg[i][0] = w0.x; wreg[i][1] = w0.y; wreg[i][2] = w0.z; wreg[i][3] = w0.w;
     wreg[i][4] = w1.x; wreg[i][5] = w1.y; wreg[i][6] = w1.z; wreg[i][7] = w1.w;
   }
+  const uint64_t seed = dz ? *seed_ptr + seed_off : 0ull;
   int row = blockIdx.x * 4 + wave;
   load_row(row, cx, cdy, cr);
   float cmu = row < rows ? mean[row] : 0.f, crs = row < rows ? rstd[row] : 0.f;
@@ -175,12 +181,24 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += bf2f(j & 1 ? ur[j >> 1] >> 16 : ur[j >> 1] & 0xFFFF);
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) gs[i][j] += o[j];  // column sums of dx (a fused bias gradient)
         uint4 q;
         q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
         q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
         *(uint4*)(dx + (int64_t)row * dx_stride + c * 8) = q;
+        if (dz) {  // uniform: dropout backward of the producing layer
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            bool k0, k1;
+            rng_keep2(seed, (uint64_t)row * D + c * 8 + j, thr, k0, k1);
+            o[j] = k0 ? o[j] * dscale : 0.f;
+            o[j + 1] = k1 ? o[j + 1] * dscale : 0.f;
+          }
+          q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
+          q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
+          *(uint4*)(dz + (int64_t)row * dz_stride + c * 8) = q;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gs[i][j] += o[j];  // column sums of dx (or dz): a fused bias gradient
       }
     }
 #pragma unroll
@@ -237,18 +255,19 @@ extern "C" hipError_t pvr_layernorm_fwd(const uint16_t* x, int64_t x_stride, con
 extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, const uint16_t* x, int64_t x_stride,
                                         const float* mean, const float* rstd, const float* w, const uint16_t* dres,
                                         int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
-                                        float* dsum, int rows, int D, hipStream_t s) {
+                                        float* dsum, uint16_t* dz, int64_t dz_stride, const uint64_t* seed_ptr,
+                                        uint64_t seed_off, uint32_t thr, float dscale, int rows, int D, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
-  if (D % 8 != 0 || D > 1280) return hipErrorInvalidValue;
+  if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
   int nblk = (rows + 3) / 4;
   if (nblk > 2048) nblk = 2048;  // 8 blocks (32 waves) per CU; each wave then pipelines ~6 rows
   const dim3 grid(nblk), block(256);
   const int maxch = (D / 8 + 63) / 64;
   switch (maxch) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, rows, D); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, rows, D); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, rows, D); break;
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D); break;
   }
   return hipGetLastError();
 }

@@ -232,7 +232,7 @@ class ViT(nn.Module):
         return seed
 
     def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops.fused_vit import EncoderBlockFn, HeadFn, PatchEmbedFn, site_drop
+        from ..ops.fused_vit import EncoderBlockFn, block_links, HeadFn, PatchEmbedFn, site_drop
         from ..runtime.param_store import get_store
 
         c = self.config
@@ -262,15 +262,16 @@ class ViT(nn.Module):
         f8 = self._fp8_state(dev, B * N)
         if f8 is not None:
             f8.begin_step(training)
-        for i, blk in enumerate(self.transformer_encoder):
+        blocks = list(self.transformer_encoder)
+        drops2 = [site_drop(seed, 2 + 2 * i, blk.mlp_block.mlp[4].p, training) for i, blk in enumerate(blocks)]
+        links = block_links(blocks, drops2)
+        for i, blk in enumerate(blocks):
             ln1 = blk.msa_block.layer_norm
             ln2 = blk.mlp_block.layer_norm
             p1 = blk.mlp_block.mlp[2].p
-            p2 = blk.mlp_block.mlp[4].p
             tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads, ln1.eps, ln2.eps,
-                                          store, site_drop(seed, 1 + 2 * i, p1, training),
-                                          site_drop(seed, 2 + 2 * i, p2, training),
-                                          None if f8 is None else (f8, i), *blk.fused_params())
+                                          store, site_drop(seed, 1 + 2 * i, p1, training), drops2[i],
+                                          None if f8 is None else (f8, i), links[i], *blk.fused_params())
         head = self.classifier[0]
         return HeadFn.apply(tokens, B, N, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias,
                             head.weight, head.bias)

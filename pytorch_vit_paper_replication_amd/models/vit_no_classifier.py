@@ -30,7 +30,7 @@ class ViT(_FullViT):
         return self.forward_features(x)
 
     def _forward_fused_features(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops.fused_vit import EncoderBlockFn, PatchEmbedFn, TokenLayerNormFn, site_drop
+        from ..ops.fused_vit import EncoderBlockFn, block_links, PatchEmbedFn, TokenLayerNormFn, site_drop
         from ..runtime.param_store import get_store
 
         c = self.config
@@ -54,11 +54,13 @@ class ViT(_FullViT):
         f8 = self._fp8_state(dev, B * N)
         if f8 is not None:
             f8.begin_step(training)
-        for i, blk in enumerate(self.transformer_encoder):
+        blocks = list(self.transformer_encoder)
+        drops2 = [site_drop(seed, 2 + 2 * i, blk.mlp_block.mlp[4].p, training) for i, blk in enumerate(blocks)]
+        links = block_links(blocks, drops2)
+        for i, blk in enumerate(blocks):
             tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads,
                                           blk.msa_block.layer_norm.eps, blk.mlp_block.layer_norm.eps, store,
-                                          site_drop(seed, 1 + 2 * i, blk.mlp_block.mlp[2].p, training),
-                                          site_drop(seed, 2 + 2 * i, blk.mlp_block.mlp[4].p, training),
-                                          None if f8 is None else (f8, i), *blk.fused_params())
+                                          site_drop(seed, 1 + 2 * i, blk.mlp_block.mlp[2].p, training), drops2[i],
+                                          None if f8 is None else (f8, i), links[i], *blk.fused_params())
         y = TokenLayerNormFn.apply(tokens, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias)
         return y.float().view(B, N, -1)

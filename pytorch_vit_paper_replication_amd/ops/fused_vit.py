@@ -87,11 +87,35 @@ class PatchEmbedFn(torch.autograd.Function):
         return (None,) * 10
 
 
+class BlockLink:
+    """Backward hand-off between consecutive encoder blocks. Block i's final LayerNorm backward
+    produces dx for block i-1 and, in the same pass, block i-1's fc2 dropout backward (dz2) and fc2
+    bias gradient; block i-1's backward then starts from dz2 instead of re-reading dx with a
+    column-sum kernel."""
+
+    __slots__ = ("drop2", "b2", "dz2", "done")
+
+    def __init__(self, drop2, b2):
+        self.drop2, self.b2, self.dz2, self.done = drop2, b2, None, False
+
+
+# PVR_BLOCK_LINK=0: every block computes its own fc2 dropout backward / bias gradient (A/B switch)
+BLOCK_LINK = os.environ.get("PVR_BLOCK_LINK", "1") == "1"
+
+
+def block_links(blocks, drops2):
+    """(own link, previous block's link) per block, for EncoderBlockFn's ``links`` argument."""
+    if not BLOCK_LINK:
+        return [None] * len(blocks)
+    own = [BlockLink(d, blk.mlp_block.mlp[3].bias) for blk, d in zip(blocks, drops2)]
+    return [(own[i], own[i - 1] if i else None) for i in range(len(own))]
+
+
 class EncoderBlockFn(torch.autograd.Function):
     """One pre-LN transformer encoder block, forward and hand-written backward."""
 
     @staticmethod
-    def forward(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, f8, *params):
+    def forward(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, f8, links, *params):
         ext = _ext.ext()
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
         T, D = x.shape
@@ -126,6 +150,7 @@ class EncoderBlockFn(torch.autograd.Function):
             x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
         ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
         ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
+        ctx.links = links if links is not None else (None, None)
         return x2
 
     @staticmethod
@@ -137,8 +162,13 @@ class EncoderBlockFn(torch.autograd.Function):
         g = store.grad_dest
         dx2 = dx2.contiguous()
         T, D = dx2.shape
+        own, prev = ctx.links
         # ---- MLP branch: x2 = x1 + drop2(h . W2^T + b2),  h = drop1(gelu(u)),  u = xn2 . W1^T + b1
-        if drop2 is not None:
+        if own is not None and own.done:
+            # the next block's LayerNorm backward already produced dz2 and d(b2)
+            dz2 = own.dz2 if own.dz2 is not None else dx2
+            own.dz2 = None
+        elif drop2 is not None:
             dz2 = torch.empty_like(dx2)
             gemm.bias_grad(dx2, g(b2), drop=drop2, dz=dz2)
         else:
@@ -182,9 +212,17 @@ class EncoderBlockFn(torch.autograd.Function):
         store.on_side(attn_wgrads, dx1, o, dqkv, xn1)
         dxn1 = gemm.linear_dgrad(dqkv, store.bf16(wqkv), wt=store.bf16_t(wqkv))
         dx = torch.empty_like(dx2)
-        ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
+        if prev is not None:
+            # the previous block's fc2 dropout backward and bias gradient ride along with dx
+            seed, soff, p = gemm._drop_args(prev.drop2)
+            dzp = torch.empty_like(dx2) if seed is not None else None
+            ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T,
+                              dsum=g(prev.b2), dz=dzp, seed=seed, seed_offset=soff, drop_p=p)
+            prev.dz2, prev.done = dzp, True
+        else:
+            ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])
-        return (dx,) + (None,) * (9 + len(params))
+        return (dx,) + (None,) * (10 + len(params))
 
 
 class HeadFn(torch.autograd.Function):

@@ -363,6 +363,42 @@ def check_vit_fused_vs_reference(B=4, train=False, **over):
     return (f"vit fused vs fp32 ref (fwd {e_fwd:.2e}, worst grad {worst})", max(e_fwd, e_g / 3), 5e-2)
 
 
+def check_vit_block_link(B=3):
+    """Dropout on: the fc2 dropout backward + bias gradient fused into the next block's LayerNorm
+    backward (BlockLink) vs each block's own column-sum pass, same dropout masks."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops import fused_vit
+
+    torch.manual_seed(0)
+    m = ViT(image_size=64, patch_size=16, num_transformer_layer=3, num_heads=2, embedding_dim=128, mlp_size=256,
+            num_classes=10, mlp_dropout=0.1, embedding_dropout=0.1).to(DEV).train()
+    x = torch.rand(B, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B,), device=DEV)
+    m._dropout_seed(x.device)  # create the model's device RNG, then replay the same seed in both runs
+    rng0 = m._pvr_rng.clone()
+    grads, logits = [], []
+    old = fused_vit.BLOCK_LINK
+    try:
+        for link in (True, False):
+            fused_vit.BLOCK_LINK = link
+            m._pvr_rng.copy_(rng0)
+            for p in m.parameters():
+                p.grad = None
+            lg = m(x)
+            F.cross_entropy(lg, y).backward()
+            logits.append(lg.detach().clone())
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    finally:
+        fused_vit.BLOCK_LINK = old
+    e_fwd = rel_err(logits[0], logits[1])
+    e_g, worst = 0.0, ""
+    for n in grads[0]:
+        e = rel_err(grads[0][n], grads[1][n])
+        if e > e_g:
+            e_g, worst = e, n
+    return (f"vit dropout: linked LN-bwd dz2/db2 vs colsum (worst {worst})", max(e_fwd, e_g), 2e-2)
+
+
 def all_checks() -> List[Callable]:
     c = []
     for tile in (0, 6, 12, 13):
@@ -424,6 +460,7 @@ def all_checks() -> List[Callable]:
         lambda: check_adam(),
         lambda: check_vit_fused_vs_reference(4, False),
         lambda: check_vit_fused_vs_reference(3, True),
+        lambda: check_vit_block_link(),
         # ViT-H/14-like geometry: patch 14, head dim 80, D = 5 x 64
         lambda: check_vit_fused_vs_reference(2, True, image_size=56, patch_size=14, num_heads=4, embedding_dim=320,
                                              mlp_size=640),
