@@ -92,14 +92,18 @@ PVR_DEV v8s load_frag(const uint16_t* p, int d0) {
 }
 
 PVR_DEV v8s pack_p(const v4f& a, const v4f& b) {
-  v8s r;
-  const uint32_t w0 = pack2bf(a[0], a[1]), w1 = pack2bf(a[2], a[3]);
-  const uint32_t w2 = pack2bf(b[0], b[1]), w3 = pack2bf(b[2], b[3]);
-  r[0] = (short)(w0 & 0xFFFF); r[1] = (short)(w0 >> 16);
-  r[2] = (short)(w1 & 0xFFFF); r[3] = (short)(w1 >> 16);
-  r[4] = (short)(w2 & 0xFFFF); r[5] = (short)(w2 >> 16);
-  r[6] = (short)(w3 & 0xFFFF); r[7] = (short)(w3 >> 16);
-  return r;
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u w = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(v8s, w);
+}
+
+// c + sum_j a[j] * b[j] over 8 bf16 pairs (v_dot2c_f32_bf16, fp32 accumulation)
+PVR_DEV float dot8_bf16(const v8s& a, const v8s& b, float c) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const v8bf x = __builtin_bit_cast(v8bf, a), y = __builtin_bit_cast(v8bf, b);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_fdot2_f32_bf16(bf2{x[2 * j], x[2 * j + 1]}, bf2{y[2 * j], y[2 * j + 1]}, c, false);
+  return c;
 }
 
 PVR_DEV uint32_t clamp_bytes(int64_t b) { return b < 0 ? 0u : (b > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)b); }
@@ -505,9 +509,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         const v8s qa = frag_rows(qimg, QB, 16 * a, ks, lane);
         const v8s da = frag_rows(doimg, QB, 16 * a, ks, lane);
         if (DH % 32 == 0 || 32 * ks + 8 * g < DH) {  // staged dims past dh belong to the next head
-          const v8s oa = frag_rows(oimg, QB, 16 * a, ks, lane);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) dsum[a] = fmaf(bf2f((uint16_t)da[j]), bf2f((uint16_t)oa[j]), dsum[a]);
+          dsum[a] = dot8_bf16(da, frag_rows(oimg, QB, 16 * a, ks, lane), dsum[a]);
         }
 #pragma unroll
         for (int f = 0; f < 2; ++f) {

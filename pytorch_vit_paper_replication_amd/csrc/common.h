@@ -94,26 +94,26 @@ PVR_DEV v8s ds_read_b128(const void* lds_ptr) {
   return *(const __attribute__((address_space(3))) v8s*)lds_ptr;
 }
 
-PVR_DEV v8s cat44(v4s a, v4s b) {
-  v8s r;
-  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
-  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
-  return r;
-}
+PVR_DEV v8s cat44(v4s a, v4s b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
 
-// Counter-based dropout RNG: murmur3-style finaliser over (seed, element index).
-// Shared by every kernel that recomputes a mask in backward, so forward and backward agree bit
-// for bit without storing the mask.
+// Counter-based dropout RNG over (seed, element index). Shared by every kernel that recomputes a
+// mask in backward, so forward and backward agree bit for bit without storing the mask.
+// The seed is folded into one 32-bit key (wave-uniform, hoisted out of element loops); the element
+// index then goes through Wellons' "lowbias32" finaliser: two 32-bit multiplies per hash (a
+// quarter-rate instruction on CDNA, as costly as a v_exp) instead of four. Indices below 2^32 (every
+// tensor of these models) make the high word a no-op.
+PVR_DEV uint32_t rng_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+PVR_DEV uint32_t rng_key(uint64_t seed) { return rng_mix32((uint32_t)seed ^ rng_mix32((uint32_t)(seed >> 32) + 0x9E3779B9u)); }
 PVR_DEV uint32_t rng_hash(uint64_t seed, uint64_t idx) {
-  uint32_t h = (uint32_t)idx * 0x9E3779B1u ^ (uint32_t)seed;
-  h ^= (uint32_t)(idx >> 32) * 0x7FEB352Du;
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= (uint32_t)(seed >> 32);
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return h;
+  const uint32_t hi = (uint32_t)(idx >> 32);
+  return rng_mix32((uint32_t)idx ^ rng_key(seed) ^ ((hi << 16) | (hi >> 16)));
 }
 // Element idx is kept iff its 16-bit half of hash(seed, idx >> 1) is >= thr16 = round(p * 65536):
 // one hash serves two neighbouring elements.

@@ -84,22 +84,41 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
 }
 
 // img [B][C][H][W] fp32 -> patches [B*np][Kp] bf16, k = (c*P + ph)*P + pw, zero padded to Kp.
+// One thread per 8 consecutive k of a patch row: with P % 8 == 0 they are 8 consecutive pixels of
+// one image row (two float4 loads, one 16-B store); the zero padding past C*P*P and other patch
+// sizes (P = 14) take the per-element path.
 __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ img, uint16_t* __restrict__ out,
                                                       int B, int C, int H, int W, int P, int Kp) {
   const int gw = W / P, np = (H / P) * gw;
-  const int64_t total = (int64_t)B * np * Kp;
+  const int kc = C * P * P, k8 = Kp / 8;
+  const bool vec = (P % 8 == 0) && (W % 4 == 0);
+  const int64_t total = (int64_t)B * np * k8;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int k = (int)(i % Kp);
-    const int64_t rowi = i / Kp;
+    const int k0 = (int)(i % k8) * 8;
+    const int64_t rowi = i / k8;
     const int pidx = (int)(rowi % np);
     const int b = (int)(rowi / np);
-    float v = 0.f;
-    if (k < C * P * P) {
-      const int c = k / (P * P), rem = k % (P * P), ph = rem / P, pw = rem % P;
-      const int y = (pidx / gw) * P + ph, x = (pidx % gw) * P + pw;
-      v = img[(((int64_t)b * C + c) * H + y) * W + x];
+    const int y0 = (pidx / gw) * P, x0 = (pidx % gw) * P;
+    float v[8];
+    if (vec && k0 + 8 <= kc) {
+      const int c = k0 / (P * P), rem = k0 % (P * P), ph = rem / P, pw = rem % P;
+      const float* src = img + (((int64_t)b * C + c) * H + y0 + ph) * W + x0 + pw;
+      const float4 a = *(const float4*)src, bq = *(const float4*)(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = bq.x; v[5] = bq.y; v[6] = bq.z; v[7] = bq.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + j;
+        v[j] = 0.f;
+        if (k < kc) {
+          const int c = k / (P * P), rem = k % (P * P), ph = rem / P, pw = rem % P;
+          v[j] = img[(((int64_t)b * C + c) * H + y0 + ph) * W + x0 + pw];
+        }
+      }
     }
-    out[i] = f2bf(v);
+    uint4 o;
+    o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]); o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+    *(uint4*)(out + rowi * Kp + k0) = o;
   }
 }
 
@@ -121,52 +140,122 @@ __global__ void __launch_bounds__(256) cls_rows_kernel(const float* __restrict__
 // Backward of  E = dropout(concat(cls, conv) + pos):  dE [B][np+1][D] bf16 ->
 //   dpre = dE * mask;  dpos[n][d] += sum_b dpre;  dcls[d] += sum_b dpre[b][0][d];
 //   dconv[b*np + n-1][d] = dpre (bf16, n >= 1);  dbias[d] += sum_{b, n>=1} dpre.
-// One thread per (n, d) column, looping over the batch: deterministic, no atomics on dpos/dcls.
+// Block = (PB_TOK tokens) x (PB_BAT images), thread = 8 columns (16-B loads/stores, 4 rows in
+// flight); per-block sums go out with one f32 atomic per column and quantity.
+constexpr int PB_TOK = 8, PB_BAT = 16;
 __global__ void __launch_bounds__(256) patch_bwd_kernel(const uint16_t* __restrict__ dE, int B, int ntok, int D,
                                                          float* __restrict__ dpos, float* __restrict__ dcls,
                                                          uint16_t* __restrict__ dconv, float* __restrict__ dbias,
                                                          const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale) {
   const uint64_t seed = thr ? (*seed_ptr + seed_off) : 0ull;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= ntok * D) return;
-  const int n = i / D, d = i % D;
-  float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const int64_t row = (int64_t)b * ntok + n;
-    float v = bf2f(dE[row * D + d]);
-    if (thr) v = rng_keep(seed, (uint64_t)row * D + d, thr) ? v * scale : 0.f;
-    s += v;
-    if (n > 0 && dconv) dconv[((int64_t)b * (ntok - 1) + n - 1) * D + d] = f2bf(v);
+  const int c = threadIdx.x;  // 8-column chunk
+  if (c * 8 >= D) return;
+  const int n0 = blockIdx.x * PB_TOK, b0 = blockIdx.y * PB_BAT;
+  const int b1 = min(B, b0 + PB_BAT);
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int n = n0; n < min(ntok, n0 + PB_TOK); ++n) {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int bb = b0; bb < b1; bb += 4) {
+      uint4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = *(const uint4*)(dE + ((int64_t)min(bb + u, b1 - 1) * ntok + n) * D + c * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int b = bb + u;
+        if (b >= b1) break;
+        const int64_t row = (int64_t)b * ntok + n;
+        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[2 * j] = bf2f(w[j] & 0xFFFF);
+          v[2 * j + 1] = bf2f(w[j] >> 16);
+        }
+        if (thr) {
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            bool k0, k1;
+            rng_keep2(seed, (uint64_t)row * D + c * 8 + j, thr, k0, k1);
+            v[j] = k0 ? v[j] * scale : 0.f;
+            v[j + 1] = k1 ? v[j + 1] * scale : 0.f;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[j];
+        if (n > 0 && dconv) {
+          uint4 o;
+          o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]); o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+          *(uint4*)(dconv + ((int64_t)b * (ntok - 1) + n - 1) * D + c * 8) = o;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (dpos) atomicAdd(dpos + (int64_t)n * D + c * 8 + j, s[j]);
+      if (n == 0) {
+        if (dcls) atomicAdd(dcls + c * 8 + j, s[j]);
+      } else {
+        bsum[j] += s[j];
+      }
+    }
   }
-  if (dpos) dpos[i] += s;
-  if (n == 0) {
-    if (dcls) dcls[d] += s;
-  } else if (dbias) {
-    atomicAdd(dbias + d, s);
+  if (dbias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(dbias + c * 8 + j, bsum[j]);
   }
 }
 
 // Batched bf16 transpose: matrix t (rows R_t, cols C_t) at src + soff[t] -> dst + doff[t] as [C_t][R_t].
-// 64x64 tiles through LDS (padded rows: conflict-free column reads); tile_start[t] = prefix tile count.
+// 64x64 tiles through LDS held as bf16 pairs (u32, 33-word rows: conflict-free column reads);
+// 16-B loads and stores, 8 lanes per 128-B row. tile_start[t] = prefix tile count (binary search).
 __global__ void __launch_bounds__(256) transpose_batched_kernel(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst,
                                                                  const int64_t* __restrict__ meta, int nmat) {
-  __shared__ uint16_t tile[64][66];
-  const int b = blockIdx.x;
-  int t = 0;
-  while (t + 1 < nmat && meta[(t + 1) * 5 + 4] <= b) ++t;
+  __shared__ uint32_t tile[64][33];
+  const int blk = blockIdx.x;
+  int lo = 0, hi = nmat - 1;  // last t with tile_start[t] <= blk
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (meta[mid * 5 + 4] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const int t = lo;
   const int64_t soff = meta[t * 5 + 0], doff = meta[t * 5 + 1];
   const int R = (int)meta[t * 5 + 2], C = (int)meta[t * 5 + 3];
-  const int local = b - (int)meta[t * 5 + 4];
+  const int local = blk - (int)meta[t * 5 + 4];
   const int tc = (C + 63) / 64;
   const int r0 = (local / tc) * 64, c0 = (local % tc) * 64;
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+  const bool full = r0 + 64 <= R && c0 + 64 <= C && (C % 8) == 0 && (R % 8) == 0 && (soff % 8) == 0 && (doff % 8) == 0;
+  const int tid = threadIdx.x;
+  if (full) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = tid / 8 + 32 * it, ch = tid % 8;
+      const uint4 q = *(const uint4*)(src + soff + (int64_t)(r0 + row) * C + c0 + ch * 8);
+      tile[row][ch * 4 + 0] = q.x; tile[row][ch * 4 + 1] = q.y;
+      tile[row][ch * 4 + 2] = q.z; tile[row][ch * 4 + 3] = q.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + 256 * it;
+      const int cc = idx / 8, rch = idx % 8;  // output row (input column) cc, input rows rch*8 .. +7
+      uint32_t h[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = (tile[rch * 8 + j][cc >> 1] >> ((cc & 1) * 16)) & 0xFFFFu;
+      uint4 o;
+      o.x = h[0] | (h[1] << 16); o.y = h[2] | (h[3] << 16); o.z = h[4] | (h[5] << 16); o.w = h[6] | (h[7] << 16);
+      *(uint4*)(dst + doff + (int64_t)(c0 + cc) * R + r0 + rch * 8) = o;
+    }
+    return;
+  }
+  uint16_t* t16 = (uint16_t*)&tile[0][0];  // edge tiles: element-wise through [64][66] bf16
+  for (int i = tid; i < 64 * 64; i += 256) {
     const int rr = i / 64, cc = i % 64;
-    if (r0 + rr < R && c0 + cc < C) tile[rr][cc] = src[soff + (int64_t)(r0 + rr) * C + c0 + cc];
+    if (r0 + rr < R && c0 + cc < C) t16[rr * 66 + cc] = src[soff + (int64_t)(r0 + rr) * C + c0 + cc];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+  for (int i = tid; i < 64 * 64; i += 256) {
     const int cc = i / 64, rr = i % 64;
-    if (r0 + rr < R && c0 + cc < C) dst[doff + (int64_t)(c0 + cc) * R + r0 + rr] = tile[rr][cc];
+    if (r0 + rr < R && c0 + cc < C) dst[doff + (int64_t)(c0 + cc) * R + r0 + rr] = t16[rr * 66 + cc];
   }
 }
 
@@ -242,10 +331,11 @@ extern "C" hipError_t pvr_colsum(const uint16_t* dy, int64_t ld, int rows, int N
 
 extern "C" hipError_t pvr_im2col(const float* img, uint16_t* out, int B, int C, int H, int W, int P, int Kp, hipStream_t s) {
   using namespace pvr;
-  const int64_t total = (int64_t)B * (H / P) * (W / P) * Kp;
+  if (Kp % 8) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * (H / P) * (W / P) * (Kp / 8);
   if (total <= 0) return hipSuccess;
   int64_t blocks = (total + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)blocks), dim3(256), 0, s, img, out, B, C, H, W, P, Kp);
   return hipGetLastError();
 }
@@ -264,9 +354,11 @@ extern "C" hipError_t pvr_patch_bwd(const uint16_t* dE, int B, int ntok, int D, 
                                     float* dbias, const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
                                     hipStream_t s) {
   using namespace pvr;
-  const int n = ntok * D;
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(patch_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dE, B, ntok, D, dpos, dcls, dconv, dbias,
+  if (ntok * D <= 0 || B <= 0) return hipSuccess;
+  if (D % 8 || D / 8 > 256) return hipErrorInvalidValue;
+  const dim3 grid((ntok + PB_TOK - 1) / PB_TOK, (B + PB_BAT - 1) / PB_BAT);
+  const int threads = (D / 8 + 63) / 64 * 64;
+  hipLaunchKernelGGL(patch_bwd_kernel, grid, dim3(threads), 0, s, dE, B, ntok, D, dpos, dcls, dconv, dbias,
                      seed_ptr, seed_off, thr, scale);
   return hipGetLastError();
 }

@@ -1017,21 +1017,31 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
     // vmcnt(0) after each one, serialising them and draining every in-flight LDS-DMA.
     constexpr int RPT = RP / 8;  // rows per thread per pass
     constexpr bool HAS_IN = EPI == EPI_DGELU || (EPI == EPI_BF16 && RES);
+    // Row k of this thread is mrow0 + 8k: every per-row address and the dropout element index are
+    // a base plus k times a wave-uniform step, so no 64-bit multiply (quarter rate) runs per row.
+    const int mrow0 = m0 + half * RP + (tid >> 6);
+    const int nn = ncol ? n : 0;
+    const bool rows_in = m0 + half * RP + RP <= p.M;  // uniform: no row of this pass past M
     uint2 pin[HAS_IN ? RPT : 1];
     if constexpr (HAS_IN) {
       const uint16_t* src = EPI == EPI_DGELU ? p.aux : p.resid;
       const int64_t lsrc = EPI == EPI_DGELU ? p.ld_aux : p.ld_resid;
-      const int nn = ncol ? n : 0;
+      const uint16_t* s0 = src + (int64_t)mrow0 * lsrc + nn;
+      if (rows_in) {
 #pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const int mc = min(m0 + half * RP + (tid >> 6) + 8 * k, p.M - 1);
-        pin[k] = *(const uint2*)(src + (int64_t)mc * lsrc + nn);
+        for (int k = 0; k < RPT; ++k) pin[k] = *(const uint2*)(s0 + (int64_t)k * (8 * lsrc));
+      } else {
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) pin[k] = *(const uint2*)(src + (int64_t)min(mrow0 + 8 * k, p.M - 1) * lsrc + nn);
       }
     }
+    const uint64_t idx0 = (uint64_t)mrow0 * p.N + n, idx_step = 8ull * p.N;
+    uint16_t* c0 = (uint16_t*)p.C + (int64_t)mrow0 * p.ldc + n;
+    uint16_t* x0 = EPI == EPI_GELU ? p.aux + (int64_t)mrow0 * p.ld_aux + n : nullptr;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int r = (tid >> 6) + 8 * k;
-      const int m = m0 + half * RP + r;
+      const int m = mrow0 + 8 * k;
       const v4f a = *(const v4f*)(smem + r * 1024 + ((cq ^ (r & 63)) << 4));
       const bool ok = m < p.M && ncol;
       float v[4] = {a[0] * deq, a[1] * deq, a[2] * deq, a[3] * deq};
@@ -1039,7 +1049,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         v[0] += bias.x; v[1] += bias.y; v[2] += bias.z; v[3] += bias.w;
         bool keep[4] = {true, true, true, true};
         if (p.drop_thr) {
-          const uint64_t idx = (uint64_t)m * p.N + n;
+          const uint64_t idx = idx0 + (uint64_t)k * idx_step;
           rng_keep2(seed, idx, p.drop_thr, keep[0], keep[1]);
           rng_keep2(seed, idx + 2, p.drop_thr, keep[2], keep[3]);
         }
@@ -1064,7 +1074,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
             gp[q] = gd * sc;
           }
           uint2 ax; ax.x = pack2bf(gp[0], gp[1]); ax.y = pack2bf(gp[2], gp[3]);
-          if (ok) *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = ax;
+          if (ok) *(uint2*)(x0 + (int64_t)k * (8 * p.ld_aux)) = ax;
         }
       } else if constexpr (EPI == EPI_DGELU) {
         const uint2 gg = pin[k];
@@ -1078,7 +1088,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         if (ok) *(float4*)((float*)p.C + (int64_t)blockIdx.z * p.split_stride + (int64_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
-        if (ok) *(uint2*)((uint16_t*)p.C + (int64_t)m * p.ldc + n) = o;
+        if (ok) *(uint2*)(c0 + (int64_t)k * (8 * p.ldc)) = o;
       }
     }
   }
@@ -1420,7 +1430,9 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       }
       [[fallthrough]];
     case 12:
-      if constexpr (AK == BKC) {  // k-contiguous pair (fwd / dgrad with W^T) or mn pair (wgrad)
+      // k-contiguous pair (fwd / dgrad with W^T), mn pair (wgrad) or k-contiguous A with an
+      // mn-contiguous B (dgrad straight from W, transposed B reads)
+      if constexpr (AK || !BKC) {
         if ((!AK || (p.K % PP_BK == 0 && p.k_split_len % PP_BK == 0)) && (AK || p.k_split_len % PP_BK == 0))
           return launch_pp<AK, BKC, SWAP, EPI>(p, s);
       }

@@ -24,7 +24,7 @@ _PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "0") == "1"  # A/B: 12 faste
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
 
-def _tile(M: int, N: int, K: int, kind: str) -> int:
+def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
     """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
     k-contiguous forward/dgrad at ViT sizes -> persistent 256x256 8-wave ping-pong (13; K % 64 == 0,
     else the 4-stage BK=32 ring 6); token-reduced wgrad (both operands mn-contiguous, split-K
@@ -35,9 +35,11 @@ def _tile(M: int, N: int, K: int, kind: str) -> int:
     if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
         if K % 64:
             return 6
-        # persistent ping-pong (13) where a CU gets several tiles; the kernel itself falls back to
-        # the one-tile-per-workgroup form (12) for epilogues it does not stage
-        return 13 if K >= 128 and _PERSISTENT else 12
+        # persistent ping-pong (13): the next tile's K-tiles stream in under this tile's epilogue.
+        # It pays for the VALU-heavy GELU epilogue (fc1 fwd 0.377 vs 0.457 ms at ViT-B/16 b256,
+        # profiles/kbench_epilogues.log); epilogues that load per-row inputs (residual, dGELU
+        # factor) drain the in-flight DMAs there and stay on the one-tile-per-workgroup form (12).
+        return 13 if K >= 128 and (gelu or _PERSISTENT) else 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
         return 12
     return 0
@@ -64,13 +66,13 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
     seed, soff, p = _drop_args(drop)
     epi = EPI_GELU if gelu_aux is not None else EPI_BF16
     _ext.ext().gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
-                    row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, _tile(T, N, K, "fwd"))
+                    row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, _tile(T, N, K, "fwd", epi == EPI_GELU))
     return out
 
 
 def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch.Tensor] = None,
                  drop: Drop = None, out: Optional[torch.Tensor] = None, wt: Optional[torch.Tensor] = None,
-                 colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 colsum: Optional[torch.Tensor] = None, tile: Optional[int] = None) -> torch.Tensor:
     """dx = dy . w ; optionally fused with the GELU + dropout backward of the producing layer:
     dx = (dy . w) * dgelu_aux (the factor saved by the GELU forward epilogue). With ``wt`` (= w^T, [K, N] bf16) the weight operand is
     k-contiguous and the fast forward-layout kernel runs; otherwise w is read with transposed LDS reads."""
@@ -87,7 +89,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
                         seed, soff, p, 0, _tile(T, K, N, "dgrad_t"), colsum=colsum)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-                        seed, soff, p, 0, _tile(T, K, N, "dgrad"), colsum=colsum)
+                        seed, soff, p, 0, _tile(T, K, N, "dgrad") if tile is None else tile, colsum=colsum)
     return out
 
 

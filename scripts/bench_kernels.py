@@ -65,6 +65,8 @@ def main():
                 G._FORCE_TILE = str(t)
                 tt = timeit(lambda: G.linear_dgrad(dy, w, wt=wt))
                 print(f"dgrad {name:4s} tile{t}   ours(wT) {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
+                tt = timeit(lambda: G.linear_dgrad(dy, w, tile=t))
+                print(f"dgrad {name:4s} tile{t}   ours(W)  {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
             out = torch.zeros(n, k, device=dev)
             t_lib = timeit(lambda: torch.matmul(dy.t(), x))
             print(f"wgrad {name:4s} N{n} K{k} T{T}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
@@ -73,6 +75,49 @@ def main():
                 tt = timeit(lambda: G.linear_wgrad(dy, x, out))
                 print(f"wgrad {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
             G._FORCE_TILE = None
+    if "epi" in a.only:
+        # the fused epilogues exactly as the training step runs them (ViT-B/16 b256 shapes)
+        seed = torch.tensor([1234], dtype=torch.int64, device=dev)
+        x = torch.randn(T, D, device=dev, dtype=torch.bfloat16)
+        h = torch.randn(T, M, device=dev, dtype=torch.bfloat16)
+        r = torch.randn(T, D, device=dev, dtype=torch.bfloat16)
+        w1 = (torch.randn(M, D, device=dev) * 0.02).to(torch.bfloat16)
+        w2 = (torch.randn(D, M, device=dev) * 0.02).to(torch.bfloat16)
+        wo = (torch.randn(D, D, device=dev) * 0.02).to(torch.bfloat16)
+        b1, b2 = torch.randn(M, device=dev), torch.randn(D, device=dev)
+        u = torch.empty(T, M, device=dev, dtype=torch.bfloat16)
+        cs = torch.zeros(M, device=dev)
+        w2t = w2.t().contiguous()
+        cases = [
+            ("fc1 fwd  bias+GELU+dropout+aux", 2.0 * T * M * D, lambda: G.linear_fwd(x, w1, b1, gelu_aux=u, drop=(seed, 3 << 32, 0.1))),
+            ("fc1 fwd  bias only           ", 2.0 * T * M * D, lambda: G.linear_fwd(x, w1, b1)),
+            ("fc2 fwd  bias+dropout+resid  ", 2.0 * T * M * D, lambda: G.linear_fwd(h, w2, b2, resid=r, drop=(seed, 4 << 32, 0.1))),
+            ("out fwd  bias+resid          ", 2.0 * T * D * D, lambda: G.linear_fwd(x, wo, b2, resid=r)),
+            ("fc2 dgrad dGELU+colsum (wT)  ", 2.0 * T * M * D, lambda: G.linear_dgrad(r, w2, dgelu_aux=u, wt=w2t, colsum=cs)),
+        ]
+        for name, fl, fn in cases:
+            tt = timeit(fn)
+            print(f"epi   {name} {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF", flush=True)
+        wqkv = (torch.randn(M3, D, device=dev) * 0.02).to(torch.bfloat16)
+        bqkv = torch.randn(M3, device=dev)
+        w1t = w1.t().contiguous()
+        for t in (12, 13):  # one tile per workgroup vs persistent, per epilogue kind
+            G._FORCE_TILE = str(t)
+            for name, fl, fn in [
+                ("qkv fwd  bias            ", 2.0 * T * M3 * D, lambda: G.linear_fwd(x, wqkv, bqkv)),
+                ("out fwd  bias+resid      ", 2.0 * T * D * D, lambda: G.linear_fwd(x, wo, b2, resid=r)),
+                ("fc2 fwd  bias+drop+resid ", 2.0 * T * M * D, lambda: G.linear_fwd(h, w2, b2, resid=r, drop=(seed, 4 << 32, 0.1))),
+                ("fc1 dgrad plain (wT)     ", 2.0 * T * M * D, lambda: G.linear_dgrad(u, w1, wt=w1t)),
+                ("fc2 dgrad dGELU+colsum   ", 2.0 * T * M * D, lambda: G.linear_dgrad(r, w2, dgelu_aux=u, wt=w2t, colsum=cs)),
+            ]:
+                tt = timeit(fn)
+                print(f"epi   {name} tile{t} {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF", flush=True)
+            G._FORCE_TILE = None
+        for t in (9, 10, 11, 6, 13):  # other tile structures for the GELU epilogue (2 workgroups/CU, persistent)
+            G._FORCE_TILE = str(t)
+            tt = timeit(lambda: G.linear_fwd(x, w1, b1, gelu_aux=u, drop=(seed, 3 << 32, 0.1)))
+            G._FORCE_TILE = None
+            print(f"epi   fc1 fwd GELU tile{t:<3d}            {tt:7.3f} ms {2.0 * T * M * D / tt / 1e9:7.1f} TF", flush=True)
     if "fp8" in a.only:
         from pytorch_vit_paper_replication_amd.ops import fp8 as F8
 

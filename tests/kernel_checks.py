@@ -72,6 +72,27 @@ def check_gemm_gelu(M, N, K, tile=0):
     return (f"gemm_gelu M{M} N{N} K{K} t{tile}", max(e1, e2), 2e-2)
 
 
+def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13)):
+    """GELU + dropout + aux epilogue: identical masks and values across GEMM structures."""
+    x, w, b = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05)), rnd(N)
+    seed = torch.tensor([777], dtype=torch.int64, device=DEV)
+    outs = []
+    old = G._FORCE_TILE
+    try:
+        for t in tiles:
+            G._FORCE_TILE = str(t)
+            u = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            h = G.linear_fwd(x, w, b, gelu_aux=u, drop=(seed, 5 << 32, 0.1))
+            outs.append((h, u))
+    finally:
+        G._FORCE_TILE = old
+    (h0, u0), (h1, u1) = outs
+    same_mask = torch.equal(h0 == 0, h1 == 0) and torch.equal(u0 == 0, u1 == 0)
+    rate = (u0 == 0).float().mean().item()
+    err = max(rel_err(h1, h0), rel_err(u1, u0)) + (0 if same_mask else 1) + abs(rate - 0.1)
+    return (f"gemm_gelu+dropout M{M} N{N} K{K} tiles{tiles} (drop rate {rate:.4f})", err, 1e-2)
+
+
 def check_gemm_dgrad(M, N, K, tile=0, transposed=False):
     dy, w = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05))
     old = G._FORCE_TILE
@@ -83,11 +104,13 @@ def check_gemm_dgrad(M, N, K, tile=0, transposed=False):
     return (f"gemm_dgrad M{M} N{N} K{K} t{tile} wt{int(transposed)}", rel_err(dx, dy.float() @ w.float()), 2e-2)
 
 
-def check_gemm_dgelu(M, N, K, transposed=False):
+def check_gemm_dgelu(M, N, K, transposed=False, tile=None):
     dy, w, g = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05)), bf(rnd(M, K))
-    dx = G.linear_dgrad(dy, w, dgelu_aux=g, wt=w.t().contiguous() if transposed else None)
+    cs = torch.zeros(K, device=DEV)
+    dx = G.linear_dgrad(dy, w, dgelu_aux=g, wt=w.t().contiguous() if transposed else None, tile=tile, colsum=cs)
     ref = (dy.float() @ w.float()) * g.float()
-    return (f"gemm_dgelu M{M} N{N} K{K}", rel_err(dx, ref), 2e-2)
+    e_cs = rel_err(cs, ref.sum(0)) / max(1.0, M / 64)  # column sums of dU (fused bias gradient)
+    return (f"gemm_dgelu M{M} N{N} K{K} wt{int(transposed)} t{tile} (colsum {e_cs:.1e})", max(rel_err(dx, ref), e_cs), 2e-2)
 
 
 def check_gemm_wgrad(T, N, K, tile=0):
@@ -123,6 +146,56 @@ def check_gemm_dropout(M=512, N=256, K=128, p=0.1, tile=None):
     same = torch.equal(dz.float() != 0, keep)
     err = abs(rate - p) + (0 if scale_ok else 1) + (0 if same else 1)
     return (f"dropout rate/scale/fwd-bwd mask tile{tile}", err, 1e-2)
+
+
+# ----------------------------------------------------------------------------- patch embedding / layout
+def check_im2col(B, C, H, P):
+    ext = _ext.ext()
+    img = rnd(B, C, H, H)
+    kc = C * P * P
+    kp = (kc + 63) // 64 * 64
+    g = H // P
+    out = torch.empty(B * g * g, kp, dtype=torch.bfloat16, device=DEV)
+    ext.im2col(img, out, P, kp)
+    ref = img.reshape(B, C, g, P, g, P).permute(0, 2, 4, 1, 3, 5).reshape(B * g * g, kc)
+    ref = F.pad(ref, (0, kp - kc))
+    return (f"im2col B{B} C{C} H{H} P{P}", rel_err(out, bf(ref)), 1e-6)
+
+
+def check_patch_bwd(B, ntok, D, p=0.1):
+    """Patch-embedding backward (dropout mask from the shared counter hash) vs torch sums."""
+    ext = _ext.ext()
+    dE = bf(rnd(B * ntok, D))
+    seed = torch.tensor([4242], dtype=torch.int64, device=DEV)
+    off = 3 << 32
+    mask = torch.empty_like(dE)  # mask * scale from the column-sum kernel on ones (same hash)
+    ext.colsum(bf(torch.ones(B * ntok, D, device=DEV)), B * ntok, D, None, mask, seed, off, p)
+    dpre = dE.float() * mask.float()
+    gpos, gcls, gb = torch.zeros(ntok, D, device=DEV), torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    dconv = torch.empty(B * (ntok - 1), D, dtype=torch.bfloat16, device=DEV)
+    ext.patch_bwd(dE, B, ntok, D, gpos.view(-1), gcls, dconv, gb, seed, off, p)
+    d3 = dpre.view(B, ntok, D)
+    e = max(rel_err(gpos, d3.sum(0)), rel_err(gcls, d3[:, 0].sum(0)), rel_err(gb, d3[:, 1:].sum((0, 1))) / 10,
+            rel_err(dconv, d3[:, 1:].reshape(-1, D)))
+    return (f"patch_bwd B{B} ntok{ntok} D{D} p{p}", e, 2e-2)
+
+
+def check_transpose_batched():
+    ext = _ext.ext()
+    shapes = [(128, 192), (100, 70), (768, 2304)]
+    src = torch.cat([bf(rnd(r * c)) for r, c in shapes])
+    dst = torch.zeros_like(src)
+    meta, so, tiles = [], 0, 0
+    for r, c in shapes:
+        meta.append([so, so, r, c, tiles])
+        so += r * c
+        tiles += ((r + 63) // 64) * ((c + 63) // 64)
+    ext.transpose_batched(src, dst, torch.tensor(meta, dtype=torch.int64, device=DEV), tiles)
+    e, so = 0.0, 0
+    for r, c in shapes:
+        e = max(e, rel_err(dst[so:so + r * c].view(c, r), src[so:so + r * c].view(r, c).t()))
+        so += r * c
+    return ("transpose_batched (full and edge tiles)", e, 1e-6)
 
 
 # ----------------------------------------------------------------------------- LayerNorm
@@ -413,16 +486,24 @@ def all_checks() -> List[Callable]:
         lambda: check_gemm_fwd(5000, 2304, 768, 13, True, True),   # persistent: several tiles per CU
         lambda: check_gemm_fwd(9000, 768, 128, 13, True, False),   # nk = 2: next-tile DMAs start at phase 3
         lambda: check_gemm_gelu(6000, 3072, 768, 13),
+        lambda: check_gemm_gelu_dropout(5000, 3072, 768),
         lambda: check_gemm_dropout(3000, 768, 128, 0.1, 13),
         lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
         lambda: check_gemm_fwd(100, 64, 128, 0, True, True),
         lambda: check_gemm_dgelu(394, 768, 3072),
         lambda: check_gemm_dgelu(4096, 768, 3072, True),
+        lambda: check_gemm_dgelu(4096, 768, 3072, False, 12),   # ping-pong, B = W mn-contiguous
+        lambda: check_gemm_dgelu(1000, 3072, 768, False, 12),
         lambda: check_gemm_wgrad(17, 64, 128),
         lambda: check_gemm_wgrad(3000, 768, 2304, 12),
         lambda: check_gemm_wgrad(1000, 304, 200, 12),
         lambda: check_gemm_dropout(),
         lambda: check_gemm_dropout(1000, 768, 128, 0.1, 12),
+        lambda: check_im2col(3, 3, 224, 16),
+        lambda: check_im2col(2, 3, 56, 14),
+        lambda: check_patch_bwd(37, 197, 768),
+        lambda: check_patch_bwd(5, 17, 1280, 0.0),
+        lambda: check_transpose_batched(),
         lambda: check_layernorm(394, 768),
         lambda: check_layernorm(100, 1024),
         lambda: check_layernorm(33, 1280),
