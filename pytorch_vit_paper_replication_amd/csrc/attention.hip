@@ -679,6 +679,310 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   }
 }
 
+// ------------------------------------------------------- backward, whole head (N <= 256, dh 64)
+// Two persistent kernels over (batch, head) pairs, each with the pair's operands double-buffered in
+// LDS exactly like the whole-head forward, and no barrier inside a pair:
+//   dq:  one wave per 16 queries (query on the MFMA lane). P^T is recomputed key chunk by key chunk
+//        straight from the saved log-sum-exp (no running max), dS^T = P^T (dP^T - delta) feeds
+//        dQ^T += K^T dS^T from registers. It also forms delta = rowsum(dO * O) and writes it for:
+//   dkv: one wave per 32 keys (key on the lane) with its K/V fragments in registers, sweeping every
+//        query block of the pair: dV^T += dO^T P, dK^T += Q^T dS.
+// S and dP are computed twice (once per kernel) in exchange for no dS exchange through LDS, no
+// per-query-block barriers and no idle key waves.
+template <int NF>
+__global__ void __launch_bounds__(NF * 64) attn_bwd_dq_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                                    const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                                    const uint16_t* __restrict__ o, int64_t ld_o,
+                                                                    const float* __restrict__ lse, float* __restrict__ delta,
+                                                                    uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H,
+                                                                    int D, int npairs, float scale) {
+  constexpr int DH = 64;
+  constexpr int NP = 32 * ((NF + 1) / 2);
+  constexpr int BUF = 2 * NP * 128;  // K | V images
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  PVR_ASSERT((N + 15) / 16 == NF && blockDim.x == NF * 64 && (int)gridDim.x <= npairs);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
+  const int p0 = L * per + min(L, rem);
+  const int p1 = p0 + per + (L < rem ? 1 : 0);
+  const int q = wave * 16 + li;
+  const int qrow = min(q, N - 1);
+  const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
+  const float c = scale * LOG2E;
+
+  auto issue = [&](int pr, char* buf) {
+    const uint16_t* base = qkv + (int64_t)(pr / H) * N * ld + (pr % H) * DH;
+    dma_rows<1>(make_rsrc(base + D, extent), buf, NP, ld, 0, wave, NF, lane);
+    dma_rows<1>(make_rsrc(base + 2 * D, extent), buf + NP * 128, NP, ld, 0, wave, NF, lane);
+  };
+  // per-lane query operands: Q, dO, O fragments (lane holds X[q][32ks + 8g + j]) and lse
+  struct QOps {
+    v8s qf[2], df[2], of[2];
+    float l2;
+  };
+  auto load_q = [&](int pr, QOps& t) {
+    const int64_t row = (int64_t)(pr / H) * N + qrow;
+    const int col = (pr % H) * DH + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      t.qf[ks] = *(const v8s*)(qkv + row * ld + col + 32 * ks);
+      t.df[ks] = *(const v8s*)(dout + row * ld_do + col + 32 * ks);
+      t.of[ks] = *(const v8s*)(o + row * ld_o + col + 32 * ks);
+    }
+    t.l2 = lse[(int64_t)pr * N + qrow];  // scaled at use: any math here would wait for the load now
+  };
+  auto settle = [&](QOps& t) {  // the compiler's wait for these loads sits here, not at first use
+    asm volatile("" : "+v"(t.qf[0]), "+v"(t.qf[1]), "+v"(t.df[0]), "+v"(t.df[1]));
+    asm volatile("" : "+v"(t.of[0]), "+v"(t.of[1]), "+v"(t.l2));
+  };
+  constexpr int STORES = 5;  // dQ row (4 x 8 B) + delta, per wave per pair (see the counted wait)
+  const uint32_t dq_extent = clamp_bytes(((int64_t)(N - 1) * ld_dq + DH) * 2);
+
+  if (p0 >= p1) return;
+  QOps cur, nxt;
+  issue(p0, smem);
+  load_q(p0, cur);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  settle(cur);
+  for (int pr = p0; pr < p1; ++pr) {
+    const int it = pr - p0;
+    const char* kimg = smem + (it & 1) * BUF;
+    const char* vimg = kimg + NP * 128;
+    if (pr + 1 < p1) {
+      issue(pr + 1, smem + ((it + 1) & 1) * BUF);
+      load_q(pr + 1, nxt);
+    }
+    const float l2 = cur.l2 * LOG2E;
+    // delta[q] = dO[q] . O[q]: 16 dims per lane, then across the 4 lane groups
+    float dl = dot8_bf16(cur.df[1], cur.of[1], dot8_bf16(cur.df[0], cur.of[0], 0.f));
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    v4f dq[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dq[e] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < (NF + 1) / 2; ++kk) {
+      // S^T, dP^T for keys 32kk .. 32kk+31 (two 16-key fragments)
+      v4f sv[2], dp[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int f = 2 * kk + h2;
+        sv[h2] = dp[h2] = v4f{0.f, 0.f, 0.f, 0.f};
+        if (f < NF) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            sv[h2] = mfma16(frag_rows(kimg, NP, 16 * f, ks, lane), cur.qf[ks], sv[h2]);
+            dp[h2] = mfma16(frag_rows(vimg, NP, 16 * f, ks, lane), cur.df[ks], dp[h2]);
+          }
+        }
+      }
+      // K^T fragments for dQ^T (asm transpose reads: the next pair's DMA stays in flight)
+      v4s klo[4], khi[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) frag_tr_async(kimg, NP, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, klo[e], khi[e]);
+      // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse2); keys past N contribute nothing
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 32 * kk + 16 * h2 + 4 * g + r;
+          const float pv = key < N ? __builtin_amdgcn_exp2f(fmaf(sv[h2][r], c, -l2)) : 0.f;
+          sv[h2][r] = pv * (dp[h2][r] - dl);
+        }
+      const v8s dsf = pack_p(sv[0], sv[1]);
+      lds_wait();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dq[e] = mfma16(cat44(klo[e], khi[e]), dsf, dq[e]);
+    }
+    // dQ row q (lane: dims 16e + 4g .. +3) and delta[q]: buffer stores, dropped past N / off group 0
+    {
+      typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+      const bool ok = q < N;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(dqkv + (int64_t)(pr / H) * N * ld_dq + (pr % H) * DH, dq_extent);
+      const uint32_t vo = ok ? (uint32_t)((q * ld_dq + 4 * g) * 2) : 0x80000000u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const v2u w = {pack2bf(dq[e][0] * scale, dq[e][1] * scale), pack2bf(dq[e][2] * scale, dq[e][3] * scale)};
+        __builtin_amdgcn_raw_buffer_store_b64(w, rs, vo + 32 * e, 0, 0);
+      }
+      const __amdgpu_buffer_rsrc_t dsr = make_rsrc(delta + (int64_t)pr * N, (uint32_t)N * 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dl), dsr, ok && g == 0 ? (uint32_t)q * 4 : 0x80000000u, 0, 0);
+    }
+    static_assert(STORES == 5, "the vmcnt below counts the dQ / delta store instructions");
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    __syncthreads();
+    cur = nxt;
+    settle(cur);
+  }
+}
+
+template <int NK>
+__global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                                     const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
+                                                                     uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H,
+                                                                     int D, int npairs, float scale) {
+  constexpr int DH = 64;
+  constexpr int NP = 32 * NK;                 // query rows staged (and keys covered)
+  constexpr int BUF = 2 * NP * 128 + 2048;    // Q | dO images | lse | delta (1 KiB DMA slots)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  PVR_ASSERT((N + 31) / 32 == NK && blockDim.x == NK * 64 && (int)gridDim.x <= npairs);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
+  const int p0 = L * per + min(L, rem);
+  const int p1 = p0 + per + (L < rem ? 1 : 0);
+  const int kw0 = wave * 32;
+  const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
+  const uint32_t do_extent = clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2);
+  const float c = scale * LOG2E;
+
+  auto issue = [&](int pr, char* buf) {
+    const int b = pr / H, h = pr % H;
+    dma_rows<1>(make_rsrc(qkv + (int64_t)b * N * ld + h * DH, extent), buf, NP, ld, 0, wave, NK, lane);
+    dma_rows<1>(make_rsrc(dout + (int64_t)b * N * ld_do + h * DH, do_extent), buf + NP * 128, NP, ld_do, 0, wave, NK, lane);
+    if (wave == NK - 1) {  // lse and delta rows of the pair (queries past N read as 0)
+      dma16(make_rsrc(lse + (int64_t)pr * N, (uint32_t)N * 4), to_lds(buf + 2 * NP * 128), (uint32_t)lane * 16);
+      dma16(make_rsrc(delta + (int64_t)pr * N, (uint32_t)N * 4), to_lds(buf + 2 * NP * 128 + 1024), (uint32_t)lane * 16);
+    }
+  };
+  // this wave's 32 keys: K and V fragments as B operands (lane holds X[kw0 + 16f + li][32ks + 8g + j])
+  struct KOps {
+    v8s kf[2][2], vf[2][2];
+  };
+  auto load_k = [&](int pr, KOps& t) {
+    const uint16_t* base = qkv + (int64_t)(pr / H) * N * ld + (pr % H) * DH + 8 * g;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int key = min(kw0 + 16 * f + li, N - 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        t.kf[f][ks] = *(const v8s*)(base + (int64_t)key * ld + D + 32 * ks);
+        t.vf[f][ks] = *(const v8s*)(base + (int64_t)key * ld + 2 * D + 32 * ks);
+      }
+    }
+  };
+  auto settle = [&](KOps& t) {
+    asm volatile("" : "+v"(t.kf[0][0]), "+v"(t.kf[0][1]), "+v"(t.kf[1][0]), "+v"(t.kf[1][1]));
+    asm volatile("" : "+v"(t.vf[0][0]), "+v"(t.vf[0][1]), "+v"(t.vf[1][0]), "+v"(t.vf[1][1]));
+  };
+  constexpr int STORES = 16;  // dK and dV rows: 2 key fragments x 4 dim fragments x 2
+  const uint32_t dkv_extent = clamp_bytes(((int64_t)(N - 1) * ld_dq + 2 * D + DH) * 2);
+
+  if (p0 >= p1) return;
+  KOps cur, nxt;
+  issue(p0, smem);
+  load_k(p0, cur);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  settle(cur);
+  for (int pr = p0; pr < p1; ++pr) {
+    const int it = pr - p0;
+    const char* qimg = smem + (it & 1) * BUF;
+    const char* doimg = qimg + NP * 128;
+    const float* s_l2 = (const float*)(qimg + 2 * NP * 128);
+    const float* s_dl = s_l2 + 256;
+    if (pr + 1 < p1) {
+      issue(pr + 1, smem + ((it + 1) & 1) * BUF);
+      load_k(pr + 1, nxt);
+    }
+    v4f dk[4][2], dv[4][2];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
+    if (kw0 < N) {  // uniform: waves past N only stage
+#pragma unroll 1
+      for (int qb = 0; qb < NK; ++qb) {
+        // S[q][key], dP[q][key]: lane holds [q = 32qb + 16a + 4g + r][key = kw0 + 16f + li]
+        v4f sv[2][2], dp[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int f = 0; f < 2; ++f) sv[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const v8s qa = frag_rows(qimg, NP, 32 * qb + 16 * a, ks, lane);
+            const v8s da = frag_rows(doimg, NP, 32 * qb + 16 * a, ks, lane);
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              sv[a][f] = mfma16(qa, cur.kf[f][ks], sv[a][f]);
+              dp[a][f] = mfma16(da, cur.vf[f][ks], dp[a][f]);
+            }
+          }
+        // dO^T / Q^T fragments for the dV / dK products (asm transpose reads)
+        v4s dlo[4], dhi[4], qlo[4], qhi[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          frag_tr_async(doimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, dlo[e], dhi[e]);
+          frag_tr_async(qimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, qlo[e], qhi[e]);
+        }
+        // P = exp2(S c - lse2[q]), dS = P (dP - delta[q]); queries past N have zero Q / dO rows
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const v4f l4 = *(const v4f*)(s_l2 + 32 * qb + 16 * a + 4 * g);
+          const v4f d4 = *(const v4f*)(s_dl + 32 * qb + 16 * a + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              const float pv = __builtin_amdgcn_exp2f(fmaf(sv[a][f][r], c, -l4[r] * LOG2E));
+              sv[a][f][r] = pv;
+              dp[a][f][r] = pv * (dp[a][f][r] - d4[r]);
+            }
+        }
+        v8s pf[2], sf[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          pf[f] = pack_p(sv[0][f], sv[1][f]);
+          sf[f] = pack_p(dp[0][f], dp[1][f]);
+        }
+        lds_wait();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const v8s dot = cat44(dlo[e], dhi[e]), qt = cat44(qlo[e], qhi[e]);
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
+            dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
+          }
+        }
+      }
+    }
+    // dK (x scale), dV rows: lane holds X^T[d = 16e + 4g + r][key = kw0 + 16f + li]; buffer stores
+    // (keys past N dropped), exactly STORES per wave
+    {
+      typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(dqkv + (int64_t)(pr / H) * N * ld_dq + (pr % H) * DH, dkv_extent);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const int key = kw0 + 16 * f + li;
+        const uint32_t vo = key < N ? (uint32_t)((key * ld_dq + 4 * g) * 2) : 0x80000000u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const v2u wk = {pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale), pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale)};
+          const v2u wv = {pack2bf(dv[e][f][0], dv[e][f][1]), pack2bf(dv[e][f][2], dv[e][f][3])};
+          __builtin_amdgcn_raw_buffer_store_b64(wk, rs, vo + (uint32_t)(D + 16 * e) * 2, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(wv, rs, vo + (uint32_t)(2 * D + 16 * e) * 2, 0, 0);
+        }
+      }
+    }
+    static_assert(STORES == 16, "the vmcnt below counts the dK / dV store instructions");
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __syncthreads();
+    cur = nxt;
+    settle(cur);
+  }
+}
+
 __global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
                                                           int64_t rows, int D) {
   const int64_t n = rows * D;
@@ -778,11 +1082,83 @@ extern "C" int pvr_attn_bwd_waves(int N) {
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
 }
 
+// PVR_ATTN_BWD_FUSED=1 forces the single-kernel (dS through LDS) backward everywhere (A/B switch)
+static bool bwd_fused_forced() {
+  static const bool f = [] {
+    const char* e = getenv("PVR_ATTN_BWD_FUSED");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
+template <int NF>
+static hipError_t attn_bwd_dq_head_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                          int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, int npairs,
+                                          int N, int H, int D, float scale, hipStream_t s) {
+  using namespace pvr;
+  constexpr int SMEM = 2 * 2 * 32 * ((NF + 1) / 2) * 128;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_dq_head_kernel<NF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int grid = npairs < device_cus() ? npairs : device_cus();
+  hipLaunchKernelGGL(attn_bwd_dq_head_kernel<NF>, dim3(grid), dim3(NF * 64), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, delta,
+                     dqkv, ld_dq, N, H, D, npairs, scale);
+  return hipGetLastError();
+}
+
+template <int NK>
+static hipError_t attn_bwd_dkv_head_launch(const uint16_t* qkv, int64_t ld, const uint16_t* dout, int64_t ld_do, const float* lse,
+                                           const float* delta, uint16_t* dqkv, int64_t ld_dq, int npairs, int N, int H, int D,
+                                           float scale, hipStream_t s) {
+  using namespace pvr;
+  constexpr int SMEM = 2 * (2 * 32 * NK * 128 + 2048);
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_dkv_head_kernel<NK>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int grid = npairs < device_cus() ? npairs : device_cus();
+  hipLaunchKernelGGL(attn_bwd_dkv_head_kernel<NK>, dim3(grid), dim3(NK * 64), SMEM, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
+                     N, H, D, npairs, scale);
+  return hipGetLastError();
+}
+
+// whole-head backward (dh 64, N <= 256): dQ + delta, then dK / dV
+static hipError_t attn_bwd_head(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout, int64_t ld_do,
+                                const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, int B, int N, int H, int D, float scale,
+                                hipStream_t s) {
+  const int npairs = B * H;
+  hipError_t e = hipErrorInvalidValue;
+  switch ((N + 15) / 16) {
+#define PVR_BWD_DQ(NF) \
+  case NF: e = attn_bwd_dq_head_launch<NF>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s); break;
+    PVR_BWD_DQ(1) PVR_BWD_DQ(2) PVR_BWD_DQ(3) PVR_BWD_DQ(4) PVR_BWD_DQ(5) PVR_BWD_DQ(6) PVR_BWD_DQ(7) PVR_BWD_DQ(8)
+    PVR_BWD_DQ(9) PVR_BWD_DQ(10) PVR_BWD_DQ(11) PVR_BWD_DQ(12) PVR_BWD_DQ(13) PVR_BWD_DQ(14) PVR_BWD_DQ(15) PVR_BWD_DQ(16)
+#undef PVR_BWD_DQ
+    default: break;
+  }
+  if (e != hipSuccess) return e;
+  switch ((N + 31) / 32) {
+#define PVR_BWD_DKV(NK) \
+  case NK: return attn_bwd_dkv_head_launch<NK>(qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s);
+    PVR_BWD_DKV(1) PVR_BWD_DKV(2) PVR_BWD_DKV(3) PVR_BWD_DKV(4) PVR_BWD_DKV(5) PVR_BWD_DKV(6) PVR_BWD_DKV(7) PVR_BWD_DKV(8)
+#undef PVR_BWD_DKV
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                  int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                  int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                   float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
+  if (DH == 64 && N <= 256 && !dbias && delta && !bwd_fused_forced())
+    return attn_bwd_head(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, B, N, H, D, scale, s);
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
@@ -812,15 +1188,17 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
 // dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
 // dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
 // every element is written), whose row sum is the in_proj bias gradient.
+// delta: optional f32 [B*H][N] workspace; with it, dh 64 and N <= 256 take the two-kernel
+// whole-head backward (which does not fuse the bias gradient: dbias forces the single kernel).
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                   int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                    float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
   switch (D / H) {
-    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
     default: return hipErrorInvalidValue;
   }
 }

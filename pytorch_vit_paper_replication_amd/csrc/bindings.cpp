@@ -41,7 +41,7 @@ hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const fl
 int pvr_attn_bwd_key_blocks(int);
 int pvr_attn_bwd_waves(int);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
-hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, float*, int, int, int, int, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, float*, int, int, int, int, float, hipStream_t);
 }
 
 namespace {
@@ -399,6 +399,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
                        double scale, c10::optional<torch::Tensor> dbias) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
+  auto delta = torch::empty_like(lse);  // rowsum(dO * O) workspace of the two-kernel backward
   torch::Tensor dq_acc;
   if (N > 256) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
   // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
@@ -411,7 +412,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
       dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
   check(pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"), ld_of(dout, "dout"),
-                     f32(lse, "lse"), bf_mut(dqkv, "dqkv"), ld_of(dqkv, "dqkv"),
+                     f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"), ld_of(dqkv, "dqkv"),
                      dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr,
                      dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
                      (float)scale, stream()),

@@ -241,18 +241,20 @@ def check_attn_fwd(B, N, H, dh=64):
     return (f"attn_fwd B{B} N{N} H{H} dh{dh}", max(rel_err(o, oref), rel_err(lse, lref) / 5), 2e-2)
 
 
-def check_attn_bwd(B, N, H, dh=64):
+def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
+    """dQ|dK|dV vs autograd of the fp32 reference. Without the fused bias gradient, dh 64 and
+    N <= 256 run the two-kernel whole-head backward; with it, the single-kernel one."""
     ext = _ext.ext()
     D = H * dh
     qkv = bf(rnd(B * N, 3 * D))
     o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / math.sqrt(dh))
     do = bf(rnd(B * N, D))
-    dbias = torch.zeros(3 * D, device=DEV)
+    dbias = torch.zeros(3 * D, device=DEV) if fused_bias else None
     dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
     qr = qkv.float().requires_grad_(True)
     oref, _ = _attn_ref(qr, B, N, H)
     oref.backward(do.float())
-    e_b = rel_err(dbias, qr.grad.sum(0))  # fused in_proj bias gradient
+    e_b = rel_err(dbias, qr.grad.sum(0)) if fused_bias else 0.0  # fused in_proj bias gradient
     return (f"attn_bwd B{B} N{N} H{H} dh{dh} (dbias {e_b:.1e})", max(rel_err(dqkv, qr.grad), e_b), 3e-2)
 
 
@@ -518,9 +520,13 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_fwd(300, 33, 2),
         lambda: check_attn_fwd(4, 1, 3),
         lambda: check_attn_bwd(2, 197, 3),
+        lambda: check_attn_bwd(2, 197, 3, 64, True),
+        lambda: check_attn_bwd(40, 197, 12),   # whole-head backward, several pairs per workgroup
+        lambda: check_attn_bwd(3, 256, 5),
+        lambda: check_attn_bwd(7, 1, 3),
         lambda: check_attn_bwd(1, 17, 2),
-        lambda: check_attn_bwd(1, 64, 1),
-        lambda: check_attn_bwd(1, 257, 2),
+        lambda: check_attn_bwd(1, 64, 1, 64, True),
+        lambda: check_attn_bwd(1, 257, 2, 64, True),
         lambda: check_attn_bwd(1, 577, 2),
         lambda: check_attn_fwd(2, 257, 3, 80),
         lambda: check_attn_fwd(1, 33, 2, 80),
