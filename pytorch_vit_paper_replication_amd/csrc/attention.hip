@@ -1091,6 +1091,18 @@ static bool bwd_fused_forced() {
   return f;
 }
 
+// Backward grids: one persistent workgroup per CU, like the forward. (PVR_ATTN_BWD_PPW=n deals
+// n pairs per workgroup instead; measured in-step at ViT-B/16 b256, beside the side-stream weight
+// GEMMs: 1 per CU 6996 img/s, n = 6 / 3 / 2 / 1: 6986 / 6954 / 6918 / 6851.)
+static int bwd_grid(int npairs) {
+  static const int ppw = [] {
+    const char* e = getenv("PVR_ATTN_BWD_PPW");
+    return e ? atoi(e) : 0;
+  }();
+  if (ppw > 0) return (npairs + ppw - 1) / ppw;
+  return npairs < device_cus() ? npairs : device_cus();
+}
+
 template <int NF>
 static hipError_t attn_bwd_dq_head_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                           int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, int npairs,
@@ -1103,7 +1115,7 @@ static hipError_t attn_bwd_dq_head_launch(const uint16_t* qkv, int64_t ld, const
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int grid = npairs < device_cus() ? npairs : device_cus();
+  const int grid = bwd_grid(npairs);
   hipLaunchKernelGGL(attn_bwd_dq_head_kernel<NF>, dim3(grid), dim3(NF * 64), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, delta,
                      dqkv, ld_dq, N, H, D, npairs, scale);
   return hipGetLastError();
@@ -1121,7 +1133,7 @@ static hipError_t attn_bwd_dkv_head_launch(const uint16_t* qkv, int64_t ld, cons
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int grid = npairs < device_cus() ? npairs : device_cus();
+  const int grid = bwd_grid(npairs);
   hipLaunchKernelGGL(attn_bwd_dkv_head_kernel<NK>, dim3(grid), dim3(NK * 64), SMEM, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
                      N, H, D, npairs, scale);
   return hipGetLastError();

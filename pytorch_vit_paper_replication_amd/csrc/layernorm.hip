@@ -260,8 +260,15 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
+  static const int cap = [] {  // PVR_LN_BWD_BLOCKS: grid cap (A/B of row pipelining vs atomics per column)
+    const char* e = getenv("PVR_LN_BWD_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
   int nblk = (rows + 3) / 4;
-  if (nblk > 2048) nblk = 2048;  // 8 blocks (32 waves) per CU; each wave then pipelines ~6 rows
+  // 512 blocks (2 per CU, ~25 pipelined rows per wave): 22 % faster than 2048 at ViT-B/16 b256, whose
+  // 2048 x 3 x D column atomics contended on the same addresses (profiles/kbench_ln_grid.log)
+  if (nblk > cap) nblk = cap;
   const dim3 grid(nblk), block(256);
   const int maxch = (D / 8 + 63) / 64;
   switch (maxch) {

@@ -168,8 +168,16 @@ def main():
         y, mu, rs = ext.layernorm_fwd(x, w, b, 1e-5, T, D)
         dx = torch.empty_like(x)
         dw, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
-        tt = timeit(lambda: ext.layernorm_bwd(x, D, x, D, mu, rs, w, x, D, dx, D, dw, db, T))
-        print(f"ln_bwd T{T} D{D}: ours {tt:.3f} ms {4 * T * D * 2 / 1e9 / tt * 1e3:.0f} GB/s", flush=True)
+        dy, dres = torch.randn_like(x), torch.randn_like(x)
+        tt = timeit(lambda: ext.layernorm_bwd(dy, D, x, D, mu, rs, w, dres, D, dx, D, dw, db, T))
+        print(f"ln_bwd T{T} D{D}: ours {tt:.3f} ms {4 * T * D * 2 / 1e9 / tt * 1e3:.0f} GB/s (dy, x, dres, dx distinct)", flush=True)
+        dz, ds = torch.empty_like(x), torch.zeros(D, device=dev)
+        seed = torch.tensor([99], dtype=torch.int64, device=dev)
+        tt = timeit(lambda: ext.layernorm_bwd(dy, D, x, D, mu, rs, w, dres, D, dx, D, dw, db, T, dsum=ds, dz=dz, seed=seed,
+                                              seed_offset=2 << 32, drop_p=0.1))
+        print(f"ln_bwd+dz T{T} D{D}: ours {tt:.3f} ms {5 * T * D * 2 / 1e9 / tt * 1e3:.0f} GB/s (linked dropout backward)", flush=True)
+        tt = timeit(lambda: dx.copy_(dy))
+        print(f"copy bf16 T{T} D{D}: {tt:.3f} ms {2 * T * D * 2 / 1e9 / tt * 1e3:.0f} GB/s (torch copy_, reference)", flush=True)
 
 
 if __name__ == "__main__":
