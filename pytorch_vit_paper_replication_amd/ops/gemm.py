@@ -93,13 +93,18 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
     return out
 
 
+# workgroups a 256x256 weight-gradient GEMM is split into (one resident workgroup per CU): the
+# side stream's share of the 256 CUs while the dgrad chain runs beside it (PVR_WGRAD_WGS)
+_WGRAD_WGS = int(os.environ.get("PVR_WGRAD_WGS", "256"))
+
+
 def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
     """Token splits of a weight-gradient GEMM (each split accumulates into dW with f32 atomics).
     256x256 ping-pong tiles (12): one resident workgroup per CU, so fill the 256 CUs once;
     128x128 tiles (0): about 1024 workgroups."""
     if tile == 12:
         tiles = math.ceil(N / 256) * math.ceil(K / 256)
-        return max(1, min(256 // tiles, max(1, T // 256)))
+        return max(1, min(_WGRAD_WGS // tiles, max(1, T // 256)))
     tiles = math.ceil(N / 128) * math.ceil(K / 128)
     target = 1024
     s = max(1, round(target / tiles))

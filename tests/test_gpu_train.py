@@ -129,6 +129,45 @@ def test_ddp_rccl_world1_matches_local(comm):
         dist.destroy_process_group()
 
 
+def test_ddp_callbacks_run_on_the_callers_stream():
+    """bench.py trains on a high-priority, non-default stream: the end-of-backward callbacks that join
+    the side stream and the gradient all-reduces (DDP) must then order that stream, not the default one."""
+    import torch.distributed as dist
+
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        torch.manual_seed(0)
+        m = ViT(**CFG).to(dev)
+        ddp = DistributedDataParallel(m, bucket_cap_mb=0.25, comm="native")
+        x = torch.rand(4, 3, 64, 64, device=dev)
+        y = torch.randint(0, 10, (4,), device=dev)
+        seen = []
+        fin = ddp._finalize
+
+        def spy():
+            seen.append(torch.cuda.current_stream(dev).stream_id)
+            fin()
+
+        ddp._finalize = spy
+        s = torch.cuda.Stream(device=dev, priority=-1)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                cross_entropy(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        assert ddp.transport == "native-rccl"
+        assert seen and all(v == s.stream_id for v in seen), (seen, s.stream_id)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_native_communicator_collectives_world1():
     """The C++ RCCL communicator's collectives, stream ordering and handles (world_size 1)."""
     import torch.distributed as dist
