@@ -29,7 +29,8 @@ hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
 hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
-hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+int pvr_patch_bwd_groups(int);
 hipError_t pvr_xent(const float*, int64_t, const int64_t*, int, int, float*, float*, int*, float, hipStream_t);
 int pvr_norm_partial_blocks();
 hipError_t pvr_grad_norm(const float*, int64_t, float, float*, float*, hipStream_t);
@@ -260,7 +261,9 @@ void patch_bwd(torch::Tensor dE, int64_t B, int64_t ntok, int64_t D, c10::option
     if (thr > 65535) thr = 65535;
     scale = (float)(65536.0 / (65536.0 - thr));
   }
-  check(pvr_patch_bwd(bf(dE, "dE"), (int)B, (int)ntok, (int)D, opt_ptr<float>(dpos), opt_ptr<float>(dcls), opt_ptr<uint16_t>(dconv),
+  TORCH_CHECK(dE.numel() == B * ntok * D, "patch_bwd: dE must hold B * ntok * D elements");
+  auto ws = torch::empty({(int64_t)pvr_patch_bwd_groups((int)B) * ntok * D}, dE.options().dtype(torch::kFloat32));
+  check(pvr_patch_bwd(bf(dE, "dE"), (int)B, (int)ntok, (int)D, ws.data_ptr<float>(), opt_ptr<float>(dpos), opt_ptr<float>(dcls), opt_ptr<uint16_t>(dconv),
                       opt_ptr<float>(dbias), sp, (uint64_t)seed_offset, thr, scale, stream()),
         "patch_bwd");
 }

@@ -140,68 +140,122 @@ __global__ void __launch_bounds__(256) cls_rows_kernel(const float* __restrict__
 // Backward of  E = dropout(concat(cls, conv) + pos):  dE [B][np+1][D] bf16 ->
 //   dpre = dE * mask;  dpos[n][d] += sum_b dpre;  dcls[d] += sum_b dpre[b][0][d];
 //   dconv[b*np + n-1][d] = dpre (bf16, n >= 1);  dbias[d] += sum_{b, n>=1} dpre.
-// Block = (PB_TOK tokens) x (PB_BAT images), thread = 8 columns (16-B loads/stores, 4 rows in
-// flight); per-block sums go out with one f32 atomic per column and quantity.
-constexpr int PB_TOK = 8, PB_BAT = 16;
+// Two passes and (almost) no atomics: device-scope f32 atomics that pile onto a few KB of addresses
+// (dbias: 768 columns) serialise. At ViT-B/16 b256 this is 33 us; the one-pass kernel that added
+// per-block partials with atomics took 250 us, one adding per-thread partials ~450 us
+// (scripts/atomics_probe.py, profiles/atomics_probe.log).
+//  pass 1: thread = one (token, 8-column chunk) pair of the flattened [ntok][D/8] grid (every lane
+//          busy; D/8 = 96 does not fill power-of-two blocks), block.y = a group of PB_BAT images;
+//          8 independent 16-B loads in flight per thread; writes the masked gradient (dconv) and
+//          the group's per-(token, column) sums to ws[group][ntok][D] with plain stores;
+//  pass 2: thread = (8-column chunk, token) sums the groups, owns dpos[n] (and dcls for n = 0), and
+//          the block reduces its tokens' dbias partials in LDS before one atomic per column.
+constexpr int PB_BAT = 32, PB_UNROLL = 8;
 __global__ void __launch_bounds__(256) patch_bwd_kernel(const uint16_t* __restrict__ dE, int B, int ntok, int D,
-                                                         float* __restrict__ dpos, float* __restrict__ dcls,
-                                                         uint16_t* __restrict__ dconv, float* __restrict__ dbias,
+                                                         float* __restrict__ ws, uint16_t* __restrict__ dconv,
                                                          const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale) {
   const uint64_t seed = thr ? (*seed_ptr + seed_off) : 0ull;
-  const int c = threadIdx.x;  // 8-column chunk
-  if (c * 8 >= D) return;
-  const int n0 = blockIdx.x * PB_TOK, b0 = blockIdx.y * PB_BAT;
-  const int b1 = min(B, b0 + PB_BAT);
-  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int n = n0; n < min(ntok, n0 + PB_TOK); ++n) {
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int bb = b0; bb < b1; bb += 4) {
-      uint4 q[4];
+  const int nch = D >> 3;
+  const int flat = blockIdx.x * 256 + threadIdx.x;
+  if (flat >= ntok * nch) return;
+  const int n = flat / nch, c = flat - n * nch;
+  const int b0 = blockIdx.y * PB_BAT, b1 = min(B, b0 + PB_BAT);
+  const int64_t img_stride = (int64_t)ntok * D;  // elements between consecutive images
+  const uint16_t* src = dE + (int64_t)n * D + c * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int bb = b0; bb < b1; bb += PB_UNROLL) {
+    uint4 q[PB_UNROLL];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) q[u] = *(const uint4*)(dE + ((int64_t)min(bb + u, b1 - 1) * ntok + n) * D + c * 8);
+    for (int u = 0; u < PB_UNROLL; ++u) q[u] = *(const uint4*)(src + (int64_t)min(bb + u, b1 - 1) * img_stride);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int b = bb + u;
-        if (b >= b1) break;
-        const int64_t row = (int64_t)b * ntok + n;
-        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-        float v[8];
+    for (int u = 0; u < PB_UNROLL; ++u) {
+      const int b = bb + u;
+      if (b >= b1) break;
+      const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+      float v[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[2 * j] = bf2f(w[j] & 0xFFFF);
-          v[2 * j + 1] = bf2f(w[j] >> 16);
-        }
-        if (thr) {
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = bf2f(w[j] & 0xFFFF);
+        v[2 * j + 1] = bf2f(w[j] >> 16);
+      }
+      if (thr) {
+        const uint64_t e0 = ((uint64_t)b * ntok + n) * D + c * 8;
 #pragma unroll
-          for (int j = 0; j < 8; j += 2) {
-            bool k0, k1;
-            rng_keep2(seed, (uint64_t)row * D + c * 8 + j, thr, k0, k1);
-            v[j] = k0 ? v[j] * scale : 0.f;
-            v[j + 1] = k1 ? v[j + 1] * scale : 0.f;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] += v[j];
-        if (n > 0 && dconv) {
-          uint4 o;
-          o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]); o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
-          *(uint4*)(dconv + ((int64_t)b * (ntok - 1) + n - 1) * D + c * 8) = o;
+        for (int j = 0; j < 8; j += 2) {
+          bool k0, k1;
+          rng_keep2(seed, e0 + j, thr, k0, k1);
+          v[j] = k0 ? v[j] * scale : 0.f;
+          v[j + 1] = k1 ? v[j + 1] * scale : 0.f;
         }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (dpos) atomicAdd(dpos + (int64_t)n * D + c * 8 + j, s[j]);
-      if (n == 0) {
-        if (dcls) atomicAdd(dcls + c * 8 + j, s[j]);
-      } else {
-        bsum[j] += s[j];
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+      if (n > 0 && dconv) {
+        uint4 o;
+        o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]); o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
+        *(uint4*)(dconv + ((int64_t)b * (ntok - 1) + n - 1) * D + c * 8) = o;
       }
     }
   }
-  if (dbias) {
+  float* o = ws + ((int64_t)blockIdx.y * ntok + n) * D + c * 8;
+  *(float4*)o = make_float4(s[0], s[1], s[2], s[3]);
+  *(float4*)(o + 4) = make_float4(s[4], s[5], s[6], s[7]);
+}
+
+constexpr int PR_CH = 32, PR_TOK = 8;  // pass-2 block: 32 column chunks x 8 tokens
+__global__ void __launch_bounds__(256) patch_bwd_reduce_kernel(const float* __restrict__ ws, int G, int ntok, int D,
+                                                                float* __restrict__ dpos, float* __restrict__ dcls,
+                                                                float* __restrict__ dbias) {
+  __shared__ float red[PR_TOK][PR_CH * 8];
+  const int nch = D >> 3;
+  const int cl = threadIdx.x % PR_CH, tl = threadIdx.x / PR_CH;
+  const int c = blockIdx.x * PR_CH + cl;
+  const int n = blockIdx.y * PR_TOK + tl;
+  float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool ok = c < nch && n < ntok;
+  if (ok) {
+    const float* src = ws + (int64_t)n * D + c * 8;
+    const int64_t gs = (int64_t)ntok * D;
+    int g = 0;
+    for (; g + 4 <= G; g += 4) {
+      float4 a[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(dbias + c * 8 + j, bsum[j]);
+      for (int u = 0; u < 4; ++u) {
+        a[2 * u] = *(const float4*)(src + (g + u) * gs);
+        a[2 * u + 1] = *(const float4*)(src + (g + u) * gs + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        t[0] += a[2 * u].x; t[1] += a[2 * u].y; t[2] += a[2 * u].z; t[3] += a[2 * u].w;
+        t[4] += a[2 * u + 1].x; t[5] += a[2 * u + 1].y; t[6] += a[2 * u + 1].z; t[7] += a[2 * u + 1].w;
+      }
+    }
+    for (; g < G; ++g) {
+      const float4 a0 = *(const float4*)(src + g * gs), a1 = *(const float4*)(src + g * gs + 4);
+      t[0] += a0.x; t[1] += a0.y; t[2] += a0.z; t[3] += a0.w;
+      t[4] += a1.x; t[5] += a1.y; t[6] += a1.z; t[7] += a1.w;
+    }
+    if (dpos) {  // this thread owns dpos[n][c*8 .. +8]
+      float* d = dpos + (int64_t)n * D + c * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += t[j];
+    }
+    if (n == 0 && dcls) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dcls[c * 8 + j] += t[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tl][cl * 8 + j] = (ok && n > 0) ? t[j] : 0.f;
+  __syncthreads();
+  if (dbias) {
+    const int col = blockIdx.x * PR_CH * 8 + threadIdx.x;  // 256 columns per block, one per thread
+    if (col < D) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < PR_TOK; ++k) a += red[k][threadIdx.x];
+      atomicAdd(dbias + col, a);
+    }
   }
 }
 
@@ -350,15 +404,20 @@ extern "C" hipError_t pvr_cls_rows(const float* cls, const float* pos, uint16_t*
   return hipGetLastError();
 }
 
-extern "C" hipError_t pvr_patch_bwd(const uint16_t* dE, int B, int ntok, int D, float* dpos, float* dcls, uint16_t* dconv,
-                                    float* dbias, const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
-                                    hipStream_t s) {
+extern "C" hipError_t pvr_patch_bwd(const uint16_t* dE, int B, int ntok, int D, float* ws, float* dpos, float* dcls,
+                                    uint16_t* dconv, float* dbias, const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr,
+                                    float scale, hipStream_t s) {
   using namespace pvr;
   if (ntok * D <= 0 || B <= 0) return hipSuccess;
-  if (D % 8 || D / 8 > 256) return hipErrorInvalidValue;
-  const dim3 grid((ntok + PB_TOK - 1) / PB_TOK, (B + PB_BAT - 1) / PB_BAT);
-  const int threads = (D / 8 + 63) / 64 * 64;
-  hipLaunchKernelGGL(patch_bwd_kernel, grid, dim3(threads), 0, s, dE, B, ntok, D, dpos, dcls, dconv, dbias,
+  if (D % 8) return hipErrorInvalidValue;
+  const int G = (B + PB_BAT - 1) / PB_BAT;  // ws holds G * ntok * D floats (host-checked)
+  hipLaunchKernelGGL(patch_bwd_kernel, dim3((ntok * (D / 8) + 255) / 256, G), dim3(256), 0, s, dE, B, ntok, D, ws, dconv,
                      seed_ptr, seed_off, thr, scale);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(patch_bwd_reduce_kernel, dim3((D / 8 + PR_CH - 1) / PR_CH, (ntok + PR_TOK - 1) / PR_TOK), dim3(256), 0, s,
+                     ws, G, ntok, D, dpos, dcls, dbias);
   return hipGetLastError();
 }
+
+extern "C" int pvr_patch_bwd_groups(int B) { return (B + pvr::PB_BAT - 1) / pvr::PB_BAT; }
