@@ -38,6 +38,7 @@ def parse():
                    help="fp8: encoder forward GEMMs in e4m3 with delayed scaling (ViT-H/14 fp8 config)")
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
     p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
+    p.add_argument("--pg-only", action="store_true", help="initialise a world-1 RCCL process group but do not wrap in DDP (A/B)")
     p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
     p.add_argument("--bucket-mb", type=float, default=28.0)
     p.add_argument("--graph", action="store_true", help="replay the whole training step as one captured hipGraph")
@@ -61,7 +62,7 @@ def main():
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     n = max(args.gpus, world_env)
     rank, world, device = init_distributed()
-    if args.force_ddp and not torch.distributed.is_initialized():
+    if (args.force_ddp or args.pg_only) and not torch.distributed.is_initialized():
         import datetime
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

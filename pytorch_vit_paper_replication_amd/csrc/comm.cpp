@@ -49,7 +49,11 @@ void sym(void* h, const char* name, F& out, std::string& err) {
 const Api& api() {
   static Api a = [] {
     Api r;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD | RTLD_GLOBAL);
+    // The RCCL torch already mapped: the wheel bundles its own (SONAME librccl.so), a system copy
+    // would be a second RCCL runtime in the process (measured 6 % slower steps at world 1 when
+    // /opt/rocm's librccl.so.1 was loaded beside torch's)
+    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD | RTLD_GLOBAL);
     if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
     if (!h) {
@@ -261,6 +265,12 @@ void register_comm(pybind11::module& m) {
   namespace py = pybind11;
   m.def("rccl_available", [] { return api().ok; });
   m.def("rccl_error", [] { return api().err; });
+  m.def("rccl_path", [] {  // file the resolved RCCL entry points live in
+    Dl_info info;
+    const Api& a = api();
+    if (a.get_version && dladdr(reinterpret_cast<void*>(a.get_version), &info) && info.dli_fname) return std::string(info.dli_fname);
+    return std::string();
+  });
   m.def("rccl_version", &Communicator::version);
   m.def("rccl_unique_id", [] { return py::bytes(Communicator::unique_id()); });
   py::class_<Communicator>(m, "Communicator")
