@@ -111,6 +111,38 @@ def block_links(blocks, drops2):
     return [(own[i], own[i - 1] if i else None) for i in range(len(own))]
 
 
+# Two-stream micro-batching of the encoder blocks (opt-in, PVR_MICRO=2): each block's batch is split
+# into two halves whose kernel chains run on two compute streams, so one half's memory-bound kernels
+# (LayerNorm, attention, column sums) and last-wave GEMM tiles can overlap the other half's GEMMs.
+# Every kernel of the block is row-parallel (or per (image, head)), so a half is a contiguous row range
+# of the same [B*N, D] buffers; weight gradients of both halves accumulate on the one side stream.
+# Measured on one MI355X (scripts/gpu_micro.sh): ViT-B/16 b256 6730 img/s split vs 7060 unsplit (two
+# concurrent half-size GEMM chains interfere more than they fill each other's idle CUs), b512 7409 vs
+# ~7400 — so it stays off by default. Numerics: identical logits, gradients within summation order.
+MICRO = int(os.environ.get("PVR_MICRO", "1"))
+MICRO_MIN_IMAGES = int(os.environ.get("PVR_MICRO_MIN", "32"))  # per half
+_HALF_SEED_SHIFT = 48  # half h > 0 draws its dropout masks from seed offset + (h << 48)
+
+
+def _half_drop(drop, h: int):
+    if drop is None or h == 0:
+        return drop
+    return (drop[0], drop[1] + (h << _HALF_SEED_SHIFT), drop[2])
+
+
+def _use_micro(x: torch.Tensor, B: int, f8) -> bool:
+    return MICRO > 1 and f8 is None and x.is_cuda and B >= 2 * MICRO_MIN_IMAGES
+
+
+def _micro_stream(store, main: torch.cuda.Stream) -> torch.cuda.Stream:
+    """Second compute stream, created once per store at the caller's stream priority."""
+    s = getattr(store, "_micro_stream", None)
+    if s is None or s.priority != main.priority or s.device != main.device:
+        s = torch.cuda.Stream(device=main.device, priority=main.priority)
+        store._micro_stream = s
+    return s
+
+
 class EncoderBlockFn(torch.autograd.Function):
     """One pre-LN transformer encoder block, forward and hand-written backward."""
 
@@ -119,6 +151,10 @@ class EncoderBlockFn(torch.autograd.Function):
         ext = _ext.ext()
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
         T, D = x.shape
+        ctx.links = links if links is not None else (None, None)
+        if _use_micro(x, B, f8):
+            return EncoderBlockFn._forward_micro(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, params)
+        ctx.halves = None
         M = w1.shape[0]
         scale = 1.0 / math.sqrt(D // H)
         u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
@@ -150,11 +186,48 @@ class EncoderBlockFn(torch.autograd.Function):
             x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
         ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
         ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
-        ctx.links = links if links is not None else (None, None)
+        return x2
+
+    @staticmethod
+    def _forward_micro(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, params):
+        ext = _ext.ext()
+        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
+        T, D = x.shape
+        M = w1.shape[0]
+        scale = 1.0 / math.sqrt(D // H)
+        main = torch.cuda.current_stream(x.device)
+        side = _micro_stream(store, main)
+        side.wait_stream(main)
+        x2 = torch.empty_like(x)
+        b_half = (B + 1) // 2
+        halves = []
+        for hi, (b0, nb) in enumerate(((0, b_half), (b_half, B - b_half))):
+            r0, r1 = b0 * N, (b0 + nb) * N
+            Th = r1 - r0
+            d1, d2 = _half_drop(drop1, hi), _half_drop(drop2, hi)
+            with torch.cuda.stream(main if hi == 0 else side):
+                xh = x[r0:r1]
+                u = torch.empty(Th, M, dtype=torch.bfloat16, device=x.device)
+                xn1, mean1, rstd1 = ext.layernorm_fwd(xh, ln1w, ln1b, eps1, Th, D)
+                qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
+                o, lse = ext.attn_fwd(qkv, nb, N, H, scale)
+                x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=xh)
+                xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, Th, D)
+                h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=d1)
+                gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=d2, out=x2[r0:r1])
+            halves.append((r0, r1, nb, d2, (xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)))
+        x.record_stream(side)
+        x2.record_stream(side)
+        main.wait_stream(side)
+        ctx.save_for_backward(x)
+        ctx.halves = halves
+        ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
         return x2
 
     @staticmethod
     def backward(ctx, dx2):
+        if ctx.halves is not None:
+            return EncoderBlockFn._backward_micro(ctx, dx2)
         ext = _ext.ext()
         x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = ctx.saved_tensors
         B, N, H, scale, store, drop1, drop2, params = ctx.meta
@@ -222,6 +295,89 @@ class EncoderBlockFn(torch.autograd.Function):
         else:
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])
+        return (dx,) + (None,) * (10 + len(params))
+
+    @staticmethod
+    def _backward_micro(ctx, dx2):
+        ext = _ext.ext()
+        (x,) = ctx.saved_tensors
+        B, N, H, scale, store, drop1, drop2, params = ctx.meta
+        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
+        g = store.grad_dest
+        dx2 = dx2.contiguous()
+        T, D = dx2.shape
+        own, prev = ctx.links
+        main = torch.cuda.current_stream(dx2.device)
+        side = _micro_stream(store, main)
+        # gradient destinations resolved once, before either stream touches them
+        gb2, gb1, gw2, gw1 = g(b2), g(b1), g(w2), g(w1)
+        gln2w, gln2b, gbo, gwo, gbqkv, gwqkv = g(ln2w), g(ln2b), g(bo), g(wo), g(bqkv), g(wqkv)
+        gln1w, gln1b = g(ln1w), g(ln1b)
+        gprev_b2 = g(prev.b2) if prev is not None else None
+        linked = own is not None and own.done
+        if linked:
+            dz2_full = own.dz2 if own.dz2 is not None else dx2
+            own.dz2 = None
+        elif drop2 is not None:
+            dz2_full = torch.empty_like(dx2)
+        else:
+            dz2_full = dx2
+        dx1 = torch.empty_like(dx2)
+        dx = torch.empty_like(dx2)
+        prev_drop = prev.drop2 if prev is not None else None
+        dzp = torch.empty_like(dx2) if prev_drop is not None else None
+        side.wait_stream(main)
+        w2b, w2t, w1b, w1t = store.bf16(w2), store.bf16_t(w2), store.bf16(w1), store.bf16_t(w1)
+        wob, wot, wqb, wqt = store.bf16(wo), store.bf16_t(wo), store.bf16(wqkv), store.bf16_t(wqkv)
+        for hi, (r0, r1, nb, d2, saved) in enumerate(ctx.halves):
+            xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = saved
+            Th = r1 - r0
+            with torch.cuda.stream(main if hi == 0 else side):
+                dx2h, dz2 = dx2[r0:r1], dz2_full[r0:r1]
+                if not linked:
+                    if drop2 is not None:
+                        gemm.bias_grad(dx2h, gb2, drop=d2, dz=dz2)
+                    elif gb2 is not None:
+                        gemm.bias_grad(dx2h, gb2)
+                du = gemm.linear_dgrad(dz2, w2b, dgelu_aux=u, wt=w2t, colsum=gb1)
+
+                def mlp_wgrads(dz2=dz2, h=h, du=du, xn2=xn2):
+                    if gw2 is not None:
+                        gemm.linear_wgrad(dz2, h, gw2)
+                    if gw1 is not None:
+                        gemm.linear_wgrad(du, xn2, gw1)
+
+                store.on_side(mlp_wgrads, dz2, h, du, xn2)
+                dxn2 = gemm.linear_dgrad(du, w1b, wt=w1t)
+                dx1h = dx1[r0:r1]
+                ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2h, D, dx1h, D, gln2w, gln2b, Th, dsum=gbo)
+                do = gemm.linear_dgrad(dx1h, wob, wt=wot)
+                dqkv = ext.attn_bwd(do, qkv, o, lse, nb, N, H, scale)
+                if gbqkv is not None:
+                    gemm.bias_grad(dqkv, gbqkv)
+
+                def attn_wgrads(dx1h=dx1h, o=o, dqkv=dqkv, xn1=xn1):
+                    if gwo is not None:
+                        gemm.linear_wgrad(dx1h, o, gwo)
+                    if gwqkv is not None:
+                        gemm.linear_wgrad(dqkv, xn1, gwqkv)
+
+                store.on_side(attn_wgrads, dx1h, o, dqkv, xn1)
+                dxn1 = gemm.linear_dgrad(dqkv, wqb, wt=wqt)
+                if prev is not None:
+                    seed, soff, p = gemm._drop_args(_half_drop(prev_drop, hi))
+                    ext.layernorm_bwd(dxn1, D, x[r0:r1], D, mean1, rstd1, ln1w, dx1h, D, dx[r0:r1], D, gln1w, gln1b, Th,
+                                      dsum=gprev_b2, dz=None if dzp is None else dzp[r0:r1], seed=seed,
+                                      seed_offset=soff, drop_p=p)
+                else:
+                    ext.layernorm_bwd(dxn1, D, x[r0:r1], D, mean1, rstd1, ln1w, dx1h, D, dx[r0:r1], D, gln1w, gln1b, Th)
+        for t in (dx2, dz2_full, dx1, dx, x) + ((dzp,) if dzp is not None else ()):
+            t.record_stream(side)
+        main.wait_stream(side)
+        if prev is not None:
+            prev.dz2, prev.done = dzp, True
+        ctx.halves = None
+        store.grad_ready([w2, b2, w1, b1, ln2w, ln2b, bo, wo, bqkv, wqkv, ln1w, ln1b])
         return (dx,) + (None,) * (10 + len(params))
 
 

@@ -474,6 +474,59 @@ def check_vit_block_link(B=3):
     return (f"vit dropout: linked LN-bwd dz2/db2 vs colsum (worst {worst})", max(e_fwd, e_g), 2e-2)
 
 
+def _micro(on: bool):
+    """Context: force the two-stream micro-batched encoder blocks on (any batch >= 2) or off."""
+    import contextlib
+
+    from pytorch_vit_paper_replication_amd.ops import fused_vit
+
+    @contextlib.contextmanager
+    def ctx():
+        old = (fused_vit.MICRO, fused_vit.MICRO_MIN_IMAGES)
+        fused_vit.MICRO, fused_vit.MICRO_MIN_IMAGES = (2, 1) if on else (1, 1)
+        try:
+            yield
+        finally:
+            fused_vit.MICRO, fused_vit.MICRO_MIN_IMAGES = old
+
+    return ctx()
+
+
+def check_vit_micro(B=7):
+    """Two-stream micro-batched blocks vs one stream, no dropout: the halves are row ranges of the
+    same buffers, so logits and every gradient must agree (up to the split-K / atomic summation order
+    of the weight and bias gradients)."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+
+    torch.manual_seed(0)
+    m = ViT(image_size=64, patch_size=16, num_transformer_layer=3, num_heads=2, embedding_dim=128, mlp_size=256,
+            num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0).to(DEV).train()
+    x = torch.rand(B, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B,), device=DEV)
+    grads, logits = [], []
+    for on in (False, True):
+        with _micro(on):
+            for p in m.parameters():
+                p.grad = None
+            lg = m(x)
+            F.cross_entropy(lg, y).backward()
+            logits.append(lg.detach().clone())
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    e_fwd = rel_err(logits[1], logits[0])
+    e_g, worst = 0.0, ""
+    for n in grads[0]:
+        e = rel_err(grads[1][n], grads[0][n])
+        if e > e_g:
+            e_g, worst = e, n
+    return (f"vit micro-batched (2 streams) vs single stream B{B} (fwd {e_fwd:.1e}, worst grad {worst})", max(e_fwd, e_g), 1e-2)
+
+
+def check_vit_block_link_micro(B=6):
+    with _micro(True):
+        name, e, tol = check_vit_block_link(B)
+    return ("micro-batched " + name, e, tol)
+
+
 def all_checks() -> List[Callable]:
     c = []
     for tile in (0, 6, 12, 13):
@@ -548,6 +601,9 @@ def all_checks() -> List[Callable]:
         lambda: check_vit_fused_vs_reference(4, False),
         lambda: check_vit_fused_vs_reference(3, True),
         lambda: check_vit_block_link(),
+        lambda: check_vit_micro(),
+        lambda: check_vit_micro(64),
+        lambda: check_vit_block_link_micro(),
         # ViT-H/14-like geometry: patch 14, head dim 80, D = 5 x 64
         lambda: check_vit_fused_vs_reference(2, True, image_size=56, patch_size=14, num_heads=4, embedding_dim=320,
                                              mlp_size=640),
