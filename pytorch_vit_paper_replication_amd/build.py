@@ -73,7 +73,7 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
     hip_flags = [
         f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
         "-munsafe-fp-atomics", "-Wno-unused-result",
-    ]
+    ] + os.environ.get("PVR_HIPCC_EXTRA", "").split()  # experiment builds (e.g. -DPVR_EXP=1)
     for src in hip_srcs:
         obj = build_dir / (src.stem + ".o")
         objs.append(obj)

@@ -20,6 +20,7 @@ EPI_BF16, EPI_GELU, EPI_DGELU, EPI_F32_ATOMIC, EPI_F32_STORE = range(5)
 # tile configs: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves), 2 = 128x256 (8 waves)
 _FORCE_TILE = os.environ.get("PVR_GEMM_TILE")
 _PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "0") == "1"  # A/B: 12 faster once its epilogue loads were fixed
+_GELU_TILE = int(os.environ.get("PVR_GELU_TILE", "13"))  # tile config of the fc1 GELU forward (A/B)
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
@@ -39,7 +40,9 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
         # It pays for the VALU-heavy GELU epilogue (fc1 fwd 0.377 vs 0.457 ms at ViT-B/16 b256,
         # profiles/kbench_epilogues.log); epilogues that load per-row inputs (residual, dGELU
         # factor) drain the in-flight DMAs there and stay on the one-tile-per-workgroup form (12).
-        return 13 if K >= 128 and (gelu or _PERSISTENT) else 12
+        if gelu:
+            return _GELU_TILE if K >= 128 else 12
+        return 13 if K >= 128 and _PERSISTENT else 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
         return 12
     return 0
