@@ -431,6 +431,16 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 
 }  // namespace
 
+// A HIP stream restricted to the CUs whose bits are set in `words` (32 CUs per word): the
+// weight-gradient side stream can be confined to a CU partition (PVR_SIDE_CU_MASK, A/B knob).
+int64_t cu_mask_stream(std::vector<int64_t> words) {
+  std::vector<uint32_t> m(words.size());
+  for (size_t i = 0; i < words.size(); ++i) m[i] = (uint32_t)words[i];
+  hipStream_t st = nullptr;
+  check(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()), "hipExtStreamCreateWithCUMask");
+  return (int64_t)(intptr_t)st;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pvr_comm::register_comm(m);
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
@@ -451,6 +461,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("im2col", &im2col);
   m.def("cls_rows", &cls_rows);
   m.def("patch_bwd", &patch_bwd);
+  m.def("cu_mask_stream", &cu_mask_stream);
   m.def("xent", &xent);
   m.def("grad_norm", &grad_norm);
   m.def("norm_partial_blocks", []() { return pvr_norm_partial_blocks(); });

@@ -234,7 +234,12 @@ class ParamStore:
         if self.device.type != "cuda" or os.environ.get("PVR_SIDE_WGRAD", "1") == "0":
             return None
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            spec = os.environ.get("PVR_SIDE_CU_MASK")
+            if spec:
+                handle = _ext.ext().cu_mask_stream(cu_mask_words(spec, torch.cuda.get_device_properties(self.device).multi_processor_count))
+                self._side = torch.cuda.ExternalStream(handle, device=self.device)
+            else:
+                self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
     def on_side(self, fn: Callable[[], None], *tensors: torch.Tensor) -> None:
@@ -297,6 +302,26 @@ class ParamStore:
                 return
             for fn in self._listeners:
                 fn(ps)
+
+
+def cu_mask_words(spec: str, n_cu: int) -> List[int]:
+    """CU-mask words for a spec: comma-separated ``lo-hi`` CU ranges, or ``mod:M:r1+r2`` (CUs whose
+    index mod M is one of the r's)."""
+    sel = set()
+    for part in spec.split(","):
+        part = part.strip()
+        if part.startswith("mod:"):
+            _, m, rs = part.split(":")
+            keep = {int(r) for r in rs.split("+")}
+            sel |= {c for c in range(n_cu) if c % int(m) in keep}
+        elif part:
+            lo, _, hi = part.partition("-")
+            sel |= set(range(int(lo), int(hi or lo) + 1))
+    words = [0] * ((n_cu + 31) // 32)
+    for c in sel:
+        if 0 <= c < n_cu:
+            words[c // 32] |= 1 << (c % 32)
+    return words
 
 
 def lookup_store(p: torch.nn.Parameter) -> Optional[ParamStore]:
