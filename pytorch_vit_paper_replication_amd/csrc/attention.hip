@@ -404,7 +404,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
                                                         const uint16_t* __restrict__ o, int64_t ld_o,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
-                                                        float* __restrict__ dbias, int N, int H, int D, float scale) {
+                                                        float* __restrict__ dbias, int N, int H, int D, float scale,
+                                                        int key_off, int key_end) {
   using C = Hd<DH>;
   constexpr int QB = 32;
   constexpr int RB = 128 * C::NH;  // LDS bytes per staged head row
@@ -414,10 +415,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
-  const int nkb = (N + KB - 1) / KB;
+  // this launch owns keys [key_off, key_end) (the whole range, or the KB-aligned body / the tail)
+  const int nkb = (key_end - key_off + KB - 1) / KB;
   const int L = xcd_remap(blockIdx.x, gridDim.x);  // key blocks of one (batch, head) share an XCD's L2
   const int bh = L / nkb, b = bh / H, h = bh % H;
-  const int kb0 = (L % nkb) * KB;
+  const int kb0 = key_off + (L % nkb) * KB;
   const int kw0 = kb0 + wave * 32;
   PVR_ASSERT(kb0 < N && L < (int)gridDim.x && (KB & (KB - 1)) == 0);
 
@@ -1177,8 +1179,6 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   const int RB = 128 * Hd<DH>::NH;
-  // K image | 2 x (Q | dO | O) blocks | dS | 2 x 1 KiB lse DMA slots
-  const size_t smem = (size_t)KB * RB + 6 * 32 * RB + 32 * KB * 2 + 2 * 1024;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1186,8 +1186,30 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3(nkb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq,
-                     nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale);
+  // K image | 2 x (Q | dO | O) blocks | dS | 2 x 1 KiB lse DMA slots
+  auto launch = [&](int nw, int k0, int k1) {
+    const int kb = nw * 32;
+    const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
+    hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout, ld_do, out,
+                       ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1);
+  };
+  static const bool tail_split = [] {  // PVR_ATTN_BWD_TAIL=0: one launch over every key block (A/B)
+    const char* e = getenv("PVR_ATTN_BWD_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  const int rem = N % KB;
+  if (tail_split && nkb > 1 && rem >= 16 && rem <= 128 && !dbias) {
+    // N = a multiple of KB plus a short tail (ViT-L/16@384: 577 = 2 x 256 + 65): the KB-aligned body
+    // in full-size workgroups, the tail in workgroups sized for it, instead of 8-wave workgroups with
+    // 3 live waves holding a CU each (818 vs 862 us at B64 H16). A 1-key tail (257 = 256 + 1, the
+    // CLS token of 224/14) is cheaper left interleaved in the one grid: as its own launch of 1-wave
+    // workgroups it serialises 9 query-block staging round trips per pair (975 vs 915 us at H/14
+    // b128; scripts/attn_shape_probe.py)
+    launch(NW, 0, N - rem);
+    launch(pvr_attn_bwd_waves(rem), N - rem, N);
+  } else {
+    launch(NW, 0, N);
+  }
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
     int64_t blocks = (rows * D + 255) / 256;
