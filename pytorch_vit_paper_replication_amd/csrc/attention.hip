@@ -985,6 +985,109 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
   }
 }
 
+// Backward contribution of ONE key (index kt = N - 1) of every (batch, head) pair, after the main
+// kernel has covered keys [0, N - 1) and written dQ directly (bf16). For ViT's N = 256 + 1 (the CLS
+// token of 224/14) the main kernel's key blocks are then exactly full: a 512-thread workgroup per
+// pair for the one remaining key doubled the whole backward (918 vs 451 us at H/14 b128).
+// Thread = (row slot, 16-B head-dim chunk): 16 lanes share one query row (coalesced 16-B chunks),
+// 16 row slots per workgroup walk the queries. Per query: s = Q.K, dp = dO.V, delta = dO.O reduced
+// over the row's lanes, p = exp(s*scale - lse), ds = p (dp - delta); dQ += scale * ds * K in place
+// (bf16 read-modify-write of the main kernel's row); dV += p dO and dK += ds Q accumulate per lane
+// and are reduced over the row slots in LDS at the end. Memory-bound, no MFMA.
+template <int DH>
+__global__ void __launch_bounds__(256) attn_bwd_lastkey_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                                const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                                const uint16_t* __restrict__ o, int64_t ld_o,
+                                                                const float* __restrict__ lse, uint16_t* __restrict__ dqkv,
+                                                                int64_t ld_dq, int N, int H, int D, float scale) {
+  constexpr int NCH = DH / 8;  // 16-B chunks per head row (<= 16)
+  constexpr int RS = 16;       // row slots
+  static_assert(NCH <= 16, "head dim <= 128");
+  __shared__ float red[2][RS][DH];
+  const int pr = blockIdx.x;
+  const int b = pr / H, h = pr % H;
+  const int tid = threadIdx.x;
+  const int ch = tid & 15, rs = tid >> 4;
+  const bool act = ch < NCH;
+  const int cc = act ? ch : 0;
+  const int kt = N - 1;
+  const uint16_t* qbase = qkv + (int64_t)b * N * ld + h * DH + cc * 8;
+  // this lane's chunk of K and V of key kt
+  float kf[8], vf[8];
+  {
+    const uint4 kq = *(const uint4*)(qbase + (int64_t)kt * ld + D);
+    const uint4 vq = *(const uint4*)(qbase + (int64_t)kt * ld + 2 * D);
+    const uint32_t uk[4] = {kq.x, kq.y, kq.z, kq.w}, uv[4] = {vq.x, vq.y, vq.z, vq.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      kf[j] = act ? bf2f(j & 1 ? uk[j >> 1] >> 16 : uk[j >> 1] & 0xFFFF) : 0.f;
+      vf[j] = act ? bf2f(j & 1 ? uv[j >> 1] >> 16 : uv[j >> 1] & 0xFFFF) : 0.f;
+    }
+  }
+  const float c = scale * LOG2E;
+  float av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int q = rs; q < N; q += RS) {
+    const int64_t row = (int64_t)b * N + q;
+    const uint4 qq = *(const uint4*)(qbase + (int64_t)q * ld);
+    const uint4 dd = *(const uint4*)(dout + row * ld_do + h * DH + cc * 8);
+    const uint4 oo = *(const uint4*)(o + row * ld_o + h * DH + cc * 8);
+    uint4* dqp = (uint4*)(dqkv + row * ld_dq + h * DH + cc * 8);
+    const uint4 dq = *dqp;
+    const float l2 = lse[(int64_t)pr * N + q] * LOG2E;
+    const uint32_t uq[4] = {qq.x, qq.y, qq.z, qq.w}, ud[4] = {dd.x, dd.y, dd.z, dd.w}, uo[4] = {oo.x, oo.y, oo.z, oo.w};
+    float qv[8], dv[8];
+    float sdot = 0.f, dpdot = 0.f, dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qv[j] = bf2f(j & 1 ? uq[j >> 1] >> 16 : uq[j >> 1] & 0xFFFF);
+      dv[j] = bf2f(j & 1 ? ud[j >> 1] >> 16 : ud[j >> 1] & 0xFFFF);
+      const float ov = bf2f(j & 1 ? uo[j >> 1] >> 16 : uo[j >> 1] & 0xFFFF);
+      sdot = fmaf(qv[j], kf[j], sdot);
+      dpdot = fmaf(dv[j], vf[j], dpdot);
+      dl = act ? fmaf(dv[j], ov, dl) : dl;
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {  // the row's 16 lanes
+      sdot += __shfl_xor(sdot, off, 16);
+      dpdot += __shfl_xor(dpdot, off, 16);
+      dl += __shfl_xor(dl, off, 16);
+    }
+    const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -l2));
+    const float ds = p * (dpdot - dl);
+    const float f = ds * scale;
+    const uint32_t u[4] = {dq.x, dq.y, dq.z, dq.w};
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = pack2bf(fmaf(f, kf[2 * j], bf2f(u[j] & 0xFFFF)), fmaf(f, kf[2 * j + 1], bf2f(u[j] >> 16)));
+    if (act) *dqp = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av[j] = fmaf(p, dv[j], av[j]);
+      ak[j] = fmaf(ds, qv[j], ak[j]);
+    }
+  }
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][rs][cc * 8 + j] = av[j];
+      red[1][rs][cc * 8 + j] = ak[j];
+    }
+  }
+  __syncthreads();
+  if (tid < DH) {
+    float sv = 0.f, sk = 0.f;
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+      sv += red[0][r][tid];
+      sk += red[1][r][tid];
+    }
+    uint16_t* krow = dqkv + ((int64_t)b * N + kt) * ld_dq + h * DH;
+    krow[D + tid] = f2bf(sk * scale);
+    krow[2 * D + tid] = f2bf(sv);
+  }
+}
+
 __global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
                                                           int64_t rows, int D) {
   const int64_t n = rows * D;
@@ -1084,6 +1187,28 @@ extern "C" int pvr_attn_bwd_waves(int N) {
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
 }
 
+// PVR_ATTN_BWD_TAIL=0: one launch over every key block (A/B of the body / tail launches below)
+static bool attn_bwd_tail_split() {
+  static const bool on = [] {
+    const char* e = getenv("PVR_ATTN_BWD_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// N = (full key blocks) + 1 key: main kernel + last-key kernel, dQ written directly (no dq_acc)
+static bool attn_bwd_lastkey_path(int N, bool dbias) {
+  const int KB = 32 * pvr_attn_bwd_waves(N);
+  return attn_bwd_tail_split() && (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && N <= 512;
+}
+
+// 1 if pvr_attn_bwd needs the zero-initialised f32 dQ workspace for this shape
+extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias) {
+  if (dh == 64 && N <= 256) return 0;
+  if (pvr_attn_bwd_key_blocks(N) <= 1) return 0;
+  return attn_bwd_lastkey_path(N, dbias != 0) ? 0 : 1;
+}
+
 // PVR_ATTN_BWD_FUSED=1 forces the single-kernel (dS through LDS) backward everywhere (A/B switch)
 static bool bwd_fused_forced() {
   static const bool f = [] {
@@ -1176,7 +1301,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
-  if (nkb > 1 && !dq_acc) return hipErrorInvalidValue;
+  if (nkb > 1 && !dq_acc && !attn_bwd_lastkey_path(N, dbias != nullptr)) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   const int RB = 128 * Hd<DH>::NH;
   static bool attr = false;
@@ -1193,11 +1318,19 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout, ld_do, out,
                        ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1);
   };
-  static const bool tail_split = [] {  // PVR_ATTN_BWD_TAIL=0: one launch over every key block (A/B)
-    const char* e = getenv("PVR_ATTN_BWD_TAIL");
-    return !(e && e[0] == '0');
-  }();
+  const bool tail_split = attn_bwd_tail_split();
   const int rem = N % KB;
+  if (attn_bwd_lastkey_path(N, dbias != nullptr)) {
+    // one key past a full key block: the main kernel over keys [0, N - 1) writes dQ directly, the
+    // last key's dK / dV and dQ contribution come from the streaming kernel above
+    const int kb = NW * 32, k1 = N - 1;
+    const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
+    hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 + kb - 1) / kb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, out,
+                       ld_o, lse, dqkv, ld_dq, nullptr, nullptr, N, H, D, scale, 0, k1);
+    hipLaunchKernelGGL(attn_bwd_lastkey_kernel<DH>, dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq,
+                       N, H, D, scale);
+    return hipGetLastError();
+  }
   if (tail_split && nkb > 1 && rem >= 16 && rem <= 128 && !dbias) {
     // N = a multiple of KB plus a short tail (ViT-L/16@384: 577 = 2 x 256 + 65): the KB-aligned body
     // in full-size workgroups, the tail in workgroups sized for it, instead of 8-wave workgroups with

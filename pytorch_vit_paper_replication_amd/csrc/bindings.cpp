@@ -40,6 +40,7 @@ hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, i
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
 int pvr_attn_bwd_key_blocks(int);
+int pvr_attn_bwd_needs_dq_acc(int, int, int);
 int pvr_attn_bwd_waves(int);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, float*, int, int, int, int, float, hipStream_t);
@@ -404,7 +405,9 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   auto dqkv = torch::empty_like(qkv);
   auto delta = torch::empty_like(lse);  // rowsum(dO * O) workspace of the two-kernel backward
   torch::Tensor dq_acc;
-  if (N > 256) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
+  const bool has_db = dbias.has_value() && dbias->defined();
+  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)(D / H), has_db ? 1 : 0))
+    dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
   // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
   torch::Tensor dbias_part;
   const bool want_db = dbias.has_value() && dbias->defined();

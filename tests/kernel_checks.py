@@ -584,6 +584,8 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_fwd(2, 257, 3, 80),
         lambda: check_attn_fwd(1, 33, 2, 80),
         lambda: check_attn_bwd(2, 257, 3, 80),
+        lambda: check_attn_bwd(3, 257, 4, 64),    # N = 256 + 1: key-block body + last-key kernel
+        lambda: check_attn_bwd(2, 257, 2, 128),
         lambda: check_attn_bwd(1, 40, 2, 80),
         lambda: check_attn_fwd(1, 197, 2, 128),
         lambda: check_attn_bwd(1, 300, 2, 128),
