@@ -28,6 +28,8 @@ SITE_SHIFT = 32
 # in_proj bias gradient inside the attention backward: correct, but A/B-measured 0.35 ms/step slower than
 # the separate column-sum kernel on ViT-B/16 b256, so opt-in
 _FUSE_QKV_DBIAS = os.environ.get("PVR_ATTN_DBIAS", "0") == "1"
+# in_proj bias gradient on the weight-gradient side stream (PVR_SIDE_QKV_DB=0: on the dgrad chain, A/B)
+_SIDE_QKV_DB = os.environ.get("PVR_SIDE_QKV_DB", "1") == "1"
 
 
 def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
@@ -268,15 +270,21 @@ class EncoderBlockFn(torch.autograd.Function):
         do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
         # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
         gbqkv = g(bqkv)
+        side_db = False
         if _FUSE_QKV_DBIAS:
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None if gbqkv is None else gbqkv.view(-1))
         else:
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
-            if gbqkv is not None:
+            side_db = gbqkv is not None and _SIDE_QKV_DB
+            if gbqkv is not None and not _SIDE_QKV_DB:
                 gemm.bias_grad(dqkv, gbqkv)
         gwo, gwqkv = g(wo), g(wqkv)
 
         def attn_wgrads():
+            # the in_proj bias gradient (a memory-bound column sum, consumed only by the optimizer)
+            # rides on the side stream with the weight gradients, off the dgrad chain
+            if side_db:
+                gemm.bias_grad(dqkv, gbqkv)
             if gwo is not None:
                 gemm.linear_wgrad(dx1, o, gwo)
             if gwqkv is not None:
