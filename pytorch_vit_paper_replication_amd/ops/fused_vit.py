@@ -30,6 +30,8 @@ SITE_SHIFT = 32
 _FUSE_QKV_DBIAS = os.environ.get("PVR_ATTN_DBIAS", "0") == "1"
 # in_proj bias gradient on the weight-gradient side stream (PVR_SIDE_QKV_DB=0: on the dgrad chain, A/B)
 _SIDE_QKV_DB = os.environ.get("PVR_SIDE_QKV_DB", "1") == "1"
+# fc1 bias gradient as a side-stream column sum instead of inside the dGELU GEMM epilogue (A/B)
+_SIDE_B1_DB = os.environ.get("PVR_SIDE_B1_DB", "0") == "1"
 
 
 def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
@@ -251,10 +253,14 @@ class EncoderBlockFn(torch.autograd.Function):
             if b2.requires_grad:
                 gemm.bias_grad(dx2, g(b2))
         # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
-        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=g(b1))
+        gb1 = g(b1)
+        side_b1 = _SIDE_B1_DB and gb1 is not None
+        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=None if side_b1 else gb1)
         gw2, gw1 = g(w2), g(w1)
 
         def mlp_wgrads():
+            if side_b1:
+                gemm.bias_grad(du, gb1)
             if gw2 is not None:
                 gemm.linear_wgrad(dz2, h, gw2)
             if gw1 is not None:
