@@ -32,6 +32,9 @@ _FUSE_QKV_DBIAS = os.environ.get("PVR_ATTN_DBIAS", "0") == "1"
 _SIDE_QKV_DB = os.environ.get("PVR_SIDE_QKV_DB", "1") == "1"
 # fc1 bias gradient as a side-stream column sum instead of inside the dGELU GEMM epilogue (A/B)
 _SIDE_B1_DB = os.environ.get("PVR_SIDE_B1_DB", "0") == "1"
+# queue each weight gradient on the side stream as soon as its operands exist (W2 before the fc2
+# dgrad, Wo before the attention backward) instead of in two batches behind later dgrad kernels
+EARLY_WGRAD = os.environ.get("PVR_EARLY_WGRAD", "0") == "1"  # A/B: slower (profiles/early_wgrad_ab.log)
 
 
 def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
@@ -255,13 +258,16 @@ class EncoderBlockFn(torch.autograd.Function):
         # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
         gb1 = g(b1)
         side_b1 = _SIDE_B1_DB and gb1 is not None
-        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=None if side_b1 else gb1)
         gw2, gw1 = g(w2), g(w1)
+        early = EARLY_WGRAD
+        if early and gw2 is not None:  # dW2 = dz2^T h needs nothing from this block's dgrads
+            store.on_side(lambda: gemm.linear_wgrad(dz2, h, gw2), dz2, h)
+        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=None if side_b1 else gb1)
 
         def mlp_wgrads():
             if side_b1:
                 gemm.bias_grad(du, gb1)
-            if gw2 is not None:
+            if gw2 is not None and not early:
                 gemm.linear_wgrad(dz2, h, gw2)
             if gw1 is not None:
                 gemm.linear_wgrad(du, xn2, gw1)
@@ -273,6 +279,9 @@ class EncoderBlockFn(torch.autograd.Function):
         ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T, dsum=g(bo))
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
+        gwo, gwqkv = g(wo), g(wqkv)
+        if early and gwo is not None:  # dWo = dx1^T o: ready as soon as dx1 is
+            store.on_side(lambda: gemm.linear_wgrad(dx1, o, gwo), dx1, o)
         do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
         # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
         gbqkv = g(bqkv)
@@ -284,14 +293,13 @@ class EncoderBlockFn(torch.autograd.Function):
             side_db = gbqkv is not None and _SIDE_QKV_DB
             if gbqkv is not None and not _SIDE_QKV_DB:
                 gemm.bias_grad(dqkv, gbqkv)
-        gwo, gwqkv = g(wo), g(wqkv)
 
         def attn_wgrads():
             # the in_proj bias gradient (a memory-bound column sum, consumed only by the optimizer)
             # rides on the side stream with the weight gradients, off the dgrad chain
             if side_db:
                 gemm.bias_grad(dqkv, gbqkv)
-            if gwo is not None:
+            if gwo is not None and not early:
                 gemm.linear_wgrad(dx1, o, gwo)
             if gwqkv is not None:
                 gemm.linear_wgrad(dqkv, xn1, gwqkv)
