@@ -32,28 +32,45 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
   const int64_t n = rows * per_row;
   const float qs = qscale ? *qscale : 1.f;
   float m = 0.f;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / per_row;
-    const int c = (int)(i % per_row) * 16;
-    const uint16_t* src = x + r * ldx + c;
-    const uint4 u0 = *(const uint4*)src, u1 = *(const uint4*)(src + 8);
-    const uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-    float v[16];
+  // U grid-stride steps per trip with all their loads issued first (clamped, so unconditional):
+  // the grid is capped at 256 blocks for the amax atomics, so memory-level parallelism has to come
+  // from each thread keeping several 32-B loads in flight
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i0 = blockIdx.x * 256ll + threadIdx.x; i0 < n; i0 += U * stride) {
+    uint4 ua[U], ub[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v[2 * j] = bf2f(w[j] & 0xFFFF);
-      v[2 * j + 1] = bf2f(w[j] >> 16);
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = min(i0 + u * stride, n - 1);
+      const int64_t r = i / per_row;
+      const uint16_t* src = x + r * ldx + (int)(i % per_row) * 16;
+      ua[u] = *(const uint4*)src;
+      ub[u] = *(const uint4*)(src + 8);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[j]));
-    if (y) {
-      int o[4];
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n) break;
+      const int64_t r = i / per_row;
+      const int c = (int)(i % per_row) * 16;
+      const uint32_t w[8] = {ua[u].x, ua[u].y, ua[u].z, ua[u].w, ub[u].x, ub[u].y, ub[u].z, ub[u].w};
+      float v[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int t = pack2_fp8<FMT, false>(v[4 * q] * qs, v[4 * q + 1] * qs, 0);
-        o[q] = pack2_fp8<FMT, true>(v[4 * q + 2] * qs, v[4 * q + 3] * qs, t);
+      for (int j = 0; j < 8; ++j) {
+        v[2 * j] = bf2f(w[j] & 0xFFFF);
+        v[2 * j + 1] = bf2f(w[j] >> 16);
       }
-      *(int4*)(y + r * ldy + c) = make_int4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[j]));
+      if (y) {
+        int o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int t = pack2_fp8<FMT, false>(v[4 * q] * qs, v[4 * q + 1] * qs, 0);
+          o[q] = pack2_fp8<FMT, true>(v[4 * q + 2] * qs, v[4 * q + 3] * qs, t);
+        }
+        *(int4*)(y + r * ldy + c) = make_int4(o[0], o[1], o[2], o[3]);
+      }
     }
   }
   // one same-address atomic per BLOCK: those serialise at L2 (~12 ns each), so the grid is capped
