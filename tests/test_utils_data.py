@@ -1,0 +1,146 @@
+"""CPU tests of the auxiliary API surface: torchinfo-style summary (MAIN.ipynb:2317-2322), transforms
+(MAIN.ipynb:254-265, EX.ipynb:225-232, GM/predictions.py:46-54), single-image prediction
+(GM/predictions.py:20-83), plot_loss_curves / download_data / set_seeds (the course helper_functions,
+MAIN.ipynb:81), JSONL metrics and ROCTX ranges."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+from pytorch_vit_paper_replication_amd.data import transforms as T
+from pytorch_vit_paper_replication_amd.models import ViT
+from pytorch_vit_paper_replication_amd.utils.metrics import StepTimer, WallTimer, append_jsonl
+from pytorch_vit_paper_replication_amd.utils.profiling import range_push
+from pytorch_vit_paper_replication_amd.utils.summary import count_params, summary
+
+
+def _img(w=40, h=30, seed=0):
+    rng = np.random.default_rng(seed)
+    return Image.fromarray(rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8), "RGB")
+
+
+def test_vit_b16_param_count_matches_reference():
+    # EX.ipynb:662 / MAIN.ipynb torchinfo output: ViT-B/16 with 3 classes has 85,800,963 params
+    m = ViT(num_classes=3)
+    assert count_params(m) == 85_800_963
+    assert count_params(m, trainable_only=True) == 85_800_963
+
+
+def test_summary_small_vit_reports_totals_and_shapes():
+    m = ViT(image_size=32, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=32, mlp_size=64,
+            num_classes=5)
+    s = summary(m, input_size=(2, 3, 32, 32), depth=1, print_out=False)
+    assert f"Total params: {count_params(m):,}" in s
+    assert "Non-trainable params: 0" in s
+    assert "[2, 5]" in s  # classifier output shape
+    for p in m.patch_embedding_block.parameters():
+        p.requires_grad_(False)
+    s2 = summary(m, input_size=(2, 3, 32, 32), depth=1, print_out=False)
+    frozen = sum(p.numel() for p in m.patch_embedding_block.parameters())
+    assert f"Non-trainable params: {frozen:,}" in s2
+    assert m.training  # summary restores the train flag
+
+
+def test_resize_totensor_normalize():
+    img = _img(40, 30)
+    x = T.Compose([T.Resize((24, 20)), T.ToTensor()])(img)
+    assert x.shape == (3, 24, 20) and x.dtype == torch.float32
+    assert 0.0 <= x.min().item() and x.max().item() <= 1.0
+    # int size resizes the short side, keeping the aspect ratio
+    assert T.Resize(15)(img).size == (20, 15)
+    # Normalize is (x - mean) / std per channel
+    n = T.Normalize()(x)
+    mean = torch.tensor(T.IMAGENET_MEAN).view(3, 1, 1)
+    std = torch.tensor(T.IMAGENET_STD).view(3, 1, 1)
+    torch.testing.assert_close(n, (x - mean) / std)
+
+
+def test_v2_pipeline_matches_totensor():
+    img = _img(16, 16, seed=1)
+    a = T.default_vit_transform(16)(img)
+    b = T.ToTensor()(img)
+    torch.testing.assert_close(a, b)  # same-size resize is the identity; scale=True maps to [0,1]
+    u8 = T.ToImage()(img)
+    assert u8.dtype == torch.uint8 and u8.shape == (3, 16, 16)
+    assert T.ToDtype(torch.float32, scale=False)(u8).max().item() > 1.0
+
+
+def test_center_crop_pil_and_tensor_agree():
+    img = _img(40, 30, seed=2)
+    crop_pil = T.ToTensor()(T.CenterCrop(20)(img))
+    crop_t = T.CenterCrop(20)(T.ToTensor()(img))
+    assert crop_pil.shape == (3, 20, 20)
+    torch.testing.assert_close(crop_pil, crop_t)
+    y = T.imagenet_eval_transform(image_size=24, resize=32)(img)
+    assert y.shape == (3, 24, 24)
+
+
+def test_tensor_resize_keeps_uint8():
+    t = torch.randint(0, 256, (3, 10, 12), dtype=torch.uint8)
+    r = T.Resize((5, 6))(t)
+    assert r.dtype == torch.uint8 and r.shape == (3, 5, 6)
+
+
+def test_predict_and_plot(tmp_path):
+    from pytorch_vit_paper_replication_amd.predictions import pred_and_plot_image, predict_image
+
+    path = tmp_path / "img.jpg"
+    _img(50, 40, seed=3).save(path)
+    torch.manual_seed(0)
+    m = ViT(image_size=32, patch_size=16, num_transformer_layer=1, num_heads=2, embedding_dim=32, mlp_size=64,
+            num_classes=3)
+    label, probs, _ = predict_image(m, str(path), image_size=(32, 32), device="cpu")
+    assert probs.shape == (1, 3) and 0 <= label < 3
+    torch.testing.assert_close(probs.sum(), torch.tensor(1.0))
+    assert label == int(probs.argmax())
+    out = tmp_path / "pred.png"
+    assert pred_and_plot_image(m, ["a", "b", "c"], str(path), image_size=(32, 32), device="cpu",
+                               save_path=str(out)) is None
+    assert out.is_file() and out.stat().st_size > 0
+
+
+def test_helper_functions(tmp_path, monkeypatch):
+    import helper_functions as hf
+
+    res = {"train_loss": [1.0, 0.5], "test_loss": [1.1, 0.7], "train_acc": [0.3, 0.6], "test_acc": [0.2, 0.5]}
+    out = tmp_path / "curves.png"
+    hf.plot_loss_curves(res, save_path=str(out))
+    assert out.is_file() and out.stat().st_size > 0
+
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "data" / "pizza_steak_sushi").mkdir(parents=True)
+    assert hf.download_data("http://unused", "pizza_steak_sushi").name == "pizza_steak_sushi"
+    with pytest.raises(RuntimeError, match="No network"):
+        hf.download_data("http://unused", "missing_dataset")
+
+    hf.set_seeds(7)
+    a = torch.rand(3)
+    hf.set_seeds(7)
+    torch.testing.assert_close(a, torch.rand(3))
+
+
+def test_metrics_jsonl_and_timers(tmp_path):
+    p = tmp_path / "m.jsonl"
+    append_jsonl(str(p), {"step": 1, "loss": 2.5})
+    append_jsonl(str(p), {"step": 2, "loss": 2.0})
+    recs = [json.loads(line) for line in p.read_text().splitlines()]
+    assert recs == [{"step": 1, "loss": 2.5}, {"step": 2, "loss": 2.0}]
+    t = StepTimer()
+    t.mark()
+    t.mark()
+    if not torch.cuda.is_available():
+        assert t.intervals_ms() == []
+    with WallTimer() as w:
+        sum(range(1000))
+    assert w.elapsed >= 0.0
+
+
+def test_range_push_is_transparent(monkeypatch):
+    for flag in ("0", "1"):  # with PVR_ROCTX=1 it pushes/pops a ROCTX range if libroctx64 loads
+        monkeypatch.setenv("PVR_ROCTX", flag)
+        with range_push("fwd"):
+            x = 1 + 1
+        assert x == 2
