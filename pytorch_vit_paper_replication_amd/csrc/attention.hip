@@ -786,13 +786,17 @@ __global__ void __launch_bounds__(NF * 64) attn_bwd_dq_head_kernel(const uint16_
       v4s klo[4], khi[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) frag_tr_async(kimg, NP, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, klo[e], khi[e]);
-      // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse2); keys past N contribute nothing
+      // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse2); keys past N contribute nothing.
+      // NF = ceil(N / 16), so keys below 16 (NF - 1) are always < N: only the chunks reaching
+      // past that need the mask (one of seven at N = 197; cmp + cndmask per element otherwise).
+      const bool tail = 32 * kk + 32 > 16 * (NF - 1);  // folds per unrolled kk
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = 32 * kk + 16 * h2 + 4 * g + r;
-          const float pv = key < N ? __builtin_amdgcn_exp2f(fmaf(sv[h2][r], c, -l2)) : 0.f;
+          const float e = __builtin_amdgcn_exp2f(fmaf(sv[h2][r], c, -l2));
+          const float pv = (!tail || key < N) ? e : 0.f;
           sv[h2][r] = pv * (dp[h2][r] - dl);
         }
       const v8s dsf = pack_p(sv[0], sv[1]);
