@@ -826,25 +826,28 @@ __global__ void __launch_bounds__(NF * 64) attn_bwd_dq_head_kernel(const uint16_
   }
 }
 
-template <int NK>
+// KF = key fragments (of 16) per wave: KF = 2 is 32 keys per wave (NK = ceil(N / 32) waves); KF = 1
+// is 16 keys per wave with twice the waves (half the accumulators per wave, more waves to hide latency).
+template <int NK, int KF>
 __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                                      const uint16_t* __restrict__ dout, int64_t ld_do,
                                                                      const float* __restrict__ lse, const float* __restrict__ delta,
                                                                      uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H,
                                                                      int D, int npairs, float scale) {
   constexpr int DH = 64;
-  constexpr int NP = 32 * NK;                 // query rows staged (and keys covered)
+  constexpr int NQB = (NK * KF + 1) / 2;      // 32-query blocks
+  constexpr int NP = 32 * NQB;                // query rows staged (and keys covered)
   constexpr int BUF = 2 * NP * 128 + 2048;    // Q | dO images | lse | delta (1 KiB DMA slots)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
-  PVR_ASSERT((N + 31) / 32 == NK && blockDim.x == NK * 64 && (int)gridDim.x <= npairs);
+  PVR_ASSERT((N + 16 * KF - 1) / (16 * KF) == NK && blockDim.x == NK * 64 && (int)gridDim.x <= npairs);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
   const int p0 = L * per + min(L, rem);
   const int p1 = p0 + per + (L < rem ? 1 : 0);
-  const int kw0 = wave * 32;
+  const int kw0 = wave * 16 * KF;
   const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
   const uint32_t do_extent = clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2);
   const float c = scale * LOG2E;
@@ -860,12 +863,12 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
   };
   // this wave's 32 keys: K and V fragments as B operands (lane holds X[kw0 + 16f + li][32ks + 8g + j])
   struct KOps {
-    v8s kf[2][2], vf[2][2];
+    v8s kf[KF][2], vf[KF][2];
   };
   auto load_k = [&](int pr, KOps& t) {
     const uint16_t* base = qkv + (int64_t)(pr / H) * N * ld + (pr % H) * DH + 8 * g;
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < KF; ++f) {
       const int key = min(kw0 + 16 * f + li, N - 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -875,10 +878,13 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
     }
   };
   auto settle = [&](KOps& t) {
-    asm volatile("" : "+v"(t.kf[0][0]), "+v"(t.kf[0][1]), "+v"(t.kf[1][0]), "+v"(t.kf[1][1]));
-    asm volatile("" : "+v"(t.vf[0][0]), "+v"(t.vf[0][1]), "+v"(t.vf[1][0]), "+v"(t.vf[1][1]));
+#pragma unroll
+    for (int f = 0; f < KF; ++f) {
+      asm volatile("" : "+v"(t.kf[f][0]), "+v"(t.kf[f][1]));
+      asm volatile("" : "+v"(t.vf[f][0]), "+v"(t.vf[f][1]));
+    }
   };
-  constexpr int STORES = 16;  // dK and dV rows: 2 key fragments x 4 dim fragments x 2
+  constexpr int STORES = 8 * KF;  // dK and dV rows: KF key fragments x 4 dim fragments x 2
   const uint32_t dkv_extent = clamp_bytes(((int64_t)(N - 1) * ld_dq + 2 * D + DH) * 2);
 
   if (p0 >= p1) return;
@@ -896,22 +902,22 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
     const float* s_dl = s_l2 + 256;
     if (pr + 1 < p1) {
       issue(pr + 1, smem + ((it + 1) & 1) * BUF);
-      load_k(pr + 1, nxt);
+      if constexpr (KF == 2) load_k(pr + 1, nxt);  // KF = 1: after the sweep (keeps 16 VGPRs free in it)
     }
-    v4f dk[4][2], dv[4][2];
+    v4f dk[4][KF], dv[4][KF];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int f = 0; f < 2; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int f = 0; f < KF; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
     if (kw0 < N) {  // uniform: waves past N only stage
 #pragma unroll 1
-      for (int qb = 0; qb < NK; ++qb) {
+      for (int qb = 0; qb < NQB; ++qb) {
         // S[q][key], dP[q][key]: lane holds [q = 32qb + 16a + 4g + r][key = kw0 + 16f + li]
-        v4f sv[2][2], dp[2][2];
+        v4f sv[2][KF], dp[2][KF];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int f = 0; f < 2; ++f) sv[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+          for (int f = 0; f < KF; ++f) sv[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -919,17 +925,18 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
             const v8s qa = frag_rows(qimg, NP, 32 * qb + 16 * a, ks, lane);
             const v8s da = frag_rows(doimg, NP, 32 * qb + 16 * a, ks, lane);
 #pragma unroll
-            for (int f = 0; f < 2; ++f) {
+            for (int f = 0; f < KF; ++f) {
               sv[a][f] = mfma16(qa, cur.kf[f][ks], sv[a][f]);
               dp[a][f] = mfma16(da, cur.vf[f][ks], dp[a][f]);
             }
           }
-        // dO^T / Q^T fragments for the dV / dK products (asm transpose reads)
+        // dO^T / Q^T fragments for the dV / dK products (asm transpose reads). KF = 1 reads Q^T only
+        // after the dV products, so both sets are never live together (fits 128 VGPRs, no spills).
         v4s dlo[4], dhi[4], qlo[4], qhi[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           frag_tr_async(doimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, dlo[e], dhi[e]);
-          frag_tr_async(qimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, qlo[e], qhi[e]);
+          if constexpr (KF == 2) frag_tr_async(qimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, qlo[e], qhi[e]);
         }
         // P = exp2(S c - lse2[q]), dS = P (dP - delta[q]); queries past N have zero Q / dO rows
 #pragma unroll
@@ -939,29 +946,43 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int f = 0; f < 2; ++f) {
+            for (int f = 0; f < KF; ++f) {
               const float pv = __builtin_amdgcn_exp2f(fmaf(sv[a][f][r], c, -l4[r] * LOG2E));
               sv[a][f][r] = pv;
               dp[a][f][r] = pv * (dp[a][f][r] - d4[r]);
             }
         }
-        v8s pf[2], sf[2];
+        v8s pf[KF], sf[KF];
 #pragma unroll
-        for (int f = 0; f < 2; ++f) {
+        for (int f = 0; f < KF; ++f) {
           pf[f] = pack_p(sv[0][f], sv[1][f]);
           sf[f] = pack_p(dp[0][f], dp[1][f]);
         }
         lds_wait();
+        if constexpr (KF == 2) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const v8s dot = cat44(dlo[e], dhi[e]), qt = cat44(qlo[e], qhi[e]);
+          for (int e = 0; e < 4; ++e) {
+            const v8s dot = cat44(dlo[e], dhi[e]), qt = cat44(qlo[e], qhi[e]);
 #pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
-            dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
+            for (int f = 0; f < KF; ++f) {
+              dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
+              dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
+            }
           }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            dv[e][0] = mfma16(cat44(dlo[e], dhi[e]), pf[0], dv[e][0]);
+            frag_tr_async(qimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, qlo[e], qhi[e]);
+          }
+          lds_wait();
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dk[e][0] = mfma16(cat44(qlo[e], qhi[e]), sf[0], dk[e][0]);
         }
       }
+    }
+    if constexpr (KF == 1) {
+      if (pr + 1 < p1) load_k(pr + 1, nxt);
     }
     // dK (x scale), dV rows: lane holds X^T[d = 16e + 4g + r][key = kw0 + 16f + li]; buffer stores
     // (keys past N dropped), exactly STORES per wave
@@ -969,7 +990,7 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
       typedef unsigned int v2u __attribute__((ext_vector_type(2)));
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(dqkv + (int64_t)(pr / H) * N * ld_dq + (pr % H) * DH, dkv_extent);
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
+      for (int f = 0; f < KF; ++f) {
         const int key = kw0 + 16 * f + li;
         const uint32_t vo = key < N ? (uint32_t)((key * ld_dq + 4 * g) * 2) : 0x80000000u;
 #pragma unroll
@@ -981,8 +1002,9 @@ __global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16
         }
       }
     }
-    static_assert(STORES == 16, "the vmcnt below counts the dK / dV store instructions");
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    static_assert(STORES == 16 || STORES == 8, "the vmcnt below counts the dK / dV store instructions");
+    if constexpr (STORES == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __syncthreads();
     cur = nxt;
     settle(cur);
@@ -1252,20 +1274,20 @@ static hipError_t attn_bwd_dq_head_launch(const uint16_t* qkv, int64_t ld, const
   return hipGetLastError();
 }
 
-template <int NK>
+template <int NK, int KF>
 static hipError_t attn_bwd_dkv_head_launch(const uint16_t* qkv, int64_t ld, const uint16_t* dout, int64_t ld_do, const float* lse,
                                            const float* delta, uint16_t* dqkv, int64_t ld_dq, int npairs, int N, int H, int D,
                                            float scale, hipStream_t s) {
   using namespace pvr;
-  constexpr int SMEM = 2 * (2 * 32 * NK * 128 + 2048);
+  constexpr int SMEM = 2 * (2 * 32 * ((NK * KF + 1) / 2) * 128 + 2048);
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_dkv_head_kernel<NK>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_dkv_head_kernel<NK, KF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int grid = bwd_grid(npairs);
-  hipLaunchKernelGGL(attn_bwd_dkv_head_kernel<NK>, dim3(grid), dim3(NK * 64), SMEM, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
+  hipLaunchKernelGGL((attn_bwd_dkv_head_kernel<NK, KF>), dim3(grid), dim3(NK * 64), SMEM, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
                      N, H, D, npairs, scale);
   return hipGetLastError();
 }
@@ -1285,9 +1307,25 @@ static hipError_t attn_bwd_head(const uint16_t* qkv, int64_t ld, const uint16_t*
     default: break;
   }
   if (e != hipSuccess) return e;
+  static const int kf = [] {  // PVR_DKV_KF: 16-key fragments per dK/dV wave (2: 32 keys, 1: 16 keys)
+    const char* e = getenv("PVR_DKV_KF");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  if (kf == 1) {
+    switch ((N + 15) / 16) {
+#define PVR_BWD_DKV1(NK) \
+  case NK: return attn_bwd_dkv_head_launch<NK, 1>(qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s);
+      PVR_BWD_DKV1(1) PVR_BWD_DKV1(2) PVR_BWD_DKV1(3) PVR_BWD_DKV1(4) PVR_BWD_DKV1(5) PVR_BWD_DKV1(6) PVR_BWD_DKV1(7)
+      PVR_BWD_DKV1(8) PVR_BWD_DKV1(9) PVR_BWD_DKV1(10) PVR_BWD_DKV1(11) PVR_BWD_DKV1(12) PVR_BWD_DKV1(13) PVR_BWD_DKV1(14)
+      PVR_BWD_DKV1(15) PVR_BWD_DKV1(16)
+#undef PVR_BWD_DKV1
+      default: break;
+    }
+    return hipErrorInvalidValue;
+  }
   switch ((N + 31) / 32) {
 #define PVR_BWD_DKV(NK) \
-  case NK: return attn_bwd_dkv_head_launch<NK>(qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s);
+  case NK: return attn_bwd_dkv_head_launch<NK, 2>(qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s);
     PVR_BWD_DKV(1) PVR_BWD_DKV(2) PVR_BWD_DKV(3) PVR_BWD_DKV(4) PVR_BWD_DKV(5) PVR_BWD_DKV(6) PVR_BWD_DKV(7) PVR_BWD_DKV(8)
 #undef PVR_BWD_DKV
     default: break;
