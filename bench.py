@@ -57,6 +57,7 @@ def main():
     from pytorch_vit_paper_replication_amd.models import vit
     from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
     from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.ops import fused_vit
     from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,7 +166,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.dtype == "bf16" else "fp8 (e4m3 forward GEMMs; bf16 backward/attention/norms)",
+            "dtype": "bf16" if args.dtype == "bf16" else ("fp8 (e4m3 forward GEMMs, e5m2-gradient dgrad GEMMs; bf16 wgrad/attention/norms)" if fused_vit.FP8_DGRAD else "fp8 (e4m3 forward GEMMs; bf16 backward/attention/norms)"),
             "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,

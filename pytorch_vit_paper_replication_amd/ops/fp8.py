@@ -70,6 +70,8 @@ class Fp8State:
 
     def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0):
         self.act = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E4M3)
+        # e5m2 gradient slots for the fp8 dgrad GEMMs (PVR_FP8_DGRAD): dz2, dU, dx1, dQKV per block
+        self.grad = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E5M2)
         self.n_blocks = n_blocks
         self._wmeta: Optional[Fp8Meta] = None
         self._wslot: Dict[int, int] = {}
@@ -79,9 +81,13 @@ class Fp8State:
     def begin_step(self, training: bool) -> None:
         if training:
             self.act.step()
+            self.grad.step()
 
     def act_quant(self, x: torch.Tensor, block: int, which: int) -> Tuple[torch.Tensor, torch.Tensor]:
         return self.act.quantize(x, block * self.ACT_PER_BLOCK + which)
+
+    def grad_quant(self, g: torch.Tensor, block: int, which: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        return self.grad.quantize(g, block * self.ACT_PER_BLOCK + which)
 
     def weight(self, w16: torch.Tensor, key: int, generation: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """fp8 (e4m3, current scaling) copy of a bf16 weight shadow, cached per store generation."""

@@ -35,6 +35,8 @@ _SIDE_B1_DB = os.environ.get("PVR_SIDE_B1_DB", "0") == "1"
 # queue each weight gradient on the side stream as soon as its operands exist (W2 before the fc2
 # dgrad, Wo before the attention backward) instead of in two batches behind later dgrad kernels
 EARLY_WGRAD = os.environ.get("PVR_EARLY_WGRAD", "0") == "1"  # A/B: slower (profiles/early_wgrad_ab.log)
+# fp8 mode: also run the four dgrad GEMMs in fp8 (e5m2 gradients x e4m3 W^T, delayed scaling)
+FP8_DGRAD = os.environ.get("PVR_FP8_DGRAD", "1") == "1"  # +5 % ViT-H/14 (profiles/fp8_dgrad_ab.log)
 
 
 def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
@@ -162,6 +164,7 @@ class EncoderBlockFn(torch.autograd.Function):
         if _use_micro(x, B, f8):
             return EncoderBlockFn._forward_micro(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, params)
         ctx.halves = None
+        ctx.f8d = f8 if FP8_DGRAD else None
         M = w1.shape[0]
         scale = 1.0 / math.sqrt(D // H)
         u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
@@ -243,6 +246,19 @@ class EncoderBlockFn(torch.autograd.Function):
         dx2 = dx2.contiguous()
         T, D = dx2.shape
         own, prev = ctx.links
+        f8d = ctx.f8d
+
+        def dgrad(dy, w, which, dgelu_aux=None, colsum=None):
+            wt = store.bf16_t(w)
+            if f8d is not None and wt is not None:
+                from . import fp8 as F8
+
+                st, blk = f8d
+                gq, gs = st.grad_quant(dy, blk, which)
+                wq, ws = st.weight(wt, ~id(w), store.generation)
+                return F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum)
+            return gemm.linear_dgrad(dy, store.bf16(w), dgelu_aux=dgelu_aux, wt=wt, colsum=colsum)
+
         # ---- MLP branch: x2 = x1 + drop2(h . W2^T + b2),  h = drop1(gelu(u)),  u = xn2 . W1^T + b1
         if own is not None and own.done:
             # the next block's LayerNorm backward already produced dz2 and d(b2)
@@ -262,7 +278,7 @@ class EncoderBlockFn(torch.autograd.Function):
         early = EARLY_WGRAD
         if early and gw2 is not None:  # dW2 = dz2^T h needs nothing from this block's dgrads
             store.on_side(lambda: gemm.linear_wgrad(dz2, h, gw2), dz2, h)
-        du = gemm.linear_dgrad(dz2, store.bf16(w2), dgelu_aux=u, wt=store.bf16_t(w2), colsum=None if side_b1 else gb1)
+        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=None if side_b1 else gb1)
 
         def mlp_wgrads():
             if side_b1:
@@ -273,7 +289,7 @@ class EncoderBlockFn(torch.autograd.Function):
                 gemm.linear_wgrad(du, xn2, gw1)
 
         store.on_side(mlp_wgrads, dz2, h, du, xn2)  # weight grads off the critical path
-        dxn2 = gemm.linear_dgrad(du, store.bf16(w1), wt=store.bf16_t(w1))
+        dxn2 = dgrad(du, w1, 1)
         dx1 = torch.empty_like(dx2)
         # dx1 = dx2 + LN2'(dxn2); d(bo) = colsum(dx1) reduced in the same kernel
         ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T, dsum=g(bo))
@@ -282,7 +298,7 @@ class EncoderBlockFn(torch.autograd.Function):
         gwo, gwqkv = g(wo), g(wqkv)
         if early and gwo is not None:  # dWo = dx1^T o: ready as soon as dx1 is
             store.on_side(lambda: gemm.linear_wgrad(dx1, o, gwo), dx1, o)
-        do = gemm.linear_dgrad(dx1, store.bf16(wo), wt=store.bf16_t(wo))
+        do = dgrad(dx1, wo, 2)
         # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
         gbqkv = g(bqkv)
         side_db = False
@@ -305,7 +321,7 @@ class EncoderBlockFn(torch.autograd.Function):
                 gemm.linear_wgrad(dqkv, xn1, gwqkv)
 
         store.on_side(attn_wgrads, dx1, o, dqkv, xn1)
-        dxn1 = gemm.linear_dgrad(dqkv, store.bf16(wqkv), wt=store.bf16_t(wqkv))
+        dxn1 = dgrad(dqkv, wqkv, 3)
         dx = torch.empty_like(dx2)
         if prev is not None:
             # the previous block's fc2 dropout backward and bias gradient ride along with dx

@@ -360,6 +360,43 @@ def check_vit_fp8(B=4):
     return (f"vit fp8 fwd vs fp32 ({e:.2e}), loss {losses[0]:.3f}->{losses[-1]:.3f}", e / 3 + (0 if ok else 1), 5e-2)
 
 
+def check_vit_fp8_dgrad(B=4):
+    """fp8 dgrad GEMMs (PVR_FP8_DGRAD: e5m2 gradients x e4m3 W^T) vs the bf16 dgrads of the same fp8-forward
+    model: gradients close, and training with them decreases the loss."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops import fused_vit
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=256, mlp_size=512,
+               num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0)
+    m = ViT(**cfg).to(DEV).enable_fp8()
+    x = torch.rand(B * 64, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B * 64,), device=DEV)
+    saved = fused_vit.FP8_DGRAD
+    grads = []
+    try:
+        for flag in (False, True, True):  # the second fp8 pass runs on calibrated (delayed) scales
+            fused_vit.FP8_DGRAD = flag
+            m.zero_grad(set_to_none=False)
+            cross_entropy(m(x), y).backward()
+            grads.append(m._pvr_store.grad_flat.float().clone())
+        e = max(((g - grads[0]).norm() / grads[0].norm()).item() for g in grads[1:])  # relative L2
+        opt = FusedAdam(m.parameters(), lr=1e-3)
+        losses = []
+        for _ in range(6):
+            loss = cross_entropy(m(x), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step(clip_norm=1.0)
+            losses.append(loss.item())
+    finally:
+        fused_vit.FP8_DGRAD = saved
+    ok = losses[-1] < losses[0] and all(math.isfinite(v) for v in losses)
+    return (f"vit fp8 dgrad vs bf16 dgrad grads ({e:.2e}), loss {losses[0]:.3f}->{losses[-1]:.3f}", e + (0 if ok else 1), 1e-1)
+
+
 # ----------------------------------------------------------------------------- misc
 def check_xent(B, C):
     ext = _ext.ext()
@@ -597,6 +634,7 @@ def all_checks() -> List[Callable]:
         lambda: check_gemm_fp8(520, 3072, 384, False, True),
         lambda: check_dgrad_fp8(1030, 1280, 768),
         lambda: check_vit_fp8(),
+        lambda: check_vit_fp8_dgrad(),
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
         lambda: check_adam(),
