@@ -14,6 +14,11 @@ import argparse
 import torch
 
 
+def _is_rank0() -> bool:
+    d = torch.distributed
+    return not (d.is_available() and d.is_initialized()) or d.get_rank() == 0
+
+
 def build_parser():
     p = argparse.ArgumentParser(description="Train a ViT (or TinyVGG) with the MI355X-native engine")
     p.add_argument("--model", default="vit_b16", help="vit_b16 | vit_l16 | vit_h14 | vit_tiny_test | tinyvgg")
@@ -24,7 +29,7 @@ def build_parser():
     p.add_argument("--synthetic", action="store_true", help="synthetic ImageNet-shaped data")
     p.add_argument("--synthetic-train-len", type=int, default=512)
     p.add_argument("--synthetic-test-len", type=int, default=128)
-    p.add_argument("--epochs", type=int, default=5)
+    p.add_argument("--epochs", type=int, default=5, help="total epochs (a --resume run trains the rest)")
     p.add_argument("--batch-size", type=int, default=32)
     p.add_argument("--lr", type=float, default=1e-3)
     p.add_argument("--weight-decay", type=float, default=0.03)
@@ -75,12 +80,19 @@ def main(argv=None) -> int:
     else:
         opt = FusedAdam(groups, lr=args.lr, betas=(0.9, 0.999))
     sched = warmup_linear_decay(opt, args.epochs * len(train_dl), args.warmup_frac)
+    start_epoch, results = 0, None
     if args.resume:
-        load_checkpoint(args.resume, model, opt, sched)
+        # --epochs is the TOTAL epoch count: a resumed run trains only the epochs not yet done, on the
+        # same (restored) LR schedule, so it ends where the uninterrupted run would have
+        info = load_checkpoint(args.resume, model, opt, sched)
+        start_epoch, results = int(info["epoch"]), info["results"]
+        if _is_rank0():
+            print(f"[INFO] Resumed {args.resume} at epoch {start_epoch} of {args.epochs}")
     net = DistributedDataParallel(model) if is_dist() else model
     engine.train(model=net, train_dataloader=train_dl, test_dataloader=test_dl, optimizer=opt,
                  loss_fn=torch.nn.CrossEntropyLoss(), lr_scheduler=sched, epochs=args.epochs, device=device,
-                 max_grad_norm=args.max_grad_norm, checkpoint_dir=args.checkpoint_dir, metrics_path=args.metrics)
+                 max_grad_norm=args.max_grad_norm, checkpoint_dir=args.checkpoint_dir, metrics_path=args.metrics,
+                 start_epoch=start_epoch, results=results)
     save_model(model, args.save_dir, args.save_name or f"{args.model}_{args.epochs}_epochs.pth")
     return 0
 

@@ -6,7 +6,8 @@
 //   quant:  y = sat(x * qscale) in fp8,  amax = max(amax, max|x|)   (one pass; qscale == null:
 //           amax only, used to calibrate a tensor the first time it is seen / for weights)
 //   update: per tensor slot, push amax into a history ring, qscale = fmax / max(history) / 2^margin,
-//           dscale = 1 / qscale (the GEMM epilogue's dequant factor), reset amax
+//           dscale = 1 / qscale (the GEMM epilogue's dequant factor), reset amax; a non-finite
+//           amax is dropped (scales unchanged), so one overflowing step cannot poison the history
 #include "common.h"
 
 namespace pvr {
@@ -15,8 +16,9 @@ namespace {
 template <int FMT, bool HI>
 PVR_DEV int pack2_fp8(float a, float b, int old) {
   constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;  // OCP e4m3fn / e5m2 largest finite
-  a = fminf(fmaxf(a, -FMAX), FMAX);
-  b = fminf(fmaxf(b, -FMAX), FMAX);
+  // saturate finite overflow; a NaN stays a NaN (fminf/fmaxf would turn it into -FMAX and hide it)
+  a = a != a ? a : fminf(fmaxf(a, -FMAX), FMAX);
+  b = b != b ? b : fminf(fmaxf(b, -FMAX), FMAX);
   if constexpr (FMT == 0)
     return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
   else
@@ -61,7 +63,12 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
         v[2 * j + 1] = bf2f(w[j] >> 16);
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[j]));
+      for (int j = 0; j < 16; ++j) {
+        // NaN-propagating max (fmaxf drops NaN): a NaN or Inf element makes this tensor's amax
+        // non-finite, which scale_update_kernel then keeps out of the history
+        const float a = fabsf(v[j]);
+        m = (a > m || a != a) ? a : m;
+      }
       if (y) {
         int o[4];
 #pragma unroll
@@ -81,7 +88,8 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
   __syncthreads();
   if (threadIdx.x == 0) {
     const float b = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-    if (b > 0.f) atomicMax(amax, __float_as_uint(b));  // |x| bits order like uints
+    // |x| bits order like uints; Inf (0x7f800000) and NaN (> 0x7f800000) sort above every finite
+    if (!(b <= 0.f)) atomicMax(amax, __float_as_uint(b));
   }
 }
 
@@ -106,6 +114,11 @@ __global__ void scale_update_kernel(float* __restrict__ hist, int H, unsigned* _
   if (i >= s1) return;
   float* h = hist + (int64_t)i * H;
   const float cur = __uint_as_float(amax[i]);
+  amax[i] = 0u;
+  // A non-finite amax (an overflowing step: Inf/NaN in the tensor) is not pushed into the history:
+  // it would make qscale 0 and dscale Inf, i.e. NaN GEMM outputs for the next H steps. The previous
+  // scales stay; the step itself is skipped by the optimizer's non-finite gradient check.
+  if (!isfinite(cur)) return;
   float m = cur;
   for (int k = H - 1; k > 0; --k) {
     h[k] = h[k - 1];
@@ -115,7 +128,6 @@ __global__ void scale_update_kernel(float* __restrict__ hist, int H, unsigned* _
   const float q = m > 0.f ? fmax[i] / m * margin_mul : 1.f;
   qscale[i] = q;
   dscale[i] = 1.f / q;
-  amax[i] = 0u;
 }
 
 }  // namespace

@@ -71,9 +71,20 @@ def _reduce_means(sums: torch.Tensor, count: int, device) -> Tuple[float, ...]:
     return tuple((vals[:-1] / n).tolist())
 
 
+def _set_sampler_epoch(dataloader, epoch: Optional[int]) -> None:
+    """Reshuffle a DistributedSampler per epoch (otherwise every epoch repeats one permutation)."""
+    sampler = getattr(dataloader, "sampler", None)
+    if epoch is not None and hasattr(sampler, "set_epoch"):
+        sampler.set_epoch(epoch)
+
+
 def train_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, optimizer: torch.optim.Optimizer,
-               lr_scheduler, device, *, max_grad_norm: Optional[float] = 1.0) -> Tuple[float, float]:
-    """One training epoch (reference GM/engine.py:9-79). Returns (train_loss, train_acc)."""
+               lr_scheduler, device, *, max_grad_norm: Optional[float] = 1.0,
+               epoch: Optional[int] = None) -> Tuple[float, float]:
+    """One training epoch (reference GM/engine.py:9-79). Returns (train_loss, train_acc).
+
+    ``epoch`` (optional) seeds a ``DistributedSampler``'s shuffle for this epoch."""
+    _set_sampler_epoch(dataloader, epoch)
     model.train()
     lf = _fused_loss(loss_fn)
     sums = torch.zeros(2, dtype=torch.float32, device=device)
@@ -117,15 +128,22 @@ def test_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, devi
 
 def train(model: torch.nn.Module, train_dataloader, test_dataloader, optimizer: torch.optim.Optimizer,
           loss_fn: torch.nn.Module, lr_scheduler, epochs: int, device, *, max_grad_norm: Optional[float] = 1.0,
-          checkpoint_dir: Optional[str] = None, metrics_path: Optional[str] = None) -> Dict[str, List]:
-    """Train and test for ``epochs`` epochs (reference GM/engine.py:132-211)."""
-    results = {"train_loss": [], "train_acc": [], "test_loss": [], "test_acc": []}
+          checkpoint_dir: Optional[str] = None, metrics_path: Optional[str] = None, start_epoch: int = 0,
+          results: Optional[Dict[str, List]] = None) -> Dict[str, List]:
+    """Train and test for ``epochs`` epochs (reference GM/engine.py:132-211).
+
+    Resume (new, optional): ``start_epoch`` epochs are already done (``load_checkpoint(...)["epoch"]``)
+    and ``results`` holds their metrics; only epochs ``start_epoch + 1 .. epochs`` run, numbered as
+    in the uninterrupted run, and their metrics are appended to ``results``."""
+    base = {"train_loss": [], "train_acc": [], "test_loss": [], "test_acc": []}
+    results = {k: list((results or {}).get(k, [])) for k in base}
     model.to(device)
-    it = tqdm(range(epochs)) if _rank0() else range(epochs)
+    epochs_left = range(start_epoch, epochs)
+    it = tqdm(epochs_left) if _rank0() else epochs_left
     for epoch in it:
         train_loss, train_acc = train_step(model=model, dataloader=train_dataloader, loss_fn=loss_fn,
                                            optimizer=optimizer, lr_scheduler=lr_scheduler, device=device,
-                                           max_grad_norm=max_grad_norm)
+                                           max_grad_norm=max_grad_norm, epoch=epoch)
         test_loss, test_acc = test_step(model=model, dataloader=test_dataloader, loss_fn=loss_fn, device=device)
         if _rank0():
             print(f"Epoch: {epoch + 1} | "

@@ -12,8 +12,12 @@ Recipe (the usual delayed-scaling scheme, all state on the device):
   * GEMMs run ``v_mfma_scale_f32_16x16x128_f8f6f4`` in the ping-pong kernel; the epilogue
     multiplies by ``dscale_a * dscale_b`` before bias / GELU / dropout / residual (csrc/gemm.hip).
 
-Forward GEMMs use e4m3 x e4m3; LayerNorm, softmax, attention, residual adds, the optimizer and the
-backward pass stay in bf16 / fp32 (fp8 dgrad e5m2 x e4m3 is available via ``linear_dgrad_fp8``).
+Forward GEMMs use e4m3 x e4m3. With ``dgrad=True`` (``ViT.enable_fp8``'s default) the four
+activation-gradient (dgrad) GEMMs of each encoder block also run in fp8: e5m2 gradients (own
+delayed-scaling slots) x e4m3 transposed weights (``linear_dgrad_fp8``). LayerNorm, softmax,
+attention, residual adds, the weight-gradient GEMMs and the optimizer stay in bf16 / fp32.
+Non-finite values: a NaN/Inf element makes its tensor's amax non-finite; the scale update then
+leaves that slot's history and scales unchanged (csrc/fp8.hip), and FusedAdam skips the step.
 """
 from __future__ import annotations
 
@@ -68,10 +72,11 @@ class Fp8State:
 
     ACT_PER_BLOCK = 4  # xn1 (qkv input), o (out-proj input), xn2 (fc1 input), h (fc2 input)
 
-    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0):
+    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0, dgrad: bool = True):
         self.act = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E4M3)
-        # e5m2 gradient slots for the fp8 dgrad GEMMs (PVR_FP8_DGRAD): dz2, dU, dx1, dQKV per block
+        # e5m2 gradient slots for the fp8 dgrad GEMMs (dgrad=True): dz2, dU, dx1, dQKV per block
         self.grad = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E5M2)
+        self.dgrad = bool(dgrad)
         self.n_blocks = n_blocks
         self._wmeta: Optional[Fp8Meta] = None
         self._wslot: Dict[int, int] = {}

@@ -35,8 +35,11 @@ _SIDE_B1_DB = os.environ.get("PVR_SIDE_B1_DB", "0") == "1"
 # queue each weight gradient on the side stream as soon as its operands exist (W2 before the fc2
 # dgrad, Wo before the attention backward) instead of in two batches behind later dgrad kernels
 EARLY_WGRAD = os.environ.get("PVR_EARLY_WGRAD", "0") == "1"  # A/B: slower (profiles/early_wgrad_ab.log)
-# fp8 mode: also run the four dgrad GEMMs in fp8 (e5m2 gradients x e4m3 W^T, delayed scaling)
-FP8_DGRAD = os.environ.get("PVR_FP8_DGRAD", "1") == "1"  # +5 % ViT-H/14 (profiles/fp8_dgrad_ab.log)
+
+
+# Test hook: called as DGRAD_TAP(which, output) after every encoder-block dgrad GEMM (which = 0 fc2,
+# 1 fc1, 2 out-proj, 3 qkv), so numerics checks can compare the dgrad outputs themselves.
+DGRAD_TAP = None
 
 
 def site_drop(seed: Optional[torch.Tensor], site: int, p: float, training: bool):
@@ -164,7 +167,9 @@ class EncoderBlockFn(torch.autograd.Function):
         if _use_micro(x, B, f8):
             return EncoderBlockFn._forward_micro(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, params)
         ctx.halves = None
-        ctx.f8d = f8 if FP8_DGRAD else None
+        # fp8 dgrad GEMMs (e5m2 gradients x e4m3 W^T) only if the model asked for them:
+        # ViT.enable_fp8(dgrad=True), the default (+5 % ViT-H/14, profiles/fp8_dgrad_ab.log)
+        ctx.f8d = f8 if f8 is not None and f8[0].dgrad else None
         M = w1.shape[0]
         scale = 1.0 / math.sqrt(D // H)
         u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
@@ -256,8 +261,12 @@ class EncoderBlockFn(torch.autograd.Function):
                 st, blk = f8d
                 gq, gs = st.grad_quant(dy, blk, which)
                 wq, ws = st.weight(wt, ~id(w), store.generation)
-                return F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum)
-            return gemm.linear_dgrad(dy, store.bf16(w), dgelu_aux=dgelu_aux, wt=wt, colsum=colsum)
+                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum)
+            else:
+                out = gemm.linear_dgrad(dy, store.bf16(w), dgelu_aux=dgelu_aux, wt=wt, colsum=colsum)
+            if DGRAD_TAP is not None:
+                DGRAD_TAP(which, out)
+            return out
 
         # ---- MLP branch: x2 = x1 + drop2(h . W2^T + b2),  h = drop1(gelu(u)),  u = xn2 . W1^T + b1
         if own is not None and own.done:

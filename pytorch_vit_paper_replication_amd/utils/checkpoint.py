@@ -79,8 +79,12 @@ def save_checkpoint(target_dir: str, model: torch.nn.Module, optimizer=None, lr_
 
 def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None, lr_scheduler=None, map_location="cpu",
                     restore_rng: bool = True) -> Dict[str, Any]:
-    """Restores state saved by ``save_checkpoint``; returns ``{"epoch", "results"}``."""
-    state = torch.load(path, map_location=map_location, weights_only=False)  # our own file (optimizer state)
+    """Restores state saved by ``save_checkpoint``; returns ``{"epoch", "results"}``.
+
+    The file is read with ``weights_only=True``: everything ``save_checkpoint`` writes (tensors,
+    dicts/lists of numbers, the optimizer and LR-scheduler state dicts, RNG byte tensors) loads
+    without unpickling arbitrary objects, so a ``--resume`` path cannot execute code."""
+    state = torch.load(path, map_location=map_location, weights_only=True)
     _unwrap(model).load_state_dict(state["model"])
     if optimizer is not None and "optimizer" in state:
         optimizer.load_state_dict(state["optimizer"])

@@ -9,7 +9,7 @@ from PIL import Image
 from pytorch_vit_paper_replication_amd.cli.train import main
 
 
-def test_cli_synthetic_vit(tmp_path):
+def test_cli_synthetic_vit(tmp_path, capsys):
     rc = main(["--model", "vit_tiny_test", "--synthetic", "--epochs", "1", "--batch-size", "4", "--image-size", "32",
                "--num-classes", "3", "--synthetic-train-len", "8", "--synthetic-test-len", "4",
                "--save-dir", str(tmp_path), "--save-name", "v.pth", "--checkpoint-dir", str(tmp_path / "ck"),
@@ -20,10 +20,14 @@ def test_cli_synthetic_vit(tmp_path):
     assert (tmp_path / "m.jsonl").exists()
     ck = sorted(os.listdir(tmp_path / "ck"))
     assert ck, "no checkpoint written"
-    rc = main(["--model", "vit_tiny_test", "--synthetic", "--epochs", "1", "--batch-size", "4", "--image-size", "32",
+    capsys.readouterr()
+    # --epochs is the total: the resumed run trains epoch 2 only, numbered 2
+    rc = main(["--model", "vit_tiny_test", "--synthetic", "--epochs", "2", "--batch-size", "4", "--image-size", "32",
                "--num-classes", "3", "--synthetic-train-len", "8", "--synthetic-test-len", "4",
                "--save-dir", str(tmp_path), "--save-name", "v2.pth", "--resume", str(tmp_path / "ck" / ck[-1])])
     assert rc == 0
+    out = capsys.readouterr().out
+    assert "Epoch: 2 |" in out and "Epoch: 1 |" not in out, out
 
 
 def test_cli_imagefolder_tinyvgg(tmp_path):

@@ -158,3 +158,68 @@ def test_vit_trains_end_to_end_on_cpu():
     sched = warmup_linear_decay(opt, 8 * len(tr))
     res = engine.train(m, tr, te, opt, nn.CrossEntropyLoss(), sched, epochs=8, device="cpu")
     assert res["train_loss"][-1] < res["train_loss"][0]
+
+
+def _resume_setup(seed=0):
+    from pytorch_vit_paper_replication_amd.data import create_synthetic_dataloaders
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
+
+    torch.manual_seed(seed)
+    tr, te, _ = create_synthetic_dataloaders(batch_size=4, train_len=16, test_len=4, image_size=32, num_classes=3)
+    m = ViT(image_size=32, patch_size=16, num_transformer_layer=1, num_heads=2, embedding_dim=32, mlp_size=64,
+            num_classes=3, mlp_dropout=0.0, embedding_dropout=0.0)
+    opt = FusedAdam(param_groups_weight_decay(m, 0.03), lr=3e-3)
+    sched = warmup_linear_decay(opt, 3 * len(tr), warmup_frac=0.25)
+    return m, tr, te, opt, sched
+
+
+def test_resume_continues_schedule_and_epochs(tmp_path):
+    """a resumed run trains only the remaining epochs on the restored LR schedule and ends
+    exactly where the uninterrupted run ends (LR, epoch numbering, metrics, weights)."""
+    m, tr, te, opt, sched = _resume_setup()
+    full = engine.train(m, tr, te, opt, nn.CrossEntropyLoss(), sched, epochs=3, device="cpu")
+    lr_full = opt.param_groups[0]["lr"]
+
+    m1, tr1, te1, opt1, sched1 = _resume_setup()
+    engine.train(m1, tr1, te1, opt1, nn.CrossEntropyLoss(), sched1, epochs=2, device="cpu",
+                 checkpoint_dir=str(tmp_path))
+    m2, tr2, te2, opt2, sched2 = _resume_setup(seed=123)  # different init: everything comes from the file
+    info = utils.load_checkpoint(str(tmp_path / "checkpoint.pt"), m2, opt2, sched2)
+    assert info["epoch"] == 2 and len(info["results"]["train_loss"]) == 2
+    res = engine.train(m2, tr2, te2, opt2, nn.CrossEntropyLoss(), sched2, epochs=3, device="cpu",
+                       start_epoch=info["epoch"], results=info["results"])
+    assert len(res["train_loss"]) == 3
+    assert sched2.last_epoch == sched.last_epoch == 3 * len(tr)
+    assert opt2.param_groups[0]["lr"] == pytest.approx(lr_full, abs=1e-12)
+    assert res["train_loss"][:2] == full["train_loss"][:2]
+    assert res["train_loss"][2] == pytest.approx(full["train_loss"][2], rel=1e-5)
+    for (k, a), b in zip(m.state_dict().items(), m2.state_dict().values()):
+        assert torch.allclose(a, b, atol=1e-6), k
+
+
+def test_checkpoint_loads_with_weights_only(tmp_path):
+    """load_checkpoint must not unpickle arbitrary objects (weights_only=True)."""
+    m, tr, te, opt, sched = _resume_setup()
+    engine.train_step(m, tr, nn.CrossEntropyLoss(), opt, sched, "cpu")
+    p = utils.save_checkpoint(str(tmp_path), m, opt, sched, epoch=1, results={"train_loss": [1.0]})
+    torch.load(p, weights_only=True)  # raises if anything in the file needs the unpickler
+
+
+def test_train_step_reshuffles_distributed_sampler():
+    """a DistributedSampler is re-seeded per epoch (set_epoch), as single-process shuffling is."""
+    from torch.utils.data.distributed import DistributedSampler
+
+    g = torch.Generator().manual_seed(0)
+    ds = TensorDataset(torch.randn(32, 4, generator=g), torch.randint(0, 3, (32,), generator=g))
+    sampler = DistributedSampler(ds, num_replicas=1, rank=0, shuffle=True)
+    dl = DataLoader(ds, batch_size=8, sampler=sampler)
+    m = Tiny()
+    opt = torch.optim.SGD(m.parameters(), lr=0.0)
+    sched = torch.optim.lr_scheduler.StepLR(opt, 1)
+    orders = []
+    for ep in range(2):
+        engine.train_step(m, dl, nn.CrossEntropyLoss(), opt, sched, "cpu", epoch=ep)
+        assert sampler.epoch == ep
+        orders.append(list(iter(sampler)))
+    assert orders[0] != orders[1]
