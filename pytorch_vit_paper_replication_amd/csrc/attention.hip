@@ -21,6 +21,7 @@
 // dS crosses LDS once for dQ = dS . K, which the waves split by output fragment, so dQ needs no
 // atomics when one workgroup holds every key (N <= 256).
 #include "common.h"
+#include <type_traits>
 
 namespace pvr {
 namespace {
@@ -104,6 +105,14 @@ PVR_DEV float dot8_bf16(const v8s& a, const v8s& b, float c) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_fdot2_f32_bf16(bf2{x[2 * j], x[2 * j + 1]}, bf2{y[2 * j], y[2 * j + 1]}, c, false);
   return c;
+}
+
+template <int I, int N, class F>
+PVR_DEV void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
 }
 
 PVR_DEV uint32_t clamp_bytes(int64_t b) { return b < 0 ? 0u : (b > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)b); }
@@ -1114,6 +1123,418 @@ __global__ void __launch_bounds__(256) attn_bwd_lastkey_kernel(const uint16_t* _
   }
 }
 
+// ------------------------------------------- backward, whole head, one pipelined kernel (dh 64)
+// 192 < N <= 256 (ViT-B/16 and ViT-L/16 at 224 px: N = 197). One persistent 4-wave workgroup per CU
+// (one wave per SIMD, 512 registers each: every operand and accumulator stays in registers) walks its
+// (batch, head) pairs; each pair is NQ = ceil(N / 32) blocks of 32 queries, and the blocks of
+// consecutive pairs form one stream. Wave w owns keys [64w, 64w + 64): their K / V fragments sit in
+// registers for the pair and dK^T / dV^T accumulate in registers over the pair's blocks (key
+// fragments entirely past N are skipped). Block t:
+//   phase 1 (t):   S = Q K^T, dP = dO V^T (query on the accumulator rows, key on the lane),
+//                  P = exp(S c - lse), dS = P (dP - delta); dV^T += dO^T P, dK^T += Q^T dS;
+//                  dS^T -> LDS ([key][query] image, ds_write_b64 per 16x16 fragment, 2 buffers).
+//   phase 2 (t-1): dQ^T = K^T dS^T of the PREVIOUS block: wave w owns dims 16w .. 16w + 15 of all 32
+//                  queries (two 16x16 fragments); the K^T fragments of its dims stay in registers.
+//   table (t+1):   lse * log2(e) and delta = rowsum(dO * O) of the NEXT block (8 queries per wave)
+//                  into a small LDS table, off phase 1's critical path.
+// One barrier per block. S and dP are computed once (the two-kernel backward computes them twice:
+// 10 instead of 14 MFMAs per 16x16 score tile), and each Q / dO fragment read from LDS feeds four
+// key fragments. LDS-DMA streams block t+3's Q / dO / O / lse rows (4-slot ring) and slices of the
+// NEXT pair's K / V images under block t: exactly 7 DMAs per wave per block, issued after the
+// block's stores, so one counted wait (vmcnt 7: only the newest group in flight) serves every block.
+template <int N>
+PVR_DEV void wait_barrier_lds0() { wait_barrier_lds<0>(); }
+#ifdef PVR_PIPE_SAFE
+#define PIPE_WAIT wait_barrier_lds0
+#else
+#define PIPE_WAIT wait_barrier_lds
+#endif
+#ifdef PVR_PRO_SAFE
+#define PRO_WAIT wait_barrier_lds0
+#else
+#define PRO_WAIT wait_barrier_lds
+#endif
+template <int NQ>
+__global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                                const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                                const uint16_t* __restrict__ o, int64_t ld_o,
+                                                                const float* __restrict__ lse, uint16_t* __restrict__ dqkv,
+                                                                int64_t ld_dq, int N, int H, int D, int npairs, float scale) {
+  static_assert(NQ == 7 || NQ == 8, "192 < N <= 256");
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  constexpr int DH = 64;
+  constexpr int NP = 32 * NQ;               // staged rows (queries / keys) per pair
+  constexpr int KR = 256;                   // key rows of the images: 4 waves x 64 keys
+  constexpr int IMG = KR * 128;             // K or V image: [256][128 B], swizzled (lds_off)
+  constexpr int SLOT = 3 * 4096 + 1024;     // ring slot: Q | dO | O rows of one block, lse DMA slot
+  constexpr int RING = 4;
+  constexpr int DSB = KR * 64;              // dS^T image [key][32 queries]
+  constexpr int NKV = NP / 4;               // 1 KiB pieces of one pair's K + V images
+  constexpr int NDMA = 7;                   // DMA instructions per wave per block
+  constexpr int NSTAGE = 13;                // 1 KiB pieces of one block: 4 Q + 4 dO + 4 O + lse
+  constexpr int KV_PER_IT = 4 * NDMA - 16;  // next-pair K/V pieces per block (slots 16 .. 27)
+  static_assert((NQ - 2) * KV_PER_IT >= NKV, "the next pair's K/V images must land two blocks before it starts");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + IMG;
+  char* ring = smem + 2 * IMG;
+  char* dsb = ring + RING * SLOT;
+  float* s_tab = (float*)(dsb + 2 * DSB);   // [2][64]: lse * log2e [32] | delta [32] of a block
+  char* sink = (char*)(s_tab + 128);        // 1 KiB target of the null DMAs that keep vmcnt uniform
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  PVR_ASSERT(blockDim.x == 256 && (N + 31) / 32 == NQ && (int)gridDim.x <= npairs);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
+  const int p0 = L * per + min(L, rem);
+  const int p1 = p0 + per + (L < rem ? 1 : 0);
+  if (p0 >= p1) return;
+  const int kw0 = wave * 64;
+  const int nf = min(4, max(0, (N - kw0 + 15) / 16));  // this wave's key fragments holding a key < N
+  const float c = scale * LOG2E;
+  const int64_t rows_all = (int64_t)(npairs / H) * N;
+  // one buffer resource per tensor (host check: every byte offset fits in 31 bits); rows past N and
+  // dropped stores use offset 0x80000000, outside every resource (zero-filled / dropped)
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv, clamp_bytes(((rows_all - 1) * ld + 3 * D) * 2));
+  const __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout, clamp_bytes(((rows_all - 1) * ld_do + D) * 2));
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(o, clamp_bytes(((rows_all - 1) * ld_o + D) * 2));
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(lse, clamp_bytes((int64_t)npairs * N * 4));
+  const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv, clamp_bytes(((rows_all - 1) * ld_dq + 3 * D) * 2));
+  constexpr uint32_t OOR = 0x80000000u;
+  const uint32_t ldq = (uint32_t)ld * 2, lddo = (uint32_t)ld_do * 2, ldoo = (uint32_t)ld_o * 2, lddq = (uint32_t)ld_dq * 2;
+
+  // ---- lane-dependent offsets, computed once
+  const int l3 = lane >> 3, l7 = lane & 7;
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+  // staging pieces: image row srl = 8 wave + l3 of a 32-row block (Q, dO, O: one piece each per wave)
+  const int srl = 8 * wave + l3;
+  const uint32_t sch = (uint32_t)((l7 ^ swz_a(srl)) << 4);
+  const uint32_t stq = (uint32_t)srl * ldq + sch, std_ = (uint32_t)srl * lddo + sch, sto = (uint32_t)srl * ldoo + sch;
+  // K/V piece rows rr + l3 (rr a multiple of 8): the swizzle term depends on rr's bit 3 only
+  const uint32_t kvo0 = (uint32_t)l3 * ldq + (uint32_t)((l7 ^ swz_a(l3)) << 4);
+  const uint32_t kvo1 = (uint32_t)l3 * ldq + (uint32_t)((l7 ^ swz_a(8 + l3)) << 4);
+  // A-operand rows (query 16a + li, dims 32ks + 8g ..): a adds 2048
+  const int fr0 = li * 128 + ((g ^ swz_a(li)) << 4);
+  const int fr1 = li * 128 + (((4 + g) ^ swz_a(li)) << 4);
+  // Q^T / dO^T transposed reads (rows 4g + q4, +16 -> +2048), dims 16e + 4p4
+  int trq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) trq[e] = (4 * g + q4) * 128 + (((2 * e + (p4 >> 1)) ^ swz_a(4 * g + q4)) << 4) + 8 * (p4 & 1);
+  // dS^T image [key][query]: 8-B unit u = query / 4 XOR-swizzled by (key >> 1) & 7 (conflict-free for
+  // the ds_write_b64 of a 16-key column and for the transposed reads); keys kw0 + 16f + li
+  auto ds_off = [](int key, int u) { return key * 64 + ((u ^ ((key >> 1) & 7)) << 3); };
+  const int dsw0 = ds_off(li, g) + kw0 * 64, dsw1 = ds_off(li, 4 + g) + kw0 * 64;  // a = 0 / 1; f adds 1024
+  // phase 2: dS^T rows 32ks + 8g + q4 (+4), queries 16a + 4p4 (a: unit + 4)
+  const int p2lo0 = ds_off(8 * g + q4, p4), p2hi0 = ds_off(8 * g + q4 + 4, p4);
+  const int p2lo1 = ds_off(8 * g + q4, 4 + p4), p2hi1 = ds_off(8 * g + q4 + 4, 4 + p4);
+  // next-block table: queries 8 wave + l3, dims 8 l7 .. 8 l7 + 7 (one 16-B chunk)
+  const int tq = 8 * wave + l3;
+  const int tbo = tq * 128 + ((l7 ^ swz_a(tq)) << 4);
+
+  struct PairOff {
+    uint32_t row, col;  // b * N, h * DH * 2 (bytes)
+  };
+  auto pair_off = [&](int pr) { return PairOff{(uint32_t)((pr / H) * N), (uint32_t)((pr % H) * DH * 2)}; };
+  auto dma = [&](__amdgpu_buffer_rsrc_t rs, char* img, uint32_t voff) { dma16(rs, to_lds(img), voff); };
+  // The counted vmcnt waits assume this wave's DMAs and stores issue in program order around each
+  // DMA group: keep the compiler from moving memory ops (or anything) across these points.
+  auto order_fence = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // the NDMA DMAs of this wave: slots 4i + wave. Slots 0..12 stage block sqb of pair `so` into ring
+  // slot `sl` (i = 0 / 1 / 2: Q / dO / O rows 8 wave ..; i = 3: lse for wave 0), slots 16.. carry K/V
+  // pieces [kvc * KV_PER_IT, ...) of pair `ko` if kvon; the rest load nothing into `sink`
+  // No DMA here ever reads out of range: a fully out-of-range load may complete ahead of older
+  // loads, and then a counted vmcnt wait passes with an older DMA still in flight. Rows past N are
+  // clamped to row N-1 (their queries get lse = +inf -> P = 0, their keys P = 0 by mask), and DMA
+  // slots without work reload a valid piece into `sink`.
+  auto issue_group = [&](bool stv, PairOff so, int sqb, int sl, bool kvon, int kvc, PairOff ko) {
+    const int r0 = 32 * sqb;
+    char* slot = ring + sl * SLOT;
+    const int row = min(r0 + srl, N - 1) - srl;  // block row r0 (clamped so that r0 + srl < N)
+    const uint32_t rb = so.row + (uint32_t)row;
+    dma(rq, slot + 8 * wave * 128, rb * ldq + so.col + stq);
+    dma(rdo, slot + 4096 + 8 * wave * 128, rb * lddo + so.col + std_);
+    dma(ro, slot + 8192 + 8 * wave * 128, rb * ldoo + so.col + sto);
+    if (wave == 0) {  // lse[(b*H + h)*N + r0 ..] with so.row = b*N, so.col = h*128 (lanes 8.. repeat lane 7)
+      const uint32_t lo = (so.row * (uint32_t)H + (so.col >> 7) * (uint32_t)N + (uint32_t)r0) * 4 + (uint32_t)min(lane, 7) * 16;
+      dma(rl, slot + 12288, lo);
+    } else {
+      dma(rq, sink, (uint32_t)lane * 16 + 3 * 1024);
+    }
+    // (the sink reloads use distinct addresses: identical DMA calls would be merged by the compiler,
+    // and a group one instruction short breaks the counted waits)
+#pragma unroll
+    for (int i = 4; i < NDMA; ++i) {
+      const int k = kvc * KV_PER_IT + 4 * (i - 4) + wave;
+      const bool live = kvon && k < NKV;
+      const int which = k >= NP / 8, rr = (k - which * (NP / 8)) * 8;
+      const int kr = min(rr + l3, N - 1) - l3;  // clamped key rows
+      const uint32_t base = (ko.row + kr) * ldq + (uint32_t)(which + 1) * D * 2 + ko.col;
+      dma(rq, live ? (which ? vimg : kimg) + rr * 128 : sink, live ? base + ((rr & 8) ? kvo1 : kvo0) : (uint32_t)lane * 16 + i * 1024);
+    }
+  };
+  // lse*log2e and delta of the block in ring slot `sl` (local block qb) into table buffer `tb`
+  auto block_table = [&](int sl, int qb, int tb) {
+    const char* sb = ring + sl * SLOT;
+    const v8s dw = ds_read_b128(sb + 4096 + tbo);
+    const v8s ow = ds_read_b128(sb + 8192 + tbo);
+    float d = dot8_bf16(dw, ow, 0.f);
+    d += __shfl_xor(d, 1, 64);
+    d += __shfl_xor(d, 2, 64);
+    d += __shfl_xor(d, 4, 64);
+    if (l7 == 0) {
+      const float l = ((const float*)(sb + 12288))[tq];
+      // queries past N (rows clamped to N-1): lse = +inf makes their P exactly 0
+      s_tab[tb * 64 + tq] = 32 * qb + tq < N ? l * LOG2E : __builtin_huge_valf();
+      s_tab[tb * 64 + 32 + tq] = d;
+    }
+  };
+  // dQ^T fragments (dims 16 wave + 4g + r, queries 16a + li) of a block from dS^T buffer `db`
+  auto phase2 = [&](int db, int pqb, PairOff po, const v8s (&ktf)[NQ]) {
+    const char* img = dsb + db * DSB;
+    v4f acc0 = v4f{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    constexpr int H1 = (NQ + 1) / 2;  // two batches of key slices: fewer registers in flight
+    static_for<0, 2>([&](auto hc) {
+      constexpr int k0 = decltype(hc)::value ? H1 : 0, k1 = decltype(hc)::value ? NQ : H1;
+      v4s lo0[H1], hi0[H1], lo1[H1], hi1[H1];
+      static_for<k0, k1>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        lo0[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2lo0);
+        hi0[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2hi0);
+        lo1[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2lo1);
+        hi1[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2hi1);
+      });
+      lds_wait();
+#pragma unroll
+      for (int ks = k0; ks < k1; ++ks) {
+        acc0 = mfma16(ktf[ks], cat44(lo0[ks - k0], hi0[ks - k0]), acc0);
+        acc1 = mfma16(ktf[ks], cat44(lo1[ks - k0], hi1[ks - k0]), acc1);
+      }
+    });
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const v4f& acc = a ? acc1 : acc0;
+      const int q = pqb * 32 + 16 * a + li;
+      const uint32_t vo = q < N ? (po.row + q) * lddq + po.col + (uint32_t)(16 * wave + 4 * g) * 2 : OOR;
+      const v2u w = {pack2bf(acc[0] * scale, acc[1] * scale), pack2bf(acc[2] * scale, acc[3] * scale)};
+      __builtin_amdgcn_raw_buffer_store_b64(w, rdq, vo, 0, 0);
+    }
+  };
+
+  v8s kf[4][2], vf[4][2], ktf[NQ];
+  v4f dk[4][4], dv[4][4];  // [dims e][key fragment f]
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
+  };
+  // 32 stores per wave (dropped past N)
+  auto store_dkv = [&](PairOff po) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int key = kw0 + 16 * f + li;
+      const uint32_t vo = key < N ? (po.row + key) * lddq + po.col + (uint32_t)(4 * g) * 2 : OOR;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const v2u wk = {pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale), pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale)};
+        const v2u wv = {pack2bf(dv[e][f][0], dv[e][f][1]), pack2bf(dv[e][f][2], dv[e][f][3])};
+        __builtin_amdgcn_raw_buffer_store_b64(wk, rdq, vo + (uint32_t)(D + 16 * e) * 2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(wv, rdq, vo + (uint32_t)(2 * D + 16 * e) * 2, 0, 0);
+      }
+    }
+  };
+  // this pair's K / V (S, dP B operands) and K^T (dQ A operand, dims 16 wave + li) fragments
+  auto load_kfrags = [&]() {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        kf[f][ks] = frag_rows(kimg, KR, kw0 + 16 * f, ks, lane);
+        vf[f][ks] = frag_rows(vimg, KR, kw0 + 16 * f, ks, lane);
+      }
+    // K^T rows 32ks + 8g + q4 (+4), dims 16 wave + 4p4: the swizzle depends on 8g + q4 -> offsets 4096 ks
+    const int chunk = 2 * wave + (p4 >> 1);
+    const char* alo = kimg + lds_off(KR, 8 * g + q4, chunk) + 8 * (p4 & 1);
+    const char* ahi = kimg + lds_off(KR, 8 * g + q4 + 4, chunk) + 8 * (p4 & 1);
+    v4s klo[NQ], khi[NQ];
+    static_for<0, NQ>([&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      klo[ks] = ds_read_tr_async_at<4096 * ks>(alo);
+      khi[ks] = ds_read_tr_async_at<4096 * ks>(ahi);
+    });
+    lds_wait();
+#pragma unroll
+    for (int ks = 0; ks < NQ; ++ks) ktf[ks] = cat44(klo[ks], khi[ks]);
+  };
+
+  // ---- prologue: image rows NP .. 255 (never staged) zeroed once, so key fragments past N compute
+  // on finite zeros; pair p0's K/V images; blocks 0, 1, 2; table of block 0
+  if constexpr (NP < KR) {
+    for (int i = threadIdx.x; i < 2 * (KR - NP) * 8; i += 256) {
+      const int r = NP + (i >> 3) % (KR - NP);
+      char* img = i < 8 * (KR - NP) ? kimg : vimg;
+      *(uint4*)(img + r * 128 + (i & 7) * 16) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  const PairOff none{0u, 0u};
+  PairOff cur = pair_off(p0);
+  for (int k = wave; k < NKV; k += 4) {
+    const int which = k >= NP / 8, rr = (k - which * (NP / 8)) * 8;
+    const int kr = min(rr + l3, N - 1) - l3;
+    const uint32_t base = (cur.row + kr) * ldq + (uint32_t)(which + 1) * D * 2 + cur.col;
+    dma(rq, (which ? vimg : kimg) + rr * 128, base + ((rr & 8) ? kvo1 : kvo0));
+  }
+  issue_group(true, cur, 0, 0, false, 0, none);
+  issue_group(true, cur, 1, 1, false, 0, none);
+  issue_group(true, cur, 2, 2, false, 0, none);
+  zero_acc();
+  PRO_WAIT<2 * NDMA>();  // K/V images and block 0 landed (blocks 1, 2 in flight)
+  block_table(0, 0, 0);
+  PRO_WAIT<NDMA>();      // block 1 landed; block 0's table visible
+
+  const int npr = p1 - p0;
+  PairOff prv = cur;
+  for (int pi = 0; pi < npr; ++pi) {
+    cur = pair_off(p0 + pi);
+    const bool has_next = pi + 1 < npr;
+    const PairOff nxt = has_next ? pair_off(p0 + pi + 1) : none;
+    const int t0 = pi * NQ;
+#pragma unroll 1
+    for (int qb = 0; qb < NQ; ++qb) {
+      const int t = t0 + qb;
+      // Blocks t, t+1 landed: the DMA groups up to t-2 are complete (group j stages block j+3) and
+      // only group t-1 may be in flight. Stores are always issued BEFORE a group, so the NDMA
+      // youngest vector-memory ops are that group's loads: loads complete in order, stores need not
+      // (gfx9 counts both in vmcnt), so a count that covered younger stores could pass early. Also:
+      // dS^T and table of block t visible; every wave past its reads of the reused buffers.
+      if (t > 0) PIPE_WAIT<NDMA>();
+      const int sl = t & (RING - 1);
+      const char* qimg = ring + sl * SLOT;
+      const char* doimg = qimg + 4096;
+      if (qb == 0) {
+        // phase 2 of the previous pair's last block BEFORE its K^T fragments are replaced (dropped
+        // stores at t = 0 keep the store count uniform)
+        if (pi > 0) phase2((t - 1) & 1, NQ - 1, prv, ktf);
+        order_fence();
+        load_kfrags();
+      }
+      // ---- phase 1a: Q / dO A fragments (query 16a + li, dims 32ks + 8g ..), reused by all four key
+      // fragments; this block's Q^T / dO^T transposed fragments for the dV / dK products
+      v8s qa[2][2], dA[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int fo = (ks ? fr1 : fr0) + 2048 * a;
+          qa[ks][a] = ds_read_b128(qimg + fo);
+          dA[ks][a] = ds_read_b128(doimg + fo);
+        }
+      // S[q][key], dP[q][key] of key fragments 0, 1 (lane holds [q = 16a + 4g + r][key = kw0 + 16f + li])
+      v4f s[2][2], dp[2][2];
+      auto sdp = [&](int f0) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int f = 0; f < 2; ++f) s[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              s[a][f] = mfma16(qa[ks][a], kf[f0 + f][ks], s[a][f]);
+              dp[a][f] = mfma16(dA[ks][a], vf[f0 + f][ks], dp[a][f]);
+            }
+      };
+      sdp(0);
+      // ---- pair end: the previous pair's dK / dV (its last block's products ran in iteration t-1)
+      order_fence();
+      if (qb == 0 && pi > 0) {
+        store_dkv(prv);
+        zero_acc();
+      }
+      // ---- phase 2 of block t-1 (same pair): its stores precede this iteration's DMA group
+      if (qb != 0) phase2((t - 1) & 1, qb - 1, cur, ktf);
+      // ---- DMA: block t+3 and, in local blocks 1 .. NQ-2, slices of the next pair's K/V images
+      order_fence();
+      const bool kvon = qb >= 1 && qb <= NQ - 2 && has_next;
+      if (qb + 3 < NQ)
+        issue_group(true, cur, qb + 3, (t + 3) & (RING - 1), kvon, qb - 1, nxt);
+      else
+        issue_group(has_next, nxt, qb + 3 - NQ, (t + 3) & (RING - 1), kvon, qb - 1, nxt);
+      order_fence();
+      // ---- table of block t+1 (landed at this iteration's wait)
+      if (qb + 1 < NQ)
+        block_table((t + 1) & (RING - 1), qb + 1, (t + 1) & 1);
+      else if (has_next)
+        block_table((t + 1) & (RING - 1), 0, (t + 1) & 1);
+      // ---- phase 1b: P, dS; dS^T -> LDS; dV^T += dO^T P, dK^T += Q^T dS (key fragments in pairs)
+      const float* tl = s_tab + (t & 1) * 64 + 4 * g;
+      const v4f l40 = *(const v4f*)(tl), l41 = *(const v4f*)(tl + 16);
+      const v4f d40 = *(const v4f*)(tl + 32), d41 = *(const v4f*)(tl + 48);
+      char* img = dsb + (t & 1) * DSB;
+      v4s dlo[4], dhi[4], qlo[4], qhi[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dlo[e] = ds_read_tr_async(doimg + trq[e]);
+        dhi[e] = ds_read_tr_async(doimg + trq[e] + 2048);
+        qlo[e] = ds_read_tr_async(qimg + trq[e]);
+        qhi[e] = ds_read_tr_async(qimg + trq[e] + 2048);
+      }
+      lds_wait();
+      auto softmax_grad = [&](int f0) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const int fk = f0 + f;
+          const bool kin = kw0 + 16 * fk + li < N;
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const v4f l4 = a ? l41 : l40, d4 = a ? d41 : d40;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float pv = kin ? __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l4[r])) : 0.f;
+              s[a][f][r] = pv;
+              dp[a][f][r] = pv * (dp[a][f][r] - d4[r]);
+            }
+            const v2u w = {pack2bf(dp[a][f][0], dp[a][f][1]), pack2bf(dp[a][f][2], dp[a][f][3])};
+            *(v2u*)(img + (a ? dsw1 : dsw0) + 1024 * fk) = w;
+          }
+          const v8s pf = pack_p(s[0][f], s[1][f]);
+          const v8s sf = pack_p(dp[0][f], dp[1][f]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            dv[e][fk] = mfma16(cat44(dlo[e], dhi[e]), pf, dv[e][fk]);
+            dk[e][fk] = mfma16(cat44(qlo[e], qhi[e]), sf, dk[e][fk]);
+          }
+        }
+      };
+      softmax_grad(0);
+      if (nf > 2) {  // key fragments 2, 3 (wave 3 at N = 197 holds no key there: zero dS^T rows instead)
+        sdp(2);
+        softmax_grad(2);
+      } else {
+#pragma unroll
+        for (int f = 2; f < 4; ++f)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) *(v2u*)(img + (a ? dsw1 : dsw0) + 1024 * f) = v2u{0u, 0u};
+      }
+    }
+    prv = cur;
+  }
+  // last block's dQ and the last pair's dK / dV
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  phase2((npr * NQ - 1) & 1, NQ - 1, prv, ktf);
+  store_dkv(prv);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
 __global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
                                                           int64_t rows, int D) {
   const int64_t n = rows * D;
@@ -1333,11 +1754,54 @@ static hipError_t attn_bwd_head(const uint16_t* qkv, int64_t ld, const uint16_t*
   return hipErrorInvalidValue;
 }
 
+// PVR_ATTN_BWD_PIPE=0: the two-kernel whole-head backward instead of the pipelined one (A/B switch)
+static bool bwd_pipe_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PVR_ATTN_BWD_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int NQ>
+static hipError_t attn_bwd_pipe_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                       int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, int B, int N, int H, int D,
+                                       float scale, hipStream_t s) {
+  using namespace pvr;
+  constexpr int SMEM = 2 * 256 * 128 + 4 * (3 * 4096 + 1024) + 2 * 256 * 64 + 512 + 1024;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_pipe_kernel<NQ>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int npairs = B * H;
+  const int grid = npairs < device_cus() ? npairs : device_cus();
+  hipLaunchKernelGGL(attn_bwd_pipe_kernel<NQ>, dim3(grid), dim3(256), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq, N, H,
+                     D, npairs, scale);
+  return hipGetLastError();
+}
+
+// pipelined whole-head backward: dh 64, 192 < N <= 256
+static hipError_t attn_bwd_pipe(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout, int64_t ld_do,
+                                const float* lse, uint16_t* dqkv, int64_t ld_dq, int B, int N, int H, int D, float scale, hipStream_t s) {
+  switch ((N + 31) / 32) {
+    case 7: return attn_bwd_pipe_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, B, N, H, D, scale, s);
+    case 8: return attn_bwd_pipe_launch<8>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, B, N, H, D, scale, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                   float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
+  const int64_t rows_all = (int64_t)B * N;
+  const bool off31 = ((rows_all - 1) * std::max(std::max(ld, ld_do), std::max(ld_o, ld_dq)) + 3 * D) * 2 < (1ll << 31) &&
+                     (int64_t)B * H * N * 4 < (1ll << 31);
+  if (DH == 64 && N > 192 && N <= 256 && !dbias && off31 && !bwd_fused_forced() && bwd_pipe_enabled())
+    return attn_bwd_pipe(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, B, N, H, D, scale, s);
   if (DH == 64 && N <= 256 && !dbias && delta && !bwd_fused_forced())
     return attn_bwd_head(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, B, N, H, D, scale, s);
   const int NW = pvr_attn_bwd_waves(N);

@@ -43,8 +43,12 @@ PVR_DEV uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
 }
+// Two f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (the scalar-cast form costs two conversions,
+// a shift and an SDWA or: 4 VALU per pair in every epilogue).
 PVR_DEV uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((v2f){a, b}, v2bf));
 }
 
 // 16x16x32 bf16 MFMA: D = A(16x32) * B(32x16) + C.
@@ -82,12 +86,46 @@ PVR_DEV v4s ds_read_tr_async(const void* lds_ptr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
   return r;
 }
+// ds_read_tr_async at a compile-time byte offset from `lds_ptr` (one address VGPR for a whole
+// unrolled sweep of reads OFF apart).
+template <int OFF>
+PVR_DEV v4s ds_read_tr_async_at(const void* lds_ptr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset is 16 bits");
+  v4s r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_ptr;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+// Lane id recomputed where it is used (volatile: not hoisted out of loops and kept live, which at
+// high register pressure gets it spilled and reloaded behind an s_waitcnt vmcnt(0))
+PVR_DEV int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 // Wait for every outstanding LDS read (including ds_read_tr_async) and keep the compiler from
 // scheduling their consumers above the wait (an MFMA has no memory operand, so the asm's "memory"
 // clobber alone does not order it).
 PVR_DEV void lds_wait() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// Wait until at most N of this wave's vector-memory ops (LDS-DMA, loads, stores) are outstanding,
+// then barrier. The asm "memory" clobbers keep the compiler from moving LDS accesses across it.
+template <int N>
+PVR_DEV void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// Same, and also retire this wave's outstanding LDS reads/writes (their slot is refilled, or their
+// data read by other waves, after the barrier).
+template <int N>
+PVR_DEV void wait_barrier_lds() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 PVR_DEV v8s ds_read_b128(const void* lds_ptr) {

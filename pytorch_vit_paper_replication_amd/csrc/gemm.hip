@@ -445,21 +445,6 @@ PVR_DEV v8s frag32(const char* lds, int r0, int lane) {
   }
 }
 
-// Wait until at most N of this wave's vector-memory ops (LDS-DMA) are outstanding, then barrier.
-// The asm "memory" clobbers keep the compiler from moving LDS accesses across the barrier.
-template <int N>
-PVR_DEV void wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-// Same, and also retire this wave's outstanding LDS reads (their slot is refilled after the barrier).
-template <int N>
-PVR_DEV void wait_barrier_lds() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 template <int BM, int BN, int WM, int WN, int STAGES, bool AK, bool BKC, bool SWAP, int EPI>
 __global__ void __launch_bounds__(WM* WN * 64) gemm_ms_kernel(GemmParams p) {

@@ -1,4 +1,6 @@
-"""Run the attention kernels at ViT-B/16 b256 shapes a few times (for rocprofv3 counter collection)."""
+"""Run the attention kernels at ViT-B/16 b256 shapes a few times (for rocprofv3 counter collection).
+
+usage: attn_probe.py [fwd|bwd|both]   (PVR_ATTN_BWD_PIPE=0 selects the two-kernel backward)"""
 import os
 import sys
 
@@ -7,13 +9,16 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
 
+which = sys.argv[1] if len(sys.argv) > 1 else "both"
 ext = _ext.ext()
 B, N, H, D = 256, 197, 12, 768
 qkv = torch.randn(B * N, 3 * D, device="cuda", dtype=torch.bfloat16)
 o, lse = ext.attn_fwd(qkv, B, N, H, 0.125)
 do = torch.randn_like(o)
 for _ in range(3):
-    ext.attn_fwd(qkv, B, N, H, 0.125)
-    ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125)
+    if which in ("fwd", "both"):
+        ext.attn_fwd(qkv, B, N, H, 0.125)
+    if which in ("bwd", "both"):
+        ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125)
 torch.cuda.synchronize()
 print("ok")
