@@ -1159,7 +1159,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
                                                                 const uint16_t* __restrict__ dout, int64_t ld_do,
                                                                 const uint16_t* __restrict__ o, int64_t ld_o,
                                                                 const float* __restrict__ lse, uint16_t* __restrict__ dqkv,
-                                                                int64_t ld_dq, int N, int H, int D, int npairs, float scale) {
+                                                                int64_t ld_dq, float* __restrict__ dbp, int N, int H, int D,
+                                                                int npairs, float scale) {
   static_assert(NQ == 7 || NQ == 8, "192 < N <= 256");
   typedef unsigned int v2u __attribute__((ext_vector_type(2)));
   constexpr int DH = 64;
@@ -1180,7 +1181,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
   char* ring = smem + 2 * IMG;
   char* dsb = ring + RING * SLOT;
   float* s_tab = (float*)(dsb + 2 * DSB);   // [2][64]: lse * log2e [32] | delta [32] of a block
-  char* sink = (char*)(s_tab + 128);        // 1 KiB target of the null DMAs that keep vmcnt uniform
+  float* vsb = s_tab + 128;                  // [64]: dV-bias partial of the last block (wave 0 only)
+  char* sink = (char*)(vsb + 64);           // 1 KiB target of the null DMAs that keep vmcnt uniform
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1282,10 +1284,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
     const char* sb = ring + sl * SLOT;
     const v8s dw = ds_read_b128(sb + 4096 + tbo);
     const v8s ow = ds_read_b128(sb + 8192 + tbo);
-    float d = dot8_bf16(dw, ow, 0.f);
-    d += __shfl_xor(d, 1, 64);
-    d += __shfl_xor(d, 2, 64);
-    d += __shfl_xor(d, 4, 64);
+    const float d = oct_sum(dot8_bf16(dw, ow, 0.f));
     if (l7 == 0) {
       const float l = ((const float*)(sb + 12288))[tq];
       // queries past N (rows clamped to N-1): lse = +inf makes their P exactly 0
@@ -1293,8 +1292,10 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
       s_tab[tb * 64 + 32 + tq] = d;
     }
   };
-  // dQ^T fragments (dims 16 wave + 4g + r, queries 16a + li) of a block from dS^T buffer `db`
-  auto phase2 = [&](int db, int pqb, PairOff po, const v8s (&ktf)[NQ]) {
+  // dQ^T fragments (dims 16 wave + 4g + r, queries 16a + li) of a block (local pqb of pair index ppair)
+  // from dS^T buffer `db`; with dbp, the block's in_proj bias-gradient partials (all stores of a
+  // block precede its DMA group)
+  auto phase2 = [&](int db, int pqb, PairOff po, int ppair, const v8s (&ktf)[NQ]) {
     const char* img = dsb + db * DSB;
     v4f acc0 = v4f{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
     constexpr int H1 = (NQ + 1) / 2;  // two batches of key slices: fewer registers in flight
@@ -1322,6 +1323,16 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
       const uint32_t vo = q < N ? (po.row + q) * lddq + po.col + (uint32_t)(16 * wave + 4 * g) * 2 : OOR;
       const v2u w = {pack2bf(acc[0] * scale, acc[1] * scale), pack2bf(acc[2] * scale, acc[3] * scale)};
       __builtin_amdgcn_raw_buffer_store_b64(w, rdq, vo, 0, 0);
+    }
+    if (dbp) {
+      // q: column sums of this block's dQ (queries past N have dS = 0, so dQ = 0 exactly);
+      // v: wave 0's column sums of dO over the block's valid queries (vsb, from its phase 1b)
+      float* dst = dbp + ((int64_t)ppair * NQ + pqb) * 128;
+      float cs[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[r] = row16_sum(acc0[r] + acc1[r]) * scale;
+      if (li == 0) *(float4*)(dst + 16 * wave + 4 * g) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      if (wave == 0) dst[64 + lane] = vsb[lane];
     }
   };
 
@@ -1419,7 +1430,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
       if (qb == 0) {
         // phase 2 of the previous pair's last block BEFORE its K^T fragments are replaced (dropped
         // stores at t = 0 keep the store count uniform)
-        if (pi > 0) phase2((t - 1) & 1, NQ - 1, prv, ktf);
+        if (pi > 0) phase2((t - 1) & 1, NQ - 1, prv, p0 + pi - 1, ktf);
         order_fence();
         load_kfrags();
       }
@@ -1459,7 +1470,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
         zero_acc();
       }
       // ---- phase 2 of block t-1 (same pair): its stores precede this iteration's DMA group
-      if (qb != 0) phase2((t - 1) & 1, qb - 1, cur, ktf);
+      if (qb != 0) phase2((t - 1) & 1, qb - 1, cur, p0 + pi, ktf);
       // ---- DMA: block t+3 and, in local blocks 1 .. NQ-2, slices of the next pair's K/V images
       order_fence();
       const bool kvon = qb >= 1 && qb <= NQ - 2 && has_next;
@@ -1523,6 +1534,22 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
 #pragma unroll
           for (int a = 0; a < 2; ++a) *(v2u*)(img + (a ? dsw1 : dsw0) + 1024 * f) = v2u{0u, 0u};
       }
+      if (dbp && wave == 0) {
+        // v-bias partial: dO^T . 1 over the block's queries < N (the dV^T product with P -> a 0/1 mask;
+        // the in_proj k bias gets no gradient: softmax rows are shift-invariant, so sum_k dS = 0)
+        v4f m0, m1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          m0[r] = 32 * qb + 4 * g + r < N ? 1.f : 0.f;
+          m1[r] = 32 * qb + 16 + 4 * g + r < N ? 1.f : 0.f;
+        }
+        const v8s ones = pack_p(m0, m1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const v4f cs = mfma16(cat44(dlo[e], dhi[e]), ones, v4f{0.f, 0.f, 0.f, 0.f});
+          if (li == 0) *(v4f*)(vsb + 16 * e + 4 * g) = cs;
+        }
+      }
     }
     prv = cur;
   }
@@ -1530,7 +1557,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  phase2((npr * NQ - 1) & 1, NQ - 1, prv, ktf);
+  phase2((npr * NQ - 1) & 1, NQ - 1, prv, p1 - 1, ktf);
   store_dkv(prv);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
@@ -1765,10 +1792,10 @@ static bool bwd_pipe_enabled() {
 
 template <int NQ>
 static hipError_t attn_bwd_pipe_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                       int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, int B, int N, int H, int D,
-                                       float scale, hipStream_t s) {
+                                       int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dbp, int B, int N, int H,
+                                       int D, float scale, hipStream_t s) {
   using namespace pvr;
-  constexpr int SMEM = 2 * 256 * 128 + 4 * (3 * 4096 + 1024) + 2 * 256 * 64 + 512 + 1024;
+  constexpr int SMEM = 2 * 256 * 128 + 4 * (3 * 4096 + 1024) + 2 * 256 * 64 + 512 + 256 + 1024;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_pipe_kernel<NQ>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -1777,19 +1804,28 @@ static hipError_t attn_bwd_pipe_launch(const uint16_t* qkv, int64_t ld, const ui
   }
   const int npairs = B * H;
   const int grid = npairs < device_cus() ? npairs : device_cus();
-  hipLaunchKernelGGL(attn_bwd_pipe_kernel<NQ>, dim3(grid), dim3(256), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq, N, H,
-                     D, npairs, scale);
+  hipLaunchKernelGGL(attn_bwd_pipe_kernel<NQ>, dim3(grid), dim3(256), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq, dbp, N,
+                     H, D, npairs, scale);
   return hipGetLastError();
 }
 
 // pipelined whole-head backward: dh 64, 192 < N <= 256
 static hipError_t attn_bwd_pipe(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout, int64_t ld_do,
-                                const float* lse, uint16_t* dqkv, int64_t ld_dq, int B, int N, int H, int D, float scale, hipStream_t s) {
+                                const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dbp, int B, int N, int H, int D, float scale,
+                                hipStream_t s) {
   switch ((N + 31) / 32) {
-    case 7: return attn_bwd_pipe_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, B, N, H, D, scale, s);
-    case 8: return attn_bwd_pipe_launch<8>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, B, N, H, D, scale, s);
+    case 7: return attn_bwd_pipe_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
+    case 8: return attn_bwd_pipe_launch<8>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// the pipelined backward serves this shape / these layouts (dh 64, 192 < N <= 256, 31-bit offsets)
+static bool attn_bwd_pipe_ok(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq) {
+  const int64_t rows_all = (int64_t)B * N;
+  const bool off31 = ((rows_all - 1) * std::max(std::max(ld, ld_do), std::max(ld_o, ld_dq)) + 3 * D) * 2 < (1ll << 31) &&
+                     (int64_t)B * H * N * 4 < (1ll << 31);
+  return H > 0 && D == 64 * H && N > 192 && N <= 256 && off31 && !bwd_fused_forced() && bwd_pipe_enabled();
 }
 
 template <int DH>
@@ -1797,11 +1833,8 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                   float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
-  const int64_t rows_all = (int64_t)B * N;
-  const bool off31 = ((rows_all - 1) * std::max(std::max(ld, ld_do), std::max(ld_o, ld_dq)) + 3 * D) * 2 < (1ll << 31) &&
-                     (int64_t)B * H * N * 4 < (1ll << 31);
-  if (DH == 64 && N > 192 && N <= 256 && !dbias && off31 && !bwd_fused_forced() && bwd_pipe_enabled())
-    return attn_bwd_pipe(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, B, N, H, D, scale, s);
+  if (DH == 64 && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][128] partials
+    return attn_bwd_pipe(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
   if (DH == 64 && N <= 256 && !dbias && delta && !bwd_fused_forced())
     return attn_bwd_head(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, B, N, H, D, scale, s);
   const int NW = pvr_attn_bwd_waves(N);
@@ -1858,9 +1891,18 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   return hipGetLastError();
 }
 
+// 1 if pvr_attn_bwd takes the pipelined whole-head backward for this shape and these layouts; its
+// dbias is then f32 [B*H][ceil(N/32)][128] partials instead: per (batch, head, 32-query block) the
+// column sums of dQ (64, the head's q-bias slice) and of dO (64: the v-bias slice, sum_k dV = sum_q dO
+// since softmax rows sum to 1); the k-bias gradient is exactly 0 (sum_k dS = 0 per query)
+extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq) {
+  return attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq) ? 1 : 0;
+}
+
 // dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
 // dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
-// every element is written), whose row sum is the in_proj bias gradient.
+// every element is written), whose row sum is the in_proj bias gradient; on the pipelined path
+// (pvr_attn_bwd_uses_pipe) the per-block partials described there.
 // delta: optional f32 [B*H][N] workspace; with it, dh 64 and N <= 256 take the two-kernel
 // whole-head backward (which does not fuse the bias gradient: dbias forces the single kernel).
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,

@@ -42,6 +42,7 @@ hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const fl
 int pvr_attn_bwd_key_blocks(int);
 int pvr_attn_bwd_needs_dq_acc(int, int, int);
 int pvr_attn_bwd_waves(int);
+int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, float*, int, int, int, int, float, hipStream_t);
 }
@@ -399,8 +400,26 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int
   return {out, lse};
 }
 
+// dbias[3D] += the in_proj bias gradient from the pipelined backward's [B*H][NQ][128] partials
+// (per query block: dQ column sums | dO column sums; the k slice gets no gradient)
+void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor dbias) {
+  TORCH_CHECK(part.is_contiguous() && part.numel() % (B * H * 128) == 0, "attn_dbias_reduce: [B*H][NQ][128] partials");
+  auto r = part.view({B, H, -1, 2, 64}).sum(at::IntArrayRef{0, 2});  // [H][2][64]
+  auto db = dbias.view({3, H, 64});
+  db.select(0, 0).add_(r.select(1, 0));
+  db.select(0, 2).add_(r.select(1, 1));
+}
+
+// pipelined backward taken for the standard layouts of this shape (qkv [T][3D], dO / O [T][D])
+bool attn_bwd_pipe_path(int64_t B, int64_t N, int64_t H, int64_t D) {
+  return pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D) != 0;
+}
+
+// dbias: [3D] f32 accumulated with the in_proj bias gradient. dbias_part (pipelined path only,
+// [B*H][ceil(N/32)][128] f32): receives the kernel's per-block partials instead, left unreduced (the
+// caller reduces them, e.g. on the weight-gradient side stream: attn_dbias_reduce).
 torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
-                       double scale, c10::optional<torch::Tensor> dbias) {
+                       double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
   auto delta = torch::empty_like(lse);  // rowsum(dO * O) workspace of the two-kernel backward
@@ -411,10 +430,22 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
   torch::Tensor dbias_part;
   const bool want_db = dbias.has_value() && dbias->defined();
+  const bool pipe = pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, ld_of(qkv, "qkv"), ld_of(dout, "dout"), ld_of(out, "out"),
+                                           ld_of(dqkv, "dqkv")) != 0;
+  const bool part_out = dbias_part_out.has_value() && dbias_part_out->defined();
+  if (part_out) {
+    TORCH_CHECK(pipe && !want_db, "dbias_part: pipelined backward only, and not together with dbias");
+    TORCH_CHECK(dbias_part_out->is_cuda() && dbias_part_out->scalar_type() == torch::kFloat32 && dbias_part_out->is_contiguous() &&
+                    dbias_part_out->numel() == B * H * ((N + 31) / 32) * 128,
+                "dbias_part [B*H][ceil(N/32)][128] f32");
+    dbias_part = *dbias_part_out;
+  }
   if (want_db) {
     TORCH_CHECK(dbias->numel() == 3 * D && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous(), "dbias [3D] f32");
     const int dh = (int)(D / H);
-    if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
+    if (pipe)  // per-(batch, head, query block) partials written by the pipelined backward: q 64 | v 64
+      dbias_part = torch::empty({B * H, (N + 31) / 32, 128}, qkv.options().dtype(torch::kFloat32));
+    else if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
       dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
   check(pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"), ld_of(dout, "dout"),
@@ -424,7 +455,9 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
                      (float)scale, stream()),
         "attn_bwd");
   if (want_db) {
-    if (dbias_part.defined())
+    if (pipe)
+      attn_dbias_reduce(dbias_part, B, H, *dbias);
+    else if (dbias_part.defined())
       dbias->add_(dbias_part.sum(0));
     else
       dbias->add_(dqkv.sum(0, false, torch::kFloat32));
@@ -458,6 +491,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none(),
         py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("attn_bwd_pipe_path", &attn_bwd_pipe_path);
+  m.def("attn_dbias_reduce", &attn_dbias_reduce);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("transpose_batched", &transpose_batched);
   m.def("colsum", &colsum);
@@ -479,6 +514,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_scale_update", &fp8_scale_update);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
-        py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none());
+        py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none());
   m.def("arch", []() { return std::string("gfx950"); });
 }

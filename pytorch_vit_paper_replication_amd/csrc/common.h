@@ -103,6 +103,28 @@ PVR_DEV int lane_here() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
+// Cross-lane sums on DPP (register-to-register lane moves inside a 16-lane row): a constant-offset
+// __shfl_xor lowers to ds_bpermute, an LDS round trip per step. dpp_mov<CTRL>: the lane value
+// selected by the DPP control (quad_perm 0x00-0xFF, row_ror:n 0x120+n, row_half_mirror 0x141).
+template <int CTRL>
+PVR_DEV float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// sum over the 16 lanes of each row (every lane of the row receives it)
+PVR_DEV float row16_sum(float v) {
+  v += dpp_mov<0x128>(v);  // row_ror:8
+  v += dpp_mov<0x124>(v);  // row_ror:4
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  return v;
+}
+// sum over each aligned group of 8 lanes (every lane of the group receives it)
+PVR_DEV float oct_sum(float v) {
+  v += dpp_mov<0x141>(v);  // row_half_mirror: lane i + lane 7 - i within each 8
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0xB1>(v);
+  return v;
+}
 // Wait for every outstanding LDS read (including ds_read_tr_async) and keep the compiler from
 // scheduling their consumers above the wait (an MFMA has no memory operand, so the asm's "memory"
 // clobber alone does not order it).

@@ -28,6 +28,8 @@ SITE_SHIFT = 32
 # in_proj bias gradient inside the attention backward: correct, but A/B-measured 0.35 ms/step slower than
 # the separate column-sum kernel on ViT-B/16 b256, so opt-in
 _FUSE_QKV_DBIAS = os.environ.get("PVR_ATTN_DBIAS", "0") == "1"
+# in_proj bias gradient from the pipelined attention backward's partial sums (PVR_PIPE_QKV_DB=0: column-sum pass, A/B)
+_PIPE_QKV_DB = os.environ.get("PVR_PIPE_QKV_DB", "1") == "1"
 # in_proj bias gradient on the weight-gradient side stream (PVR_SIDE_QKV_DB=0: on the dgrad chain, A/B)
 _SIDE_QKV_DB = os.environ.get("PVR_SIDE_QKV_DB", "1") == "1"
 # fc1 bias gradient as a side-stream column sum instead of inside the dGELU GEMM epilogue (A/B)
@@ -311,7 +313,14 @@ class EncoderBlockFn(torch.autograd.Function):
         # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
         gbqkv = g(bqkv)
         side_db = False
-        if _FUSE_QKV_DBIAS:
+        db_part = None
+        if gbqkv is not None and _PIPE_QKV_DB and ext.attn_bwd_pipe_path(B, N, H, D):
+            # the pipelined attention backward emits per-(image, head, query block) column sums of dQ and
+            # dO (= the v-bias gradient; the k bias has none); only their small reduction remains (side
+            # stream), no pass over dQKV
+            db_part = torch.empty(B * H, (N + 31) // 32, 128, dtype=torch.float32, device=do.device)
+            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part)
+        elif _FUSE_QKV_DBIAS:
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None if gbqkv is None else gbqkv.view(-1))
         else:
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
@@ -322,6 +331,8 @@ class EncoderBlockFn(torch.autograd.Function):
         def attn_wgrads():
             # the in_proj bias gradient (a memory-bound column sum, consumed only by the optimizer)
             # rides on the side stream with the weight gradients, off the dgrad chain
+            if db_part is not None:
+                ext.attn_dbias_reduce(db_part, B, H, gbqkv.view(-1))
             if side_db:
                 gemm.bias_grad(dqkv, gbqkv)
             if gwo is not None and not early:
@@ -329,7 +340,7 @@ class EncoderBlockFn(torch.autograd.Function):
             if gwqkv is not None:
                 gemm.linear_wgrad(dqkv, xn1, gwqkv)
 
-        store.on_side(attn_wgrads, dx1, o, dqkv, xn1)
+        store.on_side(attn_wgrads, dx1, o, dqkv, xn1, *(() if db_part is None else (db_part,)))
         dxn1 = dgrad(dqkv, wqkv, 3)
         dx = torch.empty_like(dx2)
         if prev is not None:

@@ -676,6 +676,8 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_bwd(2, 197, 3, 64, True),
         lambda: check_attn_bwd(40, 197, 12),   # pipelined whole-head backward, several pairs per workgroup
         lambda: check_attn_bwd(300, 197, 2),   # 600 pairs: 2-3 pairs per workgroup, pair hand-offs
+        lambda: check_attn_bwd(40, 197, 12, 64, True),  # in_proj bias gradient from the pipelined kernel's partials
+        lambda: check_attn_bwd(3, 256, 3, 64, True),
         lambda: check_attn_bwd(5, 193, 4),     # pipelined backward, one key in the last slice
         lambda: check_attn_bwd(3, 256, 3),     # 8 full key slices, no masking
         lambda: check_attn_bwd(2, 224, 3),
