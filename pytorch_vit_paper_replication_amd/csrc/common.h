@@ -180,6 +180,16 @@ PVR_DEV uint32_t rng_hash(uint64_t seed, uint64_t idx) {
 PVR_DEV bool rng_keep(uint64_t seed, uint64_t idx, uint32_t thr16) {
   return ((rng_hash(seed, idx >> 1) >> ((idx & 1) * 16)) & 0xFFFFu) >= thr16;
 }
+// Keep decisions of 4 consecutive elements from an even idx with idx + 3 < 2^32 (key = rng_key(seed)):
+// the same hashes as two rng_keep2 calls (high word 0), in 32-bit index arithmetic.
+PVR_DEV void rng_keep4_32(uint32_t key, uint32_t idx_even, uint32_t thr16, bool (&k)[4]) {
+  const uint32_t i = idx_even >> 1;
+  const uint32_t h0 = rng_mix32(i ^ key), h1 = rng_mix32((i + 1) ^ key);
+  k[0] = (h0 & 0xFFFFu) >= thr16;
+  k[1] = (h0 >> 16) >= thr16;
+  k[2] = (h1 & 0xFFFFu) >= thr16;
+  k[3] = (h1 >> 16) >= thr16;
+}
 // Pair form for an even idx: keep decisions of idx and idx + 1 from one hash.
 PVR_DEV void rng_keep2(uint64_t seed, uint64_t idx_even, uint32_t thr16, bool& k0, bool& k1) {
   const uint32_t h = rng_hash(seed, idx_even >> 1);
@@ -205,6 +215,28 @@ PVR_DEV void gelu_and_grad(float u, float& g, float& gp) {
   const float cdf = u >= 0.f ? 1.0f - half_erfc : half_erfc;
   g = u * cdf;
   gp = fmaf(u * 0.39894228040143268f, e, cdf);
+}
+// Two-lane form of gelu_and_grad: the polynomial and products as packed fp32 (v_pk_fma_f32 /
+// v_pk_mul_f32 do two lanes' work per instruction), the exp / rcp per element.
+typedef float v2f __attribute__((ext_vector_type(2)));
+PVR_DEV void gelu_and_grad2(v2f u, v2f& g, v2f& gp) {
+  const v2f uu = u * u;
+  const v2f den = __builtin_elementwise_fma((v2f){0.23164190f, 0.23164190f}, __builtin_elementwise_abs(u), (v2f){1.f, 1.f});
+  v2f e, t;
+  e.x = __builtin_amdgcn_exp2f(-0.72134752044448170f * uu.x);
+  e.y = __builtin_amdgcn_exp2f(-0.72134752044448170f * uu.y);
+  t.x = __builtin_amdgcn_rcpf(den.x);
+  t.y = __builtin_amdgcn_rcpf(den.y);
+  v2f poly = __builtin_elementwise_fma(t, (v2f){1.061405429f, 1.061405429f}, (v2f){-1.453152027f, -1.453152027f});
+  poly = __builtin_elementwise_fma(t, poly, (v2f){1.421413741f, 1.421413741f});
+  poly = __builtin_elementwise_fma(t, poly, (v2f){-0.284496736f, -0.284496736f});
+  poly = __builtin_elementwise_fma(t, poly, (v2f){0.254829592f, 0.254829592f});
+  const v2f he = (v2f){0.5f, 0.5f} * t * poly * e;  // erfc(|u|/sqrt2) / 2
+  v2f cdf;
+  cdf.x = u.x >= 0.f ? 1.0f - he.x : he.x;
+  cdf.y = u.y >= 0.f ? 1.0f - he.y : he.y;
+  g = u * cdf;
+  gp = __builtin_elementwise_fma(u * (v2f){0.39894228040143268f, 0.39894228040143268f}, e, cdf);
 }
 PVR_DEV float gelu_erf_grad(float u) {
   const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));

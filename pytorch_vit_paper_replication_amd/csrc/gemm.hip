@@ -952,6 +952,9 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
     if (p.bias && ncol) bias = *(const float4*)(p.bias + n);
   }
   const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
+  const uint32_t key = p.drop_thr ? rng_key(seed) : 0u;
+  // every dropout element index of the tensor fits in 32 bits (the usual case): 32-bit hash path
+  const bool idx32 = (uint64_t)p.M * (uint64_t)p.N + 4 <= 0xFFFFFFFFull;
   const float deq = p.scale_a ? (*p.scale_a) * (*p.scale_b) : 1.f;
   float csum[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int NPASS = 256 / RP, FPP = RP / 16;  // passes; fragment rows (of 8 per wave) per pass
@@ -1035,8 +1038,12 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         bool keep[4] = {true, true, true, true};
         if (p.drop_thr) {
           const uint64_t idx = idx0 + (uint64_t)k * idx_step;
-          rng_keep2(seed, idx, p.drop_thr, keep[0], keep[1]);
-          rng_keep2(seed, idx + 2, p.drop_thr, keep[2], keep[3]);
+          if (EPI == EPI_GELU && idx32) {
+            rng_keep4_32(key, (uint32_t)idx, p.drop_thr, keep);
+          } else {
+            rng_keep2(seed, idx, p.drop_thr, keep[0], keep[1]);
+            rng_keep2(seed, idx + 2, p.drop_thr, keep[2], keep[3]);
+          }
         }
         if constexpr (EPI == EPI_BF16) {
           if (p.drop_thr) {
@@ -1049,16 +1056,15 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
             v[2] += bf2f(rr.y & 0xFFFF); v[3] += bf2f(rr.y >> 16);
           }
         } else {
-          float gp[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float gv, gd;
-            gelu_and_grad(v[q], gv, gd);
-            const float sc = keep[q] ? p.drop_scale : 0.f;
-            v[q] = gv * sc;
-            gp[q] = gd * sc;
-          }
-          uint2 ax; ax.x = pack2bf(gp[0], gp[1]); ax.y = pack2bf(gp[2], gp[3]);
+          // two lanes per packed-fp32 instruction (v_pk_fma_f32 / v_pk_mul_f32)
+          const v2f s01 = {keep[0] ? p.drop_scale : 0.f, keep[1] ? p.drop_scale : 0.f};
+          const v2f s23 = {keep[2] ? p.drop_scale : 0.f, keep[3] ? p.drop_scale : 0.f};
+          v2f g01, d01, g23, d23;
+          gelu_and_grad2((v2f){v[0], v[1]}, g01, d01);
+          gelu_and_grad2((v2f){v[2], v[3]}, g23, d23);
+          g01 *= s01; g23 *= s23; d01 *= s01; d23 *= s23;
+          v[0] = g01.x; v[1] = g01.y; v[2] = g23.x; v[3] = g23.y;
+          uint2 ax; ax.x = pack2bf(d01.x, d01.y); ax.y = pack2bf(d23.x, d23.y);
           if (ok) *(uint2*)(x0 + (int64_t)k * (8 * p.ld_aux)) = ax;
         }
       } else if constexpr (EPI == EPI_DGELU) {
