@@ -1327,12 +1327,15 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
     if (dbp) {
       // q: column sums of this block's dQ (queries past N have dS = 0, so dQ = 0 exactly);
       // v: wave 0's column sums of dO over the block's valid queries (vsb, from its phase 1b)
-      float* dst = dbp + ((int64_t)ppair * NQ + pqb) * 128;
+      float* dst = dbp + ((int64_t)ppair * NQ + pqb) * 192;  // q | 0 (the second query half) | v
       float cs[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[r] = row16_sum(acc0[r] + acc1[r]) * scale;
       if (li == 0) *(float4*)(dst + 16 * wave + 4 * g) = make_float4(cs[0], cs[1], cs[2], cs[3]);
-      if (wave == 0) dst[64 + lane] = vsb[lane];
+      if (wave == 0) {
+        dst[64 + lane] = 0.f;
+        dst[128 + lane] = vsb[lane];
+      }
     }
   };
 
@@ -1558,6 +1561,364 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* _
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   phase2((npr * NQ - 1) & 1, NQ - 1, prv, p1 - 1, ktf);
+  store_dkv(prv);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+}
+
+// ------------------------------------------- backward, whole head, pipelined, two waves per SIMD
+// attn_bwd_pipe_kernel's algorithm (192 < N <= 224: NQ = 7 blocks) with 8 waves, two per SIMD: the
+// second wave on each SIMD hides the latency chains (exp -> pack -> MFMA, LDS reads, per-block waits)
+// that leave the one-wave-per-SIMD kernel's MFMA and VALU pipes idle. That needs <= 256 registers
+// per wave, so the persistent state shrinks: wave w owns keys [32w, 32w + 32) (two key fragments:
+// 64 accumulator registers), and the K image is double-buffered by pair so the K (S operand) and
+// K^T (dQ operand) fragments are read from LDS each block instead of being held; only V (dP
+// operand) stays in registers. Phase 2: wave w computes dQ^T dims 16(w&3) .. +15 of queries
+// 16(w>>2) .. +15. LDS: K x2 | V | 3-slot Q/dO/O/lse ring | dS^T x2 (152.75 KiB). Every block issues
+// one LDS-DMA group right after its barrier (4 per wave, slots 8i + wave: i = 0 Q / dO pieces, 1 O
+// pieces and lse, 2-3 next-pair K / V slices) with block t+2's rows; the next barrier waits for it
+// (vmcnt(0)), a whole block later. Wave 7 (no keys below N) computes the v-bias partial. Bias
+// partials: [pair][NQ][192] = dQ column sums of the two query halves | dO column sums.
+template <int NQ>
+__global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                                 const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                                 const uint16_t* __restrict__ o, int64_t ld_o,
+                                                                 const float* __restrict__ lse, uint16_t* __restrict__ dqkv,
+                                                                 int64_t ld_dq, float* __restrict__ dbp, int N, int H, int D,
+                                                                 int npairs, float scale) {
+  static_assert(NQ == 7, "192 < N <= 224");
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  constexpr int DH = 64;
+  constexpr int NP = 32 * NQ;               // staged rows (queries / keys) per pair
+  constexpr int IMG = NP * 128;             // K or V image: [NP][128 B], swizzled (lds_off)
+  constexpr int SLOT = 3 * 4096 + 1024;     // ring slot: Q | dO | O rows of one block, lse DMA slot
+  constexpr int DSB = NP * 64;              // dS^T image [key][32 queries]
+  constexpr int NKV = NP / 4;               // 1 KiB pieces of one pair's K + V images
+  constexpr int NDMA = 4;                   // DMA instructions per wave per block
+  constexpr int KV_PER_IT = 8 * (NDMA - 2); // next-pair K/V pieces per block (slots 16 .. 31)
+  constexpr int DBP = 192;                  // bias-gradient partial floats per (pair, block)
+  static_assert((NQ - 1) * KV_PER_IT >= NKV, "the next pair's K/V images must be issued within the pair");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg0 = smem;                        // K image of even pair indices (odd: + IMG)
+  char* vimg = smem + 2 * IMG;
+  char* ring = vimg + IMG;
+  char* dsb = ring + 3 * SLOT;
+  float* s_tab = (float*)(dsb + 2 * DSB);   // [2][64]: lse * log2e [32] | delta [32] of a block
+  float* vsb = s_tab + 128;                  // [64]: v-bias partial of the last block (wave 7 only)
+  char* sink = (char*)(vsb + 64);           // 1 KiB target of the filler DMAs of a group
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  PVR_ASSERT(blockDim.x == 512 && (N + 31) / 32 == NQ && (int)gridDim.x <= npairs);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
+  const int p0 = L * per + min(L, rem);
+  const int p1 = p0 + per + (L < rem ? 1 : 0);
+  if (p0 >= p1) return;
+  const int kw0 = wave * 32;
+  const int nf = min(2, max(0, (N - kw0 + 15) / 16));  // this wave's key fragments holding a key < N
+  const int j4 = wave & 3, qh = wave >> 2;            // staging piece / phase-2 dims 16 j4, queries 16 qh
+  const float c = scale * LOG2E;
+  const int64_t rows_all = (int64_t)(npairs / H) * N;
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv, clamp_bytes(((rows_all - 1) * ld + 3 * D) * 2));
+  const __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout, clamp_bytes(((rows_all - 1) * ld_do + D) * 2));
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(o, clamp_bytes(((rows_all - 1) * ld_o + D) * 2));
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(lse, clamp_bytes((int64_t)npairs * N * 4));
+  const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv, clamp_bytes(((rows_all - 1) * ld_dq + 3 * D) * 2));
+  constexpr uint32_t OOR = 0x80000000u;  // dropped stores only: no DMA ever reads out of range
+  const uint32_t ldq = (uint32_t)ld * 2, lddo = (uint32_t)ld_do * 2, ldoo = (uint32_t)ld_o * 2, lddq = (uint32_t)ld_dq * 2;
+
+  // ---- lane-dependent offsets, computed once
+  const int l3 = lane >> 3, l7 = lane & 7;
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int srl = 8 * j4 + l3;  // staging: row of a 32-row block (piece j4)
+  const uint32_t sch = (uint32_t)((l7 ^ swz_a(srl)) << 4);
+  const uint32_t stq = (uint32_t)srl * ldq + sch, std_ = (uint32_t)srl * lddo + sch, sto = (uint32_t)srl * ldoo + sch;
+  const uint32_t kvo0 = (uint32_t)l3 * ldq + (uint32_t)((l7 ^ swz_a(l3)) << 4);
+  const uint32_t kvo1 = (uint32_t)l3 * ldq + (uint32_t)((l7 ^ swz_a(8 + l3)) << 4);
+  // A-operand rows (query 16a + li, dims 32ks + 8g ..): a adds 2048; K rows kw0 + 16f + li: f adds 2048
+  const int fr0 = li * 128 + ((g ^ swz_a(li)) << 4);
+  const int fr1 = li * 128 + (((4 + g) ^ swz_a(li)) << 4);
+  int trq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) trq[e] = (4 * g + q4) * 128 + (((2 * e + (p4 >> 1)) ^ swz_a(4 * g + q4)) << 4) + 8 * (p4 & 1);
+  // K^T transposed reads for phase 2 (rows 32ks + 8g + q4, +4; dims 16 j4 + 4p4): ks adds 4096
+  const int ktlo = lds_off(NP, 8 * g + q4, 2 * j4 + (p4 >> 1)) + 8 * (p4 & 1);
+  const int kthi = lds_off(NP, 8 * g + q4 + 4, 2 * j4 + (p4 >> 1)) + 8 * (p4 & 1);
+  auto ds_off = [](int key, int u) { return key * 64 + ((u ^ ((key >> 1) & 7)) << 3); };
+  const int dsw0 = ds_off(li, g) + kw0 * 64, dsw1 = ds_off(li, 4 + g) + kw0 * 64;  // a = 0 / 1; f adds 1024
+  // phase 2: dS^T rows 32ks + 8g + q4 (+4), queries 16 qh + 4p4; ks adds 2048
+  const int p2lo = ds_off(8 * g + q4, 4 * qh + p4), p2hi = ds_off(8 * g + q4 + 4, 4 * qh + p4);
+  // next-block table: queries 4 wave + g, dims 4 li .. 4 li + 3 (one 8-B piece)
+  const int tq = 4 * wave + g;
+  const int tbo = tq * 128 + (((li >> 1) ^ swz_a(tq)) << 4) + 8 * (li & 1);
+
+  struct PairOff {
+    uint32_t row, col;  // b * N, h * DH * 2 (bytes)
+  };
+  auto pair_off = [&](int pr) { return PairOff{(uint32_t)((pr / H) * N), (uint32_t)((pr % H) * DH * 2)}; };
+  auto dma = [&](__amdgpu_buffer_rsrc_t rs, char* img, uint32_t voff) { dma16(rs, to_lds(img), voff); };
+  // this wave's NDMA DMAs: block sqb of pair `so` into ring slot `slot` and, if kvon, K / V pieces
+  // [kvc * KV_PER_IT, ...) of pair `ko` (K into `kdst`); rows past N clamped to N-1 (no DMA reads
+  // out of range); filler slots reload a valid piece into `sink` at a distinct address per slot
+  auto issue_group = [&](PairOff so, int sqb, char* slot, bool kvon, int kvc, PairOff ko, char* kdst) {
+    const int r0 = 32 * sqb;
+    const int row = min(r0 + srl, N - 1) - srl;
+    const uint32_t rb = so.row + (uint32_t)row;
+    if (wave < 4)
+      dma(rq, slot + j4 * 1024, rb * ldq + so.col + stq);
+    else
+      dma(rdo, slot + 4096 + j4 * 1024, rb * lddo + so.col + std_);
+    if (wave < 4) {
+      dma(ro, slot + 8192 + j4 * 1024, rb * ldoo + so.col + sto);
+    } else if (wave == 4) {  // lse[(b*H + h)*N + r0 ..] (lanes 8.. repeat lane 7)
+      dma(rl, slot + 12288, (so.row * (uint32_t)H + (so.col >> 7) * (uint32_t)N + (uint32_t)r0) * 4 + (uint32_t)min(lane, 7) * 16);
+    } else {
+      dma(rq, sink, (uint32_t)lane * 16 + 1024);
+    }
+#pragma unroll
+    for (int i = 2; i < NDMA; ++i) {
+      const int k = kvc * KV_PER_IT + 8 * (i - 2) + wave;
+      const bool live = kvon && k < NKV;
+      const int which = k >= NP / 8, rr = (k - which * (NP / 8)) * 8;
+      const int kr = min(rr + l3, N - 1) - l3;
+      const uint32_t base = (ko.row + kr) * ldq + (uint32_t)(which + 1) * D * 2 + ko.col;
+      dma(rq, live ? (which ? vimg : kdst) + rr * 128 : sink, live ? base + ((rr & 8) ? kvo1 : kvo0) : (uint32_t)lane * 16 + i * 1024);
+    }
+  };
+  // lse*log2e and delta of the block in ring slot `sb` (local block qb) into table buffer `tb`
+  auto block_table = [&](const char* sb, int qb, int tb) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+    const bf4 dw = *(const __attribute__((address_space(3))) bf4*)(sb + 4096 + tbo);
+    const bf4 ow = *(const __attribute__((address_space(3))) bf4*)(sb + 8192 + tbo);
+    float d = __builtin_amdgcn_fdot2_f32_bf16(bf2{dw[0], dw[1]}, bf2{ow[0], ow[1]}, 0.f, false);
+    d = __builtin_amdgcn_fdot2_f32_bf16(bf2{dw[2], dw[3]}, bf2{ow[2], ow[3]}, d, false);
+    d = row16_sum(d);
+    if (li == 0) {
+      const float l = ((const float*)(sb + 12288))[tq];
+      s_tab[tb * 64 + tq] = 32 * qb + tq < N ? l * LOG2E : __builtin_huge_valf();
+      s_tab[tb * 64 + 32 + tq] = d;
+    }
+  };
+  // dQ^T fragment (dims 16 j4 + 4g + r, queries 16 qh + li) of a block (local pqb of pair index
+  // ppair) from dS^T buffer `ds` and the pair's K image `kimg`; with dbp, its bias partials
+  auto phase2 = [&](const char* ds, const char* kimg, int pqb, PairOff po, int ppair) {
+    v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+    auto batch = [&](auto k0c, auto k1c) {
+      constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
+      v4s klo[k1 - k0], khi[k1 - k0], lo[k1 - k0], hi[k1 - k0];
+      static_for<k0, k1>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        klo[ks - k0] = ds_read_tr_async_at<4096 * ks>(kimg + ktlo);
+        khi[ks - k0] = ds_read_tr_async_at<4096 * ks>(kimg + kthi);
+        lo[ks - k0] = ds_read_tr_async_at<2048 * ks>(ds + p2lo);
+        hi[ks - k0] = ds_read_tr_async_at<2048 * ks>(ds + p2hi);
+      });
+      lds_wait();
+#pragma unroll
+      for (int j = 0; j < k1 - k0; ++j) acc = mfma16(cat44(klo[j], khi[j]), cat44(lo[j], hi[j]), acc);
+    };
+    batch(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+    batch(std::integral_constant<int, 4>{}, std::integral_constant<int, NQ>{});
+    const int q = pqb * 32 + 16 * qh + li;
+    const uint32_t vo = q < N ? (po.row + q) * lddq + po.col + (uint32_t)(16 * j4 + 4 * g) * 2 : OOR;
+    const v2u w = {pack2bf(acc[0] * scale, acc[1] * scale), pack2bf(acc[2] * scale, acc[3] * scale)};
+    __builtin_amdgcn_raw_buffer_store_b64(w, rdq, vo, 0, 0);
+    if (dbp) {  // queries past N have dS = 0, so dQ = 0 exactly
+      float* dst = dbp + ((int64_t)ppair * NQ + pqb) * DBP;
+      float cs[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[r] = row16_sum(acc[r]) * scale;
+      if (li == 0) *(float4*)(dst + 64 * qh + 16 * j4 + 4 * g) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      if (wave == 7) dst[128 + lane] = vsb[lane];
+    }
+  };
+
+  v8s vf[2][2];
+  v4f dk[4][2], dv[4][2];  // [dims e][key fragment f]
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int f = 0; f < 2; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
+  };
+  auto store_dkv = [&](PairOff po) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int key = kw0 + 16 * f + li;
+      const uint32_t vo = key < N ? (po.row + key) * lddq + po.col + (uint32_t)(4 * g) * 2 : OOR;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const v2u wk = {pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale), pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale)};
+        const v2u wv = {pack2bf(dv[e][f][0], dv[e][f][1]), pack2bf(dv[e][f][2], dv[e][f][3])};
+        __builtin_amdgcn_raw_buffer_store_b64(wk, rdq, vo + (uint32_t)(D + 16 * e) * 2, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(wv, rdq, vo + (uint32_t)(2 * D + 16 * e) * 2, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: pair p0's K (buffer 0) / V images, blocks 0 and 1; table of block 0
+  const PairOff none{0u, 0u};
+  PairOff cur = pair_off(p0);
+  for (int k = wave; k < NKV; k += 8) {
+    const int which = k >= NP / 8, rr = (k - which * (NP / 8)) * 8;
+    const int kr = min(rr + l3, N - 1) - l3;
+    const uint32_t base = (cur.row + kr) * ldq + (uint32_t)(which + 1) * D * 2 + cur.col;
+    dma(rq, (which ? vimg : kimg0) + rr * 128, base + ((rr & 8) ? kvo1 : kvo0));
+  }
+  issue_group(cur, 0, ring, false, 0, none, kimg0);
+  issue_group(cur, 1, ring + SLOT, false, 0, none, kimg0);
+  zero_acc();
+  wait_barrier_lds<0>();
+  block_table(ring, 0, 0);
+
+  const int npr = p1 - p0;
+  PairOff prv = cur;
+  int sl = 0;  // ring slot of block t (t mod 3)
+  for (int pi = 0; pi < npr; ++pi) {
+    cur = pair_off(p0 + pi);
+    const bool has_next = pi + 1 < npr;
+    const PairOff nxt = has_next ? pair_off(p0 + pi + 1) : none;
+    const char* kimg = kimg0 + (pi & 1) * IMG;
+    char* knext = kimg0 + ((pi + 1) & 1) * IMG;
+#pragma unroll 1
+    for (int qb = 0; qb < NQ; ++qb) {
+      const int t = pi * NQ + qb;
+      // everything issued before (block t+1's DMA group, the previous stores) complete; dS^T of
+      // block t-1 and the table of block t visible; every wave past its reads of the reused buffers
+      wait_barrier_lds<0>();
+      const char* qimg = ring + sl * SLOT;
+      const char* doimg = qimg + 4096;
+      const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl1 == 2 ? 0 : sl1 + 1;
+      // ---- DMA: block t+2 into slot (t+2) mod 3 (block t-1's, consumed) and, in local blocks
+      // 1 .. NQ-1, slices of the next pair's K (other buffer, free once block 0's phase 2 of the
+      // previous pair ran) / V (this pair's V fragments are in registers by then) images
+      if (qb + 2 < NQ)
+        issue_group(cur, qb + 2, ring + sl2 * SLOT, qb >= 1 && has_next, qb - 1, nxt, knext);
+      else
+        issue_group(has_next ? nxt : cur, has_next ? qb + 2 - NQ : 0, ring + sl2 * SLOT, has_next, qb - 1, nxt, knext);
+      if (qb == 0) {
+        if (pi > 0) {
+          // the previous pair's last block (its K image is the other buffer) and its dK / dV
+          phase2(dsb + ((t - 1) & 1) * DSB, knext, NQ - 1, prv, p0 + pi - 1);
+          store_dkv(prv);
+          zero_acc();
+        }
+        if (nf > 0) {
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) vf[f][ks] = ds_read_b128(vimg + kw0 * 128 + 2048 * f + (ks ? fr1 : fr0));
+        }
+      }
+      // ---- phase 1a: S[q][key], dP[q][key] of the wave's two key fragments
+      v4f s[2][2], dp[2][2];
+      if (nf > 0) {
+        v8s qa[2][2], dA[2][2], kf[2][2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const int fo = (ks ? fr1 : fr0) + 2048 * a;
+            qa[ks][a] = ds_read_b128(qimg + fo);
+            dA[ks][a] = ds_read_b128(doimg + fo);
+            kf[a][ks] = ds_read_b128(kimg + kw0 * 128 + fo);  // key fragment f = a
+          }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int f = 0; f < 2; ++f) s[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              s[a][f] = mfma16(qa[ks][a], kf[f][ks], s[a][f]);
+              dp[a][f] = mfma16(dA[ks][a], vf[f][ks], dp[a][f]);
+            }
+      }
+      // ---- phase 2 of block t-1 (same pair), while the S / dP products drain
+      if (qb != 0) phase2(dsb + ((t - 1) & 1) * DSB, kimg, qb - 1, cur, p0 + pi);
+      // ---- table of block t+1 (landed at this block's wait)
+      if (qb + 1 < NQ)
+        block_table(ring + sl1 * SLOT, qb + 1, (t + 1) & 1);
+      else if (has_next)
+        block_table(ring + sl1 * SLOT, 0, (t + 1) & 1);
+      // ---- phase 1b: P, dS of both key fragments (dS^T -> LDS), then dV^T += dO^T P, dK^T += Q^T dS
+      // one dims fragment at a time (transposed Q / dO reads double-buffered)
+      if (nf > 0) {
+        const float* tl = s_tab + (t & 1) * 64 + 4 * g;
+        char* img = dsb + (t & 1) * DSB;
+        v8s pf[2], sf[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const bool kin = kw0 + 16 * f + li < N;
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const v4f l4 = *(const v4f*)(tl + 16 * a), d4 = *(const v4f*)(tl + 32 + 16 * a);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float pv = kin ? __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l4[r])) : 0.f;
+              s[a][f][r] = pv;
+              dp[a][f][r] = pv * (dp[a][f][r] - d4[r]);
+            }
+            const v2u w = {pack2bf(dp[a][f][0], dp[a][f][1]), pack2bf(dp[a][f][2], dp[a][f][3])};
+            *(v2u*)(img + (a ? dsw1 : dsw0) + 1024 * f) = w;
+          }
+          pf[f] = pack_p(s[0][f], s[1][f]);
+          sf[f] = pack_p(dp[0][f], dp[1][f]);
+        }
+        v4s dlo[2], dhi[2], qlo[2], qhi[2];
+        auto tr_load = [&](int e, int bsel) {
+          dlo[bsel] = ds_read_tr_async(doimg + trq[e]);
+          dhi[bsel] = ds_read_tr_async(doimg + trq[e] + 2048);
+          qlo[bsel] = ds_read_tr_async(qimg + trq[e]);
+          qhi[bsel] = ds_read_tr_async(qimg + trq[e] + 2048);
+        };
+        tr_load(0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lds_wait();
+          if (e + 1 < 4) tr_load(e + 1, (e + 1) & 1);
+          const v8s dot = cat44(dlo[e & 1], dhi[e & 1]), qt = cat44(qlo[e & 1], qhi[e & 1]);
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
+            dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
+          }
+        }
+      }
+      if (dbp && wave == 7) {
+        // v-bias partial: dO^T . 1 over the block's queries < N (the k bias gets no gradient)
+        v4s vlo[4], vhi[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vlo[e] = ds_read_tr_async(doimg + trq[e]);
+          vhi[e] = ds_read_tr_async(doimg + trq[e] + 2048);
+        }
+        v4f m0, m1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          m0[r] = 32 * qb + 4 * g + r < N ? 1.f : 0.f;
+          m1[r] = 32 * qb + 16 + 4 * g + r < N ? 1.f : 0.f;
+        }
+        const v8s ones = pack_p(m0, m1);
+        lds_wait();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const v4f cs = mfma16(cat44(vlo[e], vhi[e]), ones, v4f{0.f, 0.f, 0.f, 0.f});
+          if (li == 0) *(v4f*)(vsb + 16 * e + 4 * g) = cs;
+        }
+      }
+      sl = sl1;
+    }
+    prv = cur;
+  }
+  // last block's dQ and the last pair's dK / dV
+  wait_barrier_lds<0>();
+  phase2(dsb + ((npr * NQ - 1) & 1) * DSB, kimg0 + ((npr - 1) & 1) * IMG, NQ - 1, prv, p1 - 1);
   store_dkv(prv);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
@@ -1809,10 +2170,40 @@ static hipError_t attn_bwd_pipe_launch(const uint16_t* qkv, int64_t ld, const ui
   return hipGetLastError();
 }
 
+template <int NQ>
+static hipError_t attn_bwd_pipe8_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                        int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dbp, int B, int N, int H,
+                                        int D, float scale, hipStream_t s) {
+  using namespace pvr;
+  constexpr int SMEM = 3 * (32 * NQ) * 128 + 3 * (3 * 4096 + 1024) + 2 * (32 * NQ) * 64 + 512 + 256 + 1024;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_pipe8_kernel<NQ>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int npairs = B * H;
+  const int grid = npairs < device_cus() ? npairs : device_cus();
+  hipLaunchKernelGGL(attn_bwd_pipe8_kernel<NQ>, dim3(grid), dim3(512), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq, dbp,
+                     N, H, D, npairs, scale);
+  return hipGetLastError();
+}
+
+// PVR_ATTN_BWD_WAVES=4: the one-wave-per-SIMD pipelined backward instead of the 8-wave one (A/B)
+static int bwd_pipe_waves() {
+  static const int w = [] {
+    const char* e = getenv("PVR_ATTN_BWD_WAVES");
+    return e && e[0] == '4' ? 4 : 8;
+  }();
+  return w;
+}
+
 // pipelined whole-head backward: dh 64, 192 < N <= 256
 static hipError_t attn_bwd_pipe(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout, int64_t ld_do,
                                 const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dbp, int B, int N, int H, int D, float scale,
                                 hipStream_t s) {
+  if (bwd_pipe_waves() == 8 && (N + 31) / 32 == 7)  // 192 < N <= 224 (the K double buffer fits LDS)
+    return attn_bwd_pipe8_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
   switch ((N + 31) / 32) {
     case 7: return attn_bwd_pipe_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
     case 8: return attn_bwd_pipe_launch<8>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
@@ -1892,9 +2283,10 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
 }
 
 // 1 if pvr_attn_bwd takes the pipelined whole-head backward for this shape and these layouts; its
-// dbias is then f32 [B*H][ceil(N/32)][128] partials instead: per (batch, head, 32-query block) the
-// column sums of dQ (64, the head's q-bias slice) and of dO (64: the v-bias slice, sum_k dV = sum_q dO
-// since softmax rows sum to 1); the k-bias gradient is exactly 0 (sum_k dS = 0 per query)
+// dbias is then f32 [B*H][ceil(N/32)][192] partials instead: per (batch, head, 32-query block) the
+// column sums of dQ over its two 16-query halves (2 x 64, the head's q-bias slice; summed) and of dO
+// (64: the v-bias slice, sum_k dV = sum_q dO since softmax rows sum to 1); the k-bias gradient is
+// exactly 0 (sum_k dS = 0 per query)
 extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq) {
   return attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq) ? 1 : 0;
 }

@@ -400,14 +400,14 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int
   return {out, lse};
 }
 
-// dbias[3D] += the in_proj bias gradient from the pipelined backward's [B*H][NQ][128] partials
-// (per query block: dQ column sums | dO column sums; the k slice gets no gradient)
+// dbias[3D] += the in_proj bias gradient from the pipelined backward's [B*H][NQ][192] partials
+// (per query block: dQ column sums of two query halves | dO column sums; the k slice gets none)
 void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor dbias) {
-  TORCH_CHECK(part.is_contiguous() && part.numel() % (B * H * 128) == 0, "attn_dbias_reduce: [B*H][NQ][128] partials");
-  auto r = part.view({B, H, -1, 2, 64}).sum(at::IntArrayRef{0, 2});  // [H][2][64]
+  TORCH_CHECK(part.is_contiguous() && part.numel() % (B * H * 192) == 0, "attn_dbias_reduce: [B*H][NQ][192] partials");
+  auto r = part.view({B, H, -1, 3, 64}).sum(at::IntArrayRef{0, 2});  // [H][3][64]
   auto db = dbias.view({3, H, 64});
-  db.select(0, 0).add_(r.select(1, 0));
-  db.select(0, 2).add_(r.select(1, 1));
+  db.select(0, 0).add_(r.select(1, 0) + r.select(1, 1));
+  db.select(0, 2).add_(r.select(1, 2));
 }
 
 // pipelined backward taken for the standard layouts of this shape (qkv [T][3D], dO / O [T][D])
@@ -416,7 +416,7 @@ bool attn_bwd_pipe_path(int64_t B, int64_t N, int64_t H, int64_t D) {
 }
 
 // dbias: [3D] f32 accumulated with the in_proj bias gradient. dbias_part (pipelined path only,
-// [B*H][ceil(N/32)][128] f32): receives the kernel's per-block partials instead, left unreduced (the
+// [B*H][ceil(N/32)][192] f32): receives the kernel's per-block partials instead, left unreduced (the
 // caller reduces them, e.g. on the weight-gradient side stream: attn_dbias_reduce).
 torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
                        double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out) {
@@ -436,15 +436,15 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   if (part_out) {
     TORCH_CHECK(pipe && !want_db, "dbias_part: pipelined backward only, and not together with dbias");
     TORCH_CHECK(dbias_part_out->is_cuda() && dbias_part_out->scalar_type() == torch::kFloat32 && dbias_part_out->is_contiguous() &&
-                    dbias_part_out->numel() == B * H * ((N + 31) / 32) * 128,
-                "dbias_part [B*H][ceil(N/32)][128] f32");
+                    dbias_part_out->numel() == B * H * ((N + 31) / 32) * 192,
+                "dbias_part [B*H][ceil(N/32)][192] f32");
     dbias_part = *dbias_part_out;
   }
   if (want_db) {
     TORCH_CHECK(dbias->numel() == 3 * D && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous(), "dbias [3D] f32");
     const int dh = (int)(D / H);
-    if (pipe)  // per-(batch, head, query block) partials written by the pipelined backward: q 64 | v 64
-      dbias_part = torch::empty({B * H, (N + 31) / 32, 128}, qkv.options().dtype(torch::kFloat32));
+    if (pipe)  // per-(batch, head, query block) partials written by the pipelined backward: q 2 x 64 | v 64
+      dbias_part = torch::empty({B * H, (N + 31) / 32, 192}, qkv.options().dtype(torch::kFloat32));
     else if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
       dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }

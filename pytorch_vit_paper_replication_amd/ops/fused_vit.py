@@ -318,7 +318,7 @@ class EncoderBlockFn(torch.autograd.Function):
             # the pipelined attention backward emits per-(image, head, query block) column sums of dQ and
             # dO (= the v-bias gradient; the k bias has none); only their small reduction remains (side
             # stream), no pass over dQKV
-            db_part = torch.empty(B * H, (N + 31) // 32, 128, dtype=torch.float32, device=do.device)
+            db_part = torch.empty(B * H, (N + 31) // 32, 192, dtype=torch.float32, device=do.device)
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part)
         elif _FUSE_QKV_DBIAS:
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None if gbqkv is None else gbqkv.view(-1))
