@@ -244,15 +244,29 @@ PVR_DEV float gelu_erf_grad(float u) {
   return cdf + u * pdf;
 }
 
+// Whole-wave reductions without LDS round trips: DPP within each 16-lane row, then the gfx950 row
+// swaps (v_permlane16_swap: rows 0<->1, 2<->3; v_permlane32_swap: rows 0,1 <-> 2,3). Every lane
+// receives the result.
+template <class Op>
+PVR_DEV float wave_reduce(float v, Op op) {
+  v = op(v, dpp_mov<0x128>(v));  // row_ror:8
+  v = op(v, dpp_mov<0x124>(v));  // row_ror:4
+  v = op(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
+  // (inline asm: the builtins' results for swap(x, x) are folded to one value by this compiler)
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  v = op(a, b);
+  a = v;
+  b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return op(a, b);
+}
 PVR_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float a, float b) { return a + b; });
 }
 PVR_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 // Bijective XCD-aware remap: blocks dealt round-robin over 8 XCDs (b, b+8 share one) are given
