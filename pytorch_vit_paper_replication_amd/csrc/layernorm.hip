@@ -263,11 +263,12 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   static const int cap = [] {  // PVR_LN_BWD_BLOCKS: grid cap (A/B of row pipelining vs atomics per column)
     const char* e = getenv("PVR_LN_BWD_BLOCKS");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 512;
+    return v > 0 ? v : 1024;
   }();
   int nblk = (rows + 3) / 4;
-  // 512 blocks (2 per CU, ~25 pipelined rows per wave): 22 % faster than 2048 at ViT-B/16 b256, whose
-  // 2048 x 3 x D column atomics contended on the same addresses (profiles/kbench_ln_grid.log)
+  // 1024 blocks (4 per CU, ~12 pipelined rows per wave): in-step 0.2 % ahead of 512 and 768
+  // (profiles/ln_bwd_grid_step_ab_r2.log); 2048 was 22 % slower in isolation, its 2048 x 3 x D column
+  // atomics contending on the same addresses (profiles/kbench_ln_grid.log)
   if (nblk > cap) nblk = cap;
   const dim3 grid(nblk), block(256);
   const int maxch = (D / 8 + 63) / 64;
