@@ -39,6 +39,7 @@ hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
 hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, int, const float*, unsigned*, int, hipStream_t);
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
+hipError_t pvr_fp8_quant_multi(const int64_t*, int, int64_t, const float*, unsigned*, int, int, hipStream_t);
 int pvr_attn_bwd_key_blocks(int);
 int pvr_attn_bwd_needs_dq_acc(int, int, int);
 int pvr_attn_bwd_waves(int);
@@ -379,6 +380,21 @@ torch::Tensor fp8_dequant(torch::Tensor x, c10::optional<torch::Tensor> dscale, 
   return y;
 }
 
+// multi-tensor weight quantization: segs = int64 [nseg][5] {src bf16 ptr, dst fp8 ptr, n, slot, first
+// chunk} on the device (built once by the caller), nchunks = total chunks; amax_only: record max|x|
+// per slot instead of quantizing
+void fp8_quant_multi(torch::Tensor segs, int64_t nchunks, c10::optional<torch::Tensor> qscale, torch::Tensor amax, int64_t fmt,
+                     bool amax_only) {
+  TORCH_CHECK(segs.is_cuda() && segs.scalar_type() == torch::kInt64 && segs.dim() == 2 && segs.size(1) == 5 && segs.is_contiguous(),
+              "fp8_quant_multi: segs int64 [n][5]");
+  TORCH_CHECK(amax.is_cuda() && amax.scalar_type() == torch::kInt32, "fp8_quant_multi: amax int32");
+  const float* qs = qscale.has_value() && qscale->defined() ? f32(*qscale, "qscale") : nullptr;
+  TORCH_CHECK(amax_only || qs != nullptr, "fp8_quant_multi: quantizing needs qscale");
+  check(pvr_fp8_quant_multi(segs.data_ptr<int64_t>(), (int)segs.size(0), nchunks, qs, reinterpret_cast<unsigned*>(amax.data_ptr()),
+                            (int)fmt, amax_only ? 1 : 0, stream()),
+        "fp8_quant_multi");
+}
+
 void fp8_scale_update(torch::Tensor hist, torch::Tensor amax, torch::Tensor qscale, torch::Tensor dscale, torch::Tensor fmax, int64_t s0,
                       int64_t s1, double margin_mul) {
   TORCH_CHECK(hist.dim() == 2 && hist.is_contiguous(), "hist [n][H]");
@@ -512,6 +528,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);
+  m.def("fp8_quant_multi", &fp8_quant_multi, py::arg("segs"), py::arg("nchunks"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"),
+        py::arg("amax_only"));
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
         py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none());

@@ -33,6 +33,8 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
   const int per_row = cols >> 4;
   const int64_t n = rows * per_row;
   const float qs = qscale ? *qscale : 1.f;
+  // dense tensors (the usual case): flat offsets, no 64-bit division per 16 elements
+  const bool dense = ldx == cols && (!y || ldy == cols);
   float m = 0.f;
   // U grid-stride steps per trip with all their loads issued first (clamped, so unconditional):
   // the grid is capped at 256 blocks for the amax atomics, so memory-level parallelism has to come
@@ -44,8 +46,7 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = min(i0 + u * stride, n - 1);
-      const int64_t r = i / per_row;
-      const uint16_t* src = x + r * ldx + (int)(i % per_row) * 16;
+      const uint16_t* src = dense ? x + i * 16 : x + (i / per_row) * ldx + (int)(i % per_row) * 16;
       ua[u] = *(const uint4*)src;
       ub[u] = *(const uint4*)(src + 8);
     }
@@ -53,8 +54,6 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
     for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + u * stride;
       if (i >= n) break;
-      const int64_t r = i / per_row;
-      const int c = (int)(i % per_row) * 16;
       const uint32_t w[8] = {ua[u].x, ua[u].y, ua[u].z, ua[u].w, ub[u].x, ub[u].y, ub[u].z, ub[u].w};
       float v[16];
 #pragma unroll
@@ -76,7 +75,8 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
           const int t = pack2_fp8<FMT, false>(v[4 * q] * qs, v[4 * q + 1] * qs, 0);
           o[q] = pack2_fp8<FMT, true>(v[4 * q + 2] * qs, v[4 * q + 3] * qs, t);
         }
-        *(int4*)(y + r * ldy + c) = make_int4(o[0], o[1], o[2], o[3]);
+        uint8_t* dst = dense ? y + i * 16 : y + (i / per_row) * ldy + (int)(i % per_row) * 16;
+        *(int4*)dst = make_int4(o[0], o[1], o[2], o[3]);
       }
     }
   }
@@ -90,6 +90,70 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
     const float b = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
     // |x| bits order like uints; Inf (0x7f800000) and NaN (> 0x7f800000) sort above every finite
     if (!(b <= 0.f)) atomicMax(amax, __float_as_uint(b));
+  }
+}
+
+// Multi-tensor form for the per-step weight refresh (current scaling): one launch covers every
+// weight. Segment table rows (int64): {src bf16 ptr, dst fp8 ptr, elements (multiple of 16), slot,
+// first chunk}; a workgroup handles chunks of QM_CHUNK elements of one segment. AMAX: record
+// max|x| per slot (NaN-propagating, one atomic per workgroup); else quantize with qscale[slot].
+constexpr int QM_CHUNK = 256 * 16 * 4;
+template <int FMT, bool AMAX>
+__global__ void __launch_bounds__(256) quant_multi_kernel(const int64_t* __restrict__ segs, int nseg, int64_t nchunks,
+                                                          const float* __restrict__ qscale, unsigned* __restrict__ amax) {
+  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    int lo = 0, hi = nseg - 1;  // last segment whose first chunk <= ch
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (segs[mid * 5 + 4] <= ch) lo = mid; else hi = mid - 1;
+    }
+    const int64_t* sg = segs + lo * 5;
+    const uint16_t* x = reinterpret_cast<const uint16_t*>(sg[0]);
+    uint8_t* y = reinterpret_cast<uint8_t*>(sg[1]);
+    const int64_t n16 = sg[2] >> 4;
+    const int slot = (int)sg[3];
+    const int64_t g0 = (ch - sg[4]) * (QM_CHUNK / 16);
+    const float qs = AMAX ? 1.f : qscale[slot];
+    float m = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = g0 + u * 256 + threadIdx.x;
+      if (i >= n16) break;
+      const uint4 ua = *(const uint4*)(x + i * 16), ub = *(const uint4*)(x + i * 16 + 8);
+      const uint32_t w[8] = {ua.x, ua.y, ua.z, ua.w, ub.x, ub.y, ub.z, ub.w};
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[2 * j] = bf2f(w[j] & 0xFFFF);
+        v[2 * j + 1] = bf2f(w[j] >> 16);
+      }
+      if constexpr (AMAX) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float a = fabsf(v[j]);
+          m = (a > m || a != a) ? a : m;
+        }
+      } else {
+        int o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int t = pack2_fp8<FMT, false>(v[4 * q] * qs, v[4 * q + 1] * qs, 0);
+          o[q] = pack2_fp8<FMT, true>(v[4 * q + 2] * qs, v[4 * q + 3] * qs, t);
+        }
+        *(int4*)(y + i * 16) = make_int4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    if constexpr (AMAX) {
+      __shared__ float wm[4];
+      m = wave_max(m);
+      if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const float b = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+        if (!(b <= 0.f)) atomicMax(amax + slot, __float_as_uint(b));
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -144,6 +208,20 @@ extern "C" hipError_t pvr_fp8_quant(const uint16_t* x, int64_t ldx, uint8_t* y, 
     hipLaunchKernelGGL(quant_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, x, ldx, y, ldy, rows, cols, qscale, amax);
   else
     hipLaunchKernelGGL(quant_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, s, x, ldx, y, ldy, rows, cols, qscale, amax);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_fp8_quant_multi(const int64_t* segs, int nseg, int64_t nchunks, const float* qscale, unsigned* amax,
+                                          int fmt, int amax_only, hipStream_t s) {
+  using namespace pvr;
+  if (nseg <= 0 || nchunks <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)(nchunks < 8192 ? nchunks : 8192);
+  if (amax_only)
+    hipLaunchKernelGGL((quant_multi_kernel<0, true>), dim3(grid), dim3(256), 0, s, segs, nseg, nchunks, qscale, amax);
+  else if (fmt == 0)
+    hipLaunchKernelGGL((quant_multi_kernel<0, false>), dim3(grid), dim3(256), 0, s, segs, nseg, nchunks, qscale, amax);
+  else
+    hipLaunchKernelGGL((quant_multi_kernel<1, false>), dim3(grid), dim3(256), 0, s, segs, nseg, nchunks, qscale, amax);
   return hipGetLastError();
 }
 

@@ -278,6 +278,40 @@ def check_fp8_format(fmt=0):
     return (f"fp8 quant format fmt{fmt} (byte mismatch frac {mism:.2e})", mism + (0 if amax_ok else 1) + (0 if dq_ok else 1), 1e-3)
 
 
+def check_fp8_strided(fmt=1):
+    """Strided rows (row index math) and dense rows (flat offsets) quantize to the same bytes."""
+    ext = _ext.ext()
+    big = bf(rnd(96, 512) * 2)
+    x = big[:, 128:384]  # ldx 512, cols 256
+    qs = torch.tensor([5.0], device=DEV)
+    am1, am2 = (torch.zeros(1, dtype=torch.int32, device=DEV) for _ in range(2))
+    y1, y2 = (torch.empty(96, 256, dtype=torch.uint8, device=DEV) for _ in range(2))
+    ext.fp8_quant(x, y1, qs, am1, fmt)
+    ext.fp8_quant(x.contiguous(), y2, qs, am2, fmt)
+    bad = (y1 != y2).float().mean().item() + float(am1.item() != am2.item())
+    return (f"fp8 quant strided == dense fmt{fmt}", bad, 0.0)
+
+
+def check_fp8_weight_batch():
+    """The per-step multi-tensor weight refresh gives the bytes / scales of per-weight current scaling."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    st = F8.Fp8State(1, DEV)
+    ws = [bf(rnd(256, 384, scale=0.05)), bf(rnd(384, 256, scale=0.2)), bf(rnd(64, 1024, scale=3.0))]
+    for i, w in enumerate(ws):
+        st.weight(w, i, 1)  # first generation: per-weight path, records the set
+    for w in ws:
+        w.mul_(1.7).add_(0.01)  # the optimizer's update of the bf16 shadows (same storage)
+    bad = 0.0
+    for i, w in enumerate(ws):
+        q, ds = st.weight(w, i, 2)  # first call runs the batched refresh of all three
+        meta = F8.Fp8Meta(1, DEV, history=1)
+        qr, dsr = meta.quantize(w, 0, current=True)
+        bad += (q != qr).float().mean().item() + abs(ds.item() - dsr.item()) / dsr.item()
+    ok_batched = st._batch_gen == 2
+    return ("fp8 batched weight refresh == per-weight quantization", bad + (0 if ok_batched else 1), 1e-6)
+
+
 def _fp8_operand(x, fmt=0):
     from pytorch_vit_paper_replication_amd.ops import fp8 as F8
 
@@ -699,6 +733,9 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_bwd(1, 300, 2, 128),
         lambda: check_attn_bwd(1, 100, 2, 96),
         lambda: check_fp8_format(0),
+        lambda: check_fp8_strided(0),
+        lambda: check_fp8_strided(1),
+        lambda: check_fp8_weight_batch(),
         lambda: check_fp8_format(1),
         lambda: check_gemm_fp8(3000, 768, 1280),
         lambda: check_gemm_fp8(700, 2304, 768, True, False),
