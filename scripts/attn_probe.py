@@ -19,6 +19,9 @@ for _ in range(3):
     if which in ("fwd", "both"):
         ext.attn_fwd(qkv, B, N, H, 0.125)
     if which in ("bwd", "both"):
-        ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125)
+        # with the in-step bias partials when the pipelined backward serves the shape
+        part = (torch.empty(B * H, (N + 31) // 32, 192, device="cuda", dtype=torch.float32)
+                if ext.attn_bwd_pipe_path(B, N, H, D) else None)
+        ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125, None, part)
 torch.cuda.synchronize()
 print("ok")
