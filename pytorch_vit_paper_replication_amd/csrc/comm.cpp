@@ -23,6 +23,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "comm_core.h"
+
+extern "C" hipError_t pvr_sum_chunks(float* dst, const float* src, int k, int64_t n, int64_t stride, float scale, hipStream_t s);
+
 namespace pvr_comm {
 namespace {
 
@@ -36,6 +40,10 @@ struct Api {
   decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   decltype(&ncclGetVersion) get_version = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
   bool ok = false;
   std::string err;
 };
@@ -69,6 +77,10 @@ const Api& api() {
     sym(h, "ncclAllGather", r.all_gather, r.err);
     sym(h, "ncclGetErrorString", r.error_string, r.err);
     sym(h, "ncclGetVersion", r.get_version, r.err);
+    sym(h, "ncclSend", r.send, r.err);
+    sym(h, "ncclRecv", r.recv, r.err);
+    sym(h, "ncclGroupStart", r.group_start, r.err);
+    sym(h, "ncclGroupEnd", r.group_end, r.err);
     r.ok = r.err.empty();
     return r;
   }();
@@ -105,6 +117,29 @@ ncclDataType_t dtype_of(const torch::Tensor& t) {
   }
   return ncclFloat32;
 }
+
+// comm_core.h's Transport over RCCL: grouped ncclSend / ncclRecv on the communicator's stream
+// (all world-1 peers of a phase at once: every xGMI link busy), local sums by a HIP kernel.
+class RcclTransport : public Transport {
+ public:
+  RcclTransport(ncclComm_t comm, hipStream_t stream, int rank, int world) : comm_(comm), stream_(stream), rank_(rank), world_(world) {}
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void group_start() override { nccl_check(api().group_start(), "ncclGroupStart"); }
+  void group_end() override { nccl_check(api().group_end(), "ncclGroupEnd"); }
+  void send(const void* buf, size_t bytes, int peer) override {
+    nccl_check(api().send(buf, bytes, ncclUint8, peer, comm_, stream_), "ncclSend");
+  }
+  void recv(void* buf, size_t bytes, int peer) override { nccl_check(api().recv(buf, bytes, ncclUint8, peer, comm_, stream_), "ncclRecv"); }
+  void sum_into(float* dst, const float* src, int k, size_t n, size_t stride, float scale) override {
+    hip_check(pvr_sum_chunks(dst, src, k, (int64_t)n, (int64_t)stride, scale, stream_), "sum_chunks");
+  }
+
+ private:
+  ncclComm_t comm_;
+  hipStream_t stream_;
+  int rank_, world_;
+};
 
 }  // namespace
 
@@ -155,6 +190,27 @@ class Communicator {
     nccl_check(api().all_reduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), average ? ncclAvg : ncclSum, comm_,
                                 stream_.stream()),
                "ncclAllReduce");
+    return finish(h);
+  }
+
+  // The same all-reduce with the framework's own schedule (comm_core.h mesh: reduce-scatter and
+  // all-gather as grouped point-to-point transfers to every peer at once) instead of RCCL's
+  // all-reduce algorithm; fp32 only. Its slicing / peer logic is unit-tested on a fake transport
+  // (tests/cpp/test_comm_core.cpp).
+  int64_t all_reduce_mesh_async(torch::Tensor t, bool average) {
+    live();
+    check_tensor(t);
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32, "mesh all-reduce: fp32 tensors");
+    const size_t n = (size_t)t.numel();
+    const size_t need = (size_t)(world_ > 1 ? world_ - 1 : 0) * max_chunk(n, world_);
+    if (need > 0 && (!scratch_.defined() || (size_t)scratch_.numel() < need)) {
+      // grown rarely: earlier collectives on the (in-order) comm stream may still read the old one
+      hip_check(hipStreamSynchronize(stream_.stream()), "hipStreamSynchronize");
+      scratch_ = torch::empty({(int64_t)need}, torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device_));
+    }
+    const int64_t h = gate();
+    RcclTransport tr(comm_, stream_.stream(), rank_, world_);
+    mesh_all_reduce(tr, t.data_ptr<float>(), n, need ? scratch_.data_ptr<float>() : nullptr, average);
     return finish(h);
   }
 
@@ -258,7 +314,7 @@ class Communicator {
   ncclComm_t comm_ = nullptr;
   std::vector<hipEvent_t> events_, ready_;
   int64_t issued_ = 0;
-  torch::Tensor one_;
+  torch::Tensor one_, scratch_;
 };
 
 void register_comm(pybind11::module& m) {
@@ -279,6 +335,7 @@ void register_comm(pybind11::module& m) {
            }),
            py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
       .def("all_reduce_async", &Communicator::all_reduce_async, py::arg("tensor"), py::arg("average") = true)
+      .def("all_reduce_mesh_async", &Communicator::all_reduce_mesh_async, py::arg("tensor"), py::arg("average") = true)
       .def("all_gather_async", &Communicator::all_gather_async)
       .def("reduce_scatter_async", &Communicator::reduce_scatter_async, py::arg("input"), py::arg("output"),
            py::arg("average") = true)

@@ -36,7 +36,11 @@ class NativeCommunicator:
         return cls(ext.Communicator(obj[0], rank, world, idx), device)
 
     # all collectives are stream-ordered and asynchronous; wait(h) joins them into the caller's stream
-    def all_reduce(self, t: torch.Tensor, average: bool = True) -> int:
+    def all_reduce(self, t: torch.Tensor, average: bool = True, algo: str = "rccl") -> int:
+        """``algo="mesh"``: the framework's own schedule (csrc/comm_core.h: reduce-scatter + all-gather
+        as grouped point-to-point transfers to every peer at once, fp32); else RCCL's all-reduce."""
+        if algo == "mesh":
+            return self._c.all_reduce_mesh_async(t, average)
         return self._c.all_reduce_async(t, average)
 
     def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor, average: bool = True) -> int:

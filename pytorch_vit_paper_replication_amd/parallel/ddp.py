@@ -63,6 +63,9 @@ class DistributedDataParallel(nn.Module):
         self._comm_mode = comm
         self._native = None          # parallel.comm.NativeCommunicator when the native transport is used
         self._comm_buf: Optional[torch.Tensor] = None  # persistent low-precision gradient mirror
+        # native transport's all-reduce schedule: "rccl" (RCCL's algorithm) or "mesh" (PVR_COMM_ALGO=mesh:
+        # csrc/comm_core.h grouped point-to-point reduce-scatter + all-gather over every xGMI link)
+        self._algo = os.environ.get("PVR_COMM_ALGO", "rccl")
 
     def _pick_transport(self, device):
         mode = os.environ.get("PVR_COMM", self._comm_mode)
@@ -191,7 +194,7 @@ class DistributedDataParallel(nn.Module):
                 tmp.copy_(buf)
                 self._works.append((self._native.all_reduce(tmp), buf, tmp))
             else:
-                self._works.append((self._native.all_reduce(buf), buf, None))
+                self._works.append((self._native.all_reduce(buf, algo=self._algo), buf, None))
             return
         if self.comm_dtype is not None and self.comm_dtype != buf.dtype:
             tmp = buf.to(self.comm_dtype)

@@ -180,6 +180,10 @@ def test_native_communicator_collectives_world1():
                             device_id=dev)
     try:
         c = NativeCommunicator.create(dev)
+        xm = torch.randn(1000, device=dev)
+        xm_ref = xm.clone()
+        c.wait(c.all_reduce(xm, average=True, algo="mesh"))  # world 1: the mesh schedule is the identity
+        assert torch.equal(xm, xm_ref)
         x = torch.randn(1 << 20, device=dev)
         ref = x.clone()
         x.mul_(2.0)  # queued on the compute stream: the all-reduce must observe it
