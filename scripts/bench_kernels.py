@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--tiles", default="0,1,2")
     ap.add_argument("--only", default="gemm,attn,ln")
+    ap.add_argument("--attn-shape", default="197,12,64", help="N,H,dh of the attention cases (batch: --batch)")
     a = ap.parse_args()
     dev = "cuda"
     T = a.batch * 197
@@ -142,24 +143,25 @@ def main():
                   flush=True)
     if "attn" in a.only:
         ext = _ext.ext()
-        B, N, H = a.batch, 197, 12
-        qkv = torch.randn(B * N, 3 * D, device=dev, dtype=torch.bfloat16)
-        fl = 4.0 * B * H * N * N * 64
-        tt = timeit(lambda: ext.attn_fwd(qkv, B, N, H, 0.125))
-        q, k, v = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4).contiguous()
+        N, H, dh = (int(v) for v in a.attn_shape.split(","))
+        B, Da, sc = a.batch, H * dh, dh ** -0.5
+        qkv = torch.randn(B * N, 3 * Da, device=dev, dtype=torch.bfloat16)
+        fl = 4.0 * B * H * N * N * dh
+        tt = timeit(lambda: ext.attn_fwd(qkv, B, N, H, sc))
+        q, k, v = qkv.view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4).contiguous()
         t_lib = timeit(lambda: F.scaled_dot_product_attention(q, k, v))
         print(f"attn_fwd B{B} N{N} H{H}: ours {tt:.3f} ms {fl / tt / 1e9:.1f} TF | sdpa {t_lib:.3f} ms x{t_lib / tt:.2f}", flush=True)
-        o, lse = ext.attn_fwd(qkv, B, N, H, 0.125)
+        o, lse = ext.attn_fwd(qkv, B, N, H, sc)
         do = torch.randn_like(o)
-        tt = timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125))
+        tt = timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, sc))
         qr, kr, vr = (t.detach().requires_grad_(True) for t in (q, k, v))
         orf = F.scaled_dot_product_attention(qr, kr, vr)
         dor = torch.randn_like(orf)
         t_lib = timeit(lambda: torch.autograd.grad(orf, (qr, kr, vr), dor, retain_graph=True))
         print(f"attn_bwd B{B} N{N} H{H}: ours {tt:.3f} ms {2.5 * fl / tt / 1e9:.1f} TF | sdpa {t_lib:.3f} ms x{t_lib / tt:.2f}", flush=True)
-        if ext.attn_bwd_pipe_path(B, N, H, H * 64):
+        if ext.attn_bwd_pipe_path(B, N, H, Da):
             part = torch.empty(B * H, (N + 31) // 32, 192, device=dev, dtype=torch.float32)
-            tb = timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, 0.125, None, part))
+            tb = timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, sc, None, part))
             print(f"attn_bwd+dbias B{B} N{N} H{H}: ours {tb:.3f} ms (bias partials in-kernel)", flush=True)
     if "ln" in a.only:
         ext = _ext.ext()
