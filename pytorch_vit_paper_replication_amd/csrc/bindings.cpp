@@ -39,6 +39,7 @@ hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
 hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, int, const float*, unsigned*, int, hipStream_t);
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
+hipError_t pvr_fp8_quant_t(const uint16_t*, int64_t, uint8_t*, int64_t, int, int, const float*, int, hipStream_t);
 hipError_t pvr_fp8_quant_multi(const int64_t*, int, int64_t, const float*, unsigned*, int, int, hipStream_t);
 int pvr_attn_bwd_key_blocks(int);
 int pvr_attn_bwd_needs_dq_acc(int, int, int);
@@ -351,6 +352,40 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
   check(pvr_gemm(&p, stream()), "gemm_fp8");
 }
 
+// yT[cols][ldy] (uint8 fp8) = sat(x^T * qscale), zero past x's rows (ldy: token dim padded to 128)
+void fp8_quant_t(torch::Tensor x, torch::Tensor yt, torch::Tensor qscale, int64_t fmt) {
+  TORCH_CHECK(x.dim() == 2 && yt.dim() == 2 && yt.size(0) == x.size(1) && yt.size(1) >= x.size(0) && yt.stride(1) == 1,
+              "fp8_quant_t: yT [cols][>= rows]");
+  TORCH_CHECK(yt.is_cuda() && yt.scalar_type() == torch::kUInt8 && yt.stride(0) % 64 == 0 && yt.size(1) == yt.stride(0),
+              "fp8_quant_t: yT uint8, row stride a multiple of 64");
+  check(pvr_fp8_quant_t(bf(x, "x"), ld_of(x, "x"), yt.data_ptr<uint8_t>(), yt.stride(0), (int)x.size(0), (int)x.size(1),
+                        f32(qscale, "qscale"), (int)fmt, stream()),
+        "fp8_quant_t");
+}
+
+// fp8 weight gradient partials: ws[s][N][K] = dscale_a * dscale_b * A8[N][Ks] . B8[K][Ks]^T over split s
+// of the (padded) token dim, A e5m2 (gradient^T), B e4m3 (activation^T)
+void gemm_fp8_wgrad(torch::Tensor A8, torch::Tensor B8, torch::Tensor ws, int64_t N, int64_t K, int64_t Tp, torch::Tensor scale_a,
+                    torch::Tensor scale_b, int64_t ksplit) {
+  pvr::GemmParams p{};
+  p.drop_scale = 1.f;
+  p.M = (int)N; p.N = (int)K; p.K = (int)Tp;
+  p.A = reinterpret_cast<const uint16_t*>(u8(A8, "A8")); p.lda = A8.stride(0); p.a_kcontig = 1;
+  p.B = reinterpret_cast<const uint16_t*>(u8(B8, "B8")); p.ldb = B8.stride(0); p.b_kcontig = 1;
+  TORCH_CHECK(A8.size(0) >= N && A8.size(1) >= Tp && B8.size(0) >= K && B8.size(1) >= Tp, "gemm_fp8_wgrad: operand too small");
+  TORCH_CHECK(Tp % 128 == 0 && ksplit % 128 == 0 && K % 8 == 0, "gemm_fp8_wgrad: Tp, ksplit multiples of 128");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.dim() == 3 && ws.stride(2) == 1 && ws.size(1) >= N &&
+                  ws.size(2) >= K && ws.size(0) >= (Tp + ksplit - 1) / ksplit,
+              "gemm_fp8_wgrad: workspace [splits][N][K] f32");
+  p.C = ws.data_ptr(); p.ldc = ws.stride(1); p.split_stride = ws.stride(0);
+  p.scale_a = f32(scale_a, "scale_a"); p.scale_b = f32(scale_b, "scale_b");
+  p.elem8 = 1; p.fmt_a = 1; p.fmt_b = 0;
+  p.k_split_len = (int)ksplit;
+  p.epi = 4;  // EPI_F32_STORE
+  p.tile_cfg = 14;
+  check(pvr_gemm(&p, stream()), "gemm_fp8_wgrad");
+}
+
 // y[rows][cols] (uint8 fp8) = sat(x * qscale); amax (int32 holding float bits) = max(amax, max|x|).
 // y / qscale None: amax only.
 void fp8_quant(torch::Tensor x, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> qscale, torch::Tensor amax, int64_t fmt) {
@@ -528,6 +563,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);
+  m.def("fp8_quant_t", &fp8_quant_t);
+  m.def("gemm_fp8_wgrad", &gemm_fp8_wgrad);
   m.def("fp8_quant_multi", &fp8_quant_multi, py::arg("segs"), py::arg("nchunks"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"),
         py::arg("amax_only"));
   m.def("attn_fwd", &attn_fwd);

@@ -159,6 +159,45 @@ __global__ void __launch_bounds__(256) quant_multi_kernel(const int64_t* __restr
   }
 }
 
+// Transposing quantize for the fp8 weight-gradient GEMM: x bf16 [T][C] (row stride ldx) ->
+// y fp8 [C][ldy] with y[c][t] = sat(x[t][c] * qscale) for t < T and 0 for T <= t < ldy (the GEMM's
+// reduction dim padded to a multiple of 128). 64 x 64 tiles through LDS; reads and writes are
+// 16-B per thread. No amax: the tensor's amax is recorded by its non-transposed quantize pass.
+template <int FMT>
+__global__ void __launch_bounds__(256) quant_t_kernel(const uint16_t* __restrict__ x, int64_t ldx, uint8_t* __restrict__ y, int64_t ldy,
+                                                      int T, int C, const float* __restrict__ qscale) {
+  __shared__ uint16_t tile[64][64 + 8];
+  const int t0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  const float qs = *qscale;
+  {  // load: row t0 + tid/4, cols c0 + 16 (tid%4) .. +15
+    const int r = tid >> 2, cc = (tid & 3) * 16;
+    const int t = t0 + r;
+    uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+    if (t < T && c0 + cc < C) {  // C % 16 == 0 (host check)
+      const uint16_t* src = x + (int64_t)t * ldx + c0 + cc;
+      a = *(const uint4*)src;
+      b = *(const uint4*)(src + 8);
+    }
+    *(uint4*)&tile[r][cc] = a;
+    *(uint4*)&tile[r][cc + 8] = b;
+  }
+  __syncthreads();
+  // store: output row c0 + tid/4, t range t0 + 16 (tid%4) .. +15 (16 fp8 bytes)
+  const int c = tid >> 2, tt = (tid & 3) * 16;
+  if (c0 + c >= C || t0 + tt >= ldy) return;
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = bf2f(tile[tt + j][c]) * qs;
+  int o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int w = pack2_fp8<FMT, false>(v[4 * q], v[4 * q + 1], 0);
+    o[q] = pack2_fp8<FMT, true>(v[4 * q + 2], v[4 * q + 3], w);
+  }
+  *(int4*)(y + (int64_t)(c0 + c) * ldy + t0 + tt) = make_int4(o[0], o[1], o[2], o[3]);
+}
+
 // fp8 -> f32 (tests / debugging): y[i] = dscale * x[i]
 template <int FMT>
 __global__ void dequant_kernel(const uint8_t* __restrict__ x, float* __restrict__ y, int64_t n, const float* __restrict__ dscale) {
@@ -232,6 +271,19 @@ extern "C" hipError_t pvr_fp8_quant_multi(const int64_t* segs, int nseg, int64_t
     hipLaunchKernelGGL((quant_multi_kernel<0, false>), dim3(grid), dim3(256), 0, s, segs, nseg, nchunks, qscale, amax);
   else
     hipLaunchKernelGGL((quant_multi_kernel<1, false>), dim3(grid), dim3(256), 0, s, segs, nseg, nchunks, qscale, amax);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_fp8_quant_t(const uint16_t* x, int64_t ldx, uint8_t* y, int64_t ldy, int T, int C, const float* qscale, int fmt,
+                                      hipStream_t s) {
+  using namespace pvr;
+  if (T <= 0 || C <= 0) return hipSuccess;
+  if (C % 16 || ldy % 64 || ldy < T) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(ldy / 64), (unsigned)((C + 63) / 64));
+  if (fmt == 0)
+    hipLaunchKernelGGL(quant_t_kernel<0>, grid, dim3(256), 0, s, x, ldx, y, ldy, T, C, qscale);
+  else
+    hipLaunchKernelGGL(quant_t_kernel<1>, grid, dim3(256), 0, s, x, ldx, y, ldy, T, C, qscale);
   return hipGetLastError();
 }
 

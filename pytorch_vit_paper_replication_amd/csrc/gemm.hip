@@ -1442,9 +1442,15 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
   const GemmParams& p = *pp;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return hipSuccess;
   const bool ak = p.a_kcontig, bk = p.b_kcontig;
-  if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad e5m2 x e4m3)
-    if (!ak || !bk || p.K % 128 != 0 || p.k_split_len < p.K || (p.N & 3) || !p.scale_a || !p.scale_b) return hipErrorInvalidValue;
+  if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad / wgrad e5m2 x e4m3)
     const int f = p.fmt_a * 2 + p.fmt_b;
+    if (!ak || !bk || p.K % 128 != 0 || (p.N & 3) || !p.scale_a || !p.scale_b) return hipErrorInvalidValue;
+    if (p.epi == EPI_F32_STORE) {
+      // weight gradient: split-K over the (128-padded) token dim, per-split partials (tile 14)
+      if (p.tile_cfg != 14 || p.k_split_len % 128 != 0 || f != 2) return hipErrorInvalidValue;
+      return launch_pp<true, true, true, EPI_F32_STORE, 1, 1, 0>(p, s);
+    }
+    if (p.k_split_len < p.K) return hipErrorInvalidValue;
     switch (p.epi) {
       case EPI_BF16:
         if (f == 0) return launch_pp<true, true, true, EPI_BF16, 1, 0, 0>(p, s);

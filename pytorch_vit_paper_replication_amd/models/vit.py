@@ -277,7 +277,8 @@ class ViT(nn.Module):
                             head.weight, head.bias)
 
     # ------------------------------------------------------------------ fp8
-    def enable_fp8(self, enabled: bool = True, history: int = 16, margin: int = 0, dgrad: bool = True) -> "ViT":
+    def enable_fp8(self, enabled: bool = True, history: int = 16, margin: int = 0, dgrad: bool = True,
+                   wgrad: bool = True) -> "ViT":
         """Run the encoder's GEMMs in fp8 on the fused MI355X path (ops/fp8.py), per-tensor delayed
         scaling with an amax history of ``history`` steps:
 
@@ -285,11 +286,14 @@ class ViT(nn.Module):
         * ``dgrad=True`` (default): the backward's activation-gradient GEMMs too, e5m2 gradients x
           e4m3 transposed weights. This changes the backward numerics (``tests/kernel_checks.py``
           ``check_vit_fp8_dgrad`` pins the per-tensor error); ``dgrad=False`` keeps them bf16;
-        * weight gradients, attention, LayerNorm and the optimizer stay bf16 / fp32.
+        * ``wgrad=True`` (default, with ``dgrad``): the weight-gradient GEMMs too, e5m2 gradients^T x
+          e4m3 activations^T (transposed quantize passes with the same slots' scales) from the
+          second step on (``check_vit_fp8_wgrad`` pins the per-tensor error);
+        * attention, LayerNorm, the patch embedding / head GEMMs and the optimizer stay bf16 / fp32.
 
         The constructor signature stays the reference's; fp8 is opt-in."""
         old = getattr(self, "_fp8_cfg", None)
-        cfg = (history, margin, bool(dgrad)) if enabled else None
+        cfg = (history, margin, bool(dgrad), bool(wgrad)) if enabled else None
         object.__setattr__(self, "_fp8_cfg", cfg)
         if cfg is None or old is None or old[:2] != cfg[:2]:
             object.__setattr__(self, "_fp8", None)  # new scaling state; only a dgrad switch keeps the histories
@@ -306,9 +310,10 @@ class ViT(nn.Module):
             return None
         st = getattr(self, "_fp8", None)
         if st is None or st.device != device:
-            st = F8.Fp8State(c["num_transformer_layer"], device, history=cfg[0], margin=cfg[1], dgrad=cfg[2])
+            st = F8.Fp8State(c["num_transformer_layer"], device, history=cfg[0], margin=cfg[1], dgrad=cfg[2], wgrad=cfg[3])
             object.__setattr__(self, "_fp8", st)
         st.dgrad = cfg[2]
+        st.wgrad = cfg[3] and cfg[2]
         return st
 
     def num_params(self) -> int:

@@ -14,8 +14,10 @@ Recipe (the usual delayed-scaling scheme, all state on the device):
 
 Forward GEMMs use e4m3 x e4m3. With ``dgrad=True`` (``ViT.enable_fp8``'s default) the four
 activation-gradient (dgrad) GEMMs of each encoder block also run in fp8: e5m2 gradients (own
-delayed-scaling slots) x e4m3 transposed weights (``linear_dgrad_fp8``). LayerNorm, softmax,
-attention, residual adds, the weight-gradient GEMMs and the optimizer stay in bf16 / fp32.
+delayed-scaling slots) x e4m3 transposed weights (``linear_dgrad_fp8``); with ``wgrad=True`` (also
+the default) the four weight-gradient GEMMs too: e5m2 gradients^T x e4m3 activations^T from
+transposing quantize passes (``linear_wgrad_fp8``, split-K over tokens). LayerNorm, softmax,
+attention, residual adds and the optimizer stay in bf16 / fp32.
 Non-finite values: a NaN/Inf element makes its tensor's amax non-finite; the scale update then
 leaves that slot's history and scales unchanged (csrc/fp8.hip), and FusedAdam skips the step.
 """
@@ -72,11 +74,12 @@ class Fp8State:
 
     ACT_PER_BLOCK = 4  # xn1 (qkv input), o (out-proj input), xn2 (fc1 input), h (fc2 input)
 
-    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0, dgrad: bool = True):
+    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0, dgrad: bool = True, wgrad: bool = True):
         self.act = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E4M3)
         # e5m2 gradient slots for the fp8 dgrad GEMMs (dgrad=True): dz2, dU, dx1, dQKV per block
         self.grad = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E5M2)
         self.dgrad = bool(dgrad)
+        self.wgrad = bool(wgrad) and bool(dgrad)  # fp8 weight gradients reuse the dgrad gradient slots
         self.n_blocks = n_blocks
         self._wmeta: Optional[Fp8Meta] = None
         self._wslot: Dict[int, int] = {}
@@ -96,6 +99,17 @@ class Fp8State:
 
     def grad_quant(self, g: torch.Tensor, block: int, which: int) -> Tuple[torch.Tensor, torch.Tensor]:
         return self.grad.quantize(g, block * self.ACT_PER_BLOCK + which)
+
+    def wgrad_ready(self, block: int, which_grad: int, which_act: int) -> bool:
+        """fp8 weight gradient of (grad slot, activation slot) possible: both slots calibrated (the
+        first step, which calibrates the gradient slots, computes its weight gradients in bf16)."""
+        return (self.wgrad and self.grad.calibrated[block * self.ACT_PER_BLOCK + which_grad]
+                and self.act.calibrated[block * self.ACT_PER_BLOCK + which_act])
+
+    def linear_wgrad(self, dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, block: int, which_grad: int,
+                     which_act: int) -> torch.Tensor:
+        n = self.ACT_PER_BLOCK
+        return linear_wgrad_fp8(dy, self.grad, block * n + which_grad, x, self.act, block * n + which_act, out)
 
     def weight(self, w16: torch.Tensor, key: int, generation: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """fp8 (e4m3, current scaling) copy of a bf16 weight shadow, cached per store generation.
@@ -179,6 +193,31 @@ def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts:
         out = torch.empty(T, K, dtype=torch.bfloat16, device=gq.device)
     epi = gemm.EPI_DGELU if dgelu_aux is not None else gemm.EPI_BF16
     _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum)
+    return out
+
+
+def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torch.Tensor, x_meta: "Fp8Meta", x_slot: int,
+                     out: torch.Tensor) -> torch.Tensor:
+    """out[N, K] += dequant(dy^T (e5m2) . x (e4m3)) over the tokens: the weight gradient in fp8.
+
+    Both operands are quantized TRANSPOSED ([features][tokens], the token dim padded to 128 with
+    zeros) with their slots' current delayed scales (the slots' amax is recorded by the
+    non-transposed passes of the same tensors), then the k-contiguous fp8 ping-pong GEMM runs
+    split-K over tokens into a workspace, reduced into ``out`` in a fixed order (deterministic)."""
+    ext = _ext.ext()
+    T, N = dy.shape
+    K = x.shape[1]
+    Tp = (T + 127) // 128 * 128
+    dyt = torch.empty(N, Tp, dtype=torch.uint8, device=dy.device)
+    xt = torch.empty(K, Tp, dtype=torch.uint8, device=dy.device)
+    ext.fp8_quant_t(dy, dyt, dy_meta.qscale[dy_slot:dy_slot + 1], E5M2)
+    ext.fp8_quant_t(x, xt, x_meta.qscale[x_slot:x_slot + 1], E4M3)
+    splits = gemm.wgrad_splits(T, N, K, 12)
+    ksplit = max(128, (Tp // splits + 127) // 128 * 128)
+    nsplit = (Tp + ksplit - 1) // ksplit
+    ws = gemm._workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
+    ext.gemm_fp8_wgrad(dyt, xt, ws, N, K, Tp, dy_meta.dscale[dy_slot:dy_slot + 1], x_meta.dscale[x_slot:x_slot + 1], ksplit)
+    ext.splitk_reduce(ws, nsplit, out, True)
     return out
 
 

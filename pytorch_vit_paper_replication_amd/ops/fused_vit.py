@@ -270,6 +270,13 @@ class EncoderBlockFn(torch.autograd.Function):
                 DGRAD_TAP(which, out)
             return out
 
+        def wgrad(dy, x, gw, which_grad, which_act):
+            # fp8 weight gradient (e5m2 dy^T x e4m3 x) once the slots are calibrated, else bf16
+            if f8d is not None and f8d[0].wgrad_ready(f8d[1], which_grad, which_act) and dy.shape[0] >= 256:
+                f8d[0].linear_wgrad(dy, x, gw, f8d[1], which_grad, which_act)
+            else:
+                gemm.linear_wgrad(dy, x, gw)
+
         # ---- MLP branch: x2 = x1 + drop2(h . W2^T + b2),  h = drop1(gelu(u)),  u = xn2 . W1^T + b1
         if own is not None and own.done:
             # the next block's LayerNorm backward already produced dz2 and d(b2)
@@ -288,16 +295,16 @@ class EncoderBlockFn(torch.autograd.Function):
         gw2, gw1 = g(w2), g(w1)
         early = EARLY_WGRAD
         if early and gw2 is not None:  # dW2 = dz2^T h needs nothing from this block's dgrads
-            store.on_side(lambda: gemm.linear_wgrad(dz2, h, gw2), dz2, h)
+            store.on_side(lambda: wgrad(dz2, h, gw2, 0, 3), dz2, h)
         du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=None if side_b1 else gb1)
 
         def mlp_wgrads():
             if side_b1:
                 gemm.bias_grad(du, gb1)
             if gw2 is not None and not early:
-                gemm.linear_wgrad(dz2, h, gw2)
+                wgrad(dz2, h, gw2, 0, 3)
             if gw1 is not None:
-                gemm.linear_wgrad(du, xn2, gw1)
+                wgrad(du, xn2, gw1, 1, 2)
 
         store.on_side(mlp_wgrads, dz2, h, du, xn2)  # weight grads off the critical path
         dxn2 = dgrad(du, w1, 1)
@@ -308,7 +315,7 @@ class EncoderBlockFn(torch.autograd.Function):
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
         gwo, gwqkv = g(wo), g(wqkv)
         if early and gwo is not None:  # dWo = dx1^T o: ready as soon as dx1 is
-            store.on_side(lambda: gemm.linear_wgrad(dx1, o, gwo), dx1, o)
+            store.on_side(lambda: wgrad(dx1, o, gwo, 2, 1), dx1, o)
         do = dgrad(dx1, wo, 2)
         # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
         gbqkv = g(bqkv)
@@ -336,9 +343,9 @@ class EncoderBlockFn(torch.autograd.Function):
             if side_db:
                 gemm.bias_grad(dqkv, gbqkv)
             if gwo is not None and not early:
-                gemm.linear_wgrad(dx1, o, gwo)
+                wgrad(dx1, o, gwo, 2, 1)
             if gwqkv is not None:
-                gemm.linear_wgrad(dqkv, xn1, gwqkv)
+                wgrad(dqkv, xn1, gwqkv, 3, 0)
 
         store.on_side(attn_wgrads, dx1, o, dqkv, xn1, *(() if db_part is None else (db_part,)))
         dxn1 = dgrad(dqkv, wqkv, 3)

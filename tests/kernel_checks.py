@@ -346,6 +346,30 @@ def check_gemm_fp8(M, N, K, resid=False, gelu=False):
     return (f"gemm_fp8 e4m3 M{M} N{N} K{K} r{int(resid)} g{int(gelu)} (vs bf16 {e_b:.2e})", max(e_q, e_b / 5), 2e-2)
 
 
+def check_wgrad_fp8(T, N, K):
+    """dW = dequant(dy^T (e5m2) . x (e4m3)) from the transposed quantize passes + split-K fp8 GEMM,
+    against the exact product of the same quantized operands and against bf16."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    dy, x = bf(rnd(T, N)), bf(rnd(T, K))
+    gm, am = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2), F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+    _, gs = gm.quantize(dy, 0, current=True)
+    _, xs = am.quantize(x, 0, current=True)
+    out = torch.zeros(N, K, device=DEV)
+    F8.linear_wgrad_fp8(dy, gm, 0, x, am, 0, out)
+    # reference from the same fp8 values (non-transposed quantize, dequantized)
+    ext = _ext.ext()
+    q1 = torch.empty(T, N, dtype=torch.uint8, device=DEV)
+    q2 = torch.empty(T, K, dtype=torch.uint8, device=DEV)
+    ext.fp8_quant(dy, q1, gm.qscale[0:1], gm.amax[0:1], F8.E5M2)
+    ext.fp8_quant(x, q2, am.qscale[0:1], am.amax[0:1], F8.E4M3)
+    dyd = ext.fp8_dequant(q1, gs, F8.E5M2).view(T, N)
+    xd = ext.fp8_dequant(q2, xs, F8.E4M3).view(T, K)
+    e_q = rel_err(out, dyd.t() @ xd)
+    e_b = rel_err(out, dy.float().t() @ x.float())
+    return (f"wgrad_fp8 e5m2^T x e4m3 T{T} N{N} K{K} (vs bf16 {e_b:.2e})", max(e_q, e_b / 5), 2e-2)
+
+
 def check_dgrad_fp8(M, N, K):
     """dX = dequant(g (e5m2) . W (e4m3)) with the dGELU epilogue and the fused bias-grad column sum."""
     from pytorch_vit_paper_replication_amd.ops import fp8 as F8
@@ -444,6 +468,49 @@ def check_vit_fp8_dgrad(B=4):
     ok = losses[-1] < losses[0] and all(math.isfinite(v) for v in losses) and len(errs) == 4 * cfg["num_transformer_layer"]
     return (f"vit fp8 dgrad per-tensor vs bf16 dgrad (max {worst:.2e}), loss {losses[0]:.3f}->{losses[-1]:.3f}",
             worst + (0 if ok else 1), 1.2e-1)  # e5m2 (2 mantissa bits) x e4m3: measured 6.1-9.4e-2 per tensor
+
+
+def check_vit_fp8_wgrad(B=4):
+    """fp8 weight-gradient GEMMs (enable_fp8(wgrad=True): e5m2 dy^T x e4m3 x^T) against the bf16 weight
+    gradients of the same fp8 model (identical calibrated passes, fp8 dgrads in both), per encoder
+    GEMM weight; then training with them must decrease the loss. Errors printed into the test log."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=256, mlp_size=512,
+               num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0)
+    m = ViT(**cfg).to(DEV).enable_fp8(dgrad=True, wgrad=True)
+    x = torch.rand(B * 64, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B * 64,), device=DEV)
+    names = [n for n, p in m.named_parameters() if p.dim() == 2 and "encoder" in n]
+
+    def run(wgrad_fp8: bool):
+        m.enable_fp8(dgrad=True, wgrad=wgrad_fp8)  # keeps the calibrated scaling state
+        m.zero_grad(set_to_none=False)
+        cross_entropy(m(x), y).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.float().clone() for n, p in m.named_parameters() if n in names}
+
+    run(True)  # calibrates every slot; weight gradients of this first pass are bf16
+    ref = run(False)
+    f8 = run(True)
+    errs = [(n, ((f8[n] - ref[n]).norm() / ref[n].norm().clamp_min(1e-30)).item()) for n in names]
+    worst = max(e for _, e in errs)
+    print("fp8 wgrad per-tensor rel-L2 vs bf16 wgrad: " + ", ".join(f"{n.split('.')[-2]}.{n.split('.')[-1]} {e:.3e}" for n, e in errs))
+    m.enable_fp8(dgrad=True, wgrad=True)
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(6):
+        loss = cross_entropy(m(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step(clip_norm=1.0)
+        losses.append(loss.item())
+    ok = losses[-1] < losses[0] and all(math.isfinite(v) for v in losses) and len(errs) == 4 * cfg["num_transformer_layer"]
+    return (f"vit fp8 wgrad per-tensor vs bf16 wgrad (max {worst:.2e}), loss {losses[0]:.3f}->{losses[-1]:.3f}",
+            worst + (0 if ok else 1), 1.2e-1)
 
 
 def check_fp8_nonfinite_recovery(B=2):
@@ -736,6 +803,9 @@ def all_checks() -> List[Callable]:
         lambda: check_fp8_strided(0),
         lambda: check_fp8_strided(1),
         lambda: check_fp8_weight_batch(),
+        lambda: check_wgrad_fp8(1000, 1280, 512),
+        lambda: check_wgrad_fp8(32896, 1280, 3840),
+        lambda: check_vit_fp8_wgrad(),
         lambda: check_fp8_format(1),
         lambda: check_gemm_fp8(3000, 768, 1280),
         lambda: check_gemm_fp8(700, 2304, 768, True, False),
