@@ -438,7 +438,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   char* qdo = kimg + KB * RB;
   char* dsimg = qdo + 6 * QB * RB;
   float* s_ld = (float*)(dsimg + QB * KB * 2);
-  const int ds_cpr = KB / 8;  // 16-B chunks per dS row (power of two)
+  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+  // dS^T image [key_local][32 queries]: 64-B rows of 8-B units (4 queries), unit XOR (key>>1)&7
+  auto ds_off = [](int key, int u) { return key * 64 + ((u ^ ((key >> 1) & 7)) << 3); };
+  const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int dsw0 = wave * 2048 + ds_off(li, g), dsw1 = wave * 2048 + ds_off(li, 4 + g);  // f adds 1024
 
   const uint16_t* base = qkv + (int64_t)b * N * ld;
   const int64_t extent = ((int64_t)(N - 1) * ld + DH) * 2;
@@ -448,6 +452,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const __amdgpu_buffer_rsrc_t dors = make_rsrc(dobase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2));
   const uint16_t* obase = o + (int64_t)b * N * ld_o;
   const __amdgpu_buffer_rsrc_t ors = make_rsrc(obase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_o + DH) * 2));
+  // dQ destination of this batch: the f32 accumulator [N][D] or the bf16 gradient rows directly
+  const __amdgpu_buffer_rsrc_t dqrs = dq_acc ? make_rsrc(dq_acc + (int64_t)b * N * D, clamp_bytes((int64_t)N * D * 4))
+                                             : make_rsrc(dqkv + (int64_t)b * N * ld_dq, clamp_bytes(((int64_t)(N - 1) * ld_dq + D) * 2));
 
   // own keys' K and V fragments (B operands): lane holds X[kw0 + 16f + li][32ks + 8g + j]
   v8s kf[2][C::KS], vf[2][C::KS];
@@ -494,11 +501,22 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   };
   stage(0);
   float dqb0 = 0.f, dqb1 = 0.f;  // q-bias gradient partials (column sums of this wave's dQ fragments)
+  // dQ stores this wave issues per query block (younger than the next block's staging DMAs)
+  const int nst = wave < 2 * C::NE ? 4 * ((2 * C::NE - 1 - wave) / NW + 1) : 0;
   for (int qb = 0; qb < nqb; ++qb) {
     const int q0 = qb * QB;
-    // block qb landed (issued one iteration ago); every wave is done with slot (qb+1)&1 and with dS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // block qb landed (issued one iteration ago; the previous block's dQ stores may stay in
+    // flight); every wave is done with slot (qb+1)&1 and with dS
+    if (qb == 0 || nst < 4)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (nst < 8)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // a raw barrier: __syncthreads' release fence would drain those stores (vmcnt(0)) first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     if (qb + 1 < nqb) stage(qb + 1);
     const char* qimg = qdo + (qb & 1) * 3 * QB * RB;
     const char* doimg = qimg + QB * RB;
@@ -569,53 +587,61 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
       }
     }
-    // dS -> LDS (bf16) [q][key_local], chunk-swizzled by row for the dQ row reads
+    // dS^T -> LDS (bf16) [key_local][32 queries]: the packed dK-product operands sf, four
+    // consecutive queries per 8-B write (a = 0: queries 4g.., a = 1: 16 + 4g..)
+    {
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ql = 16 * a + 4 * g + r;
-          const int kl = wave * 32 + 16 * f + li;
-          const int chunk = (kl >> 3) ^ (ql & (ds_cpr - 1) & 15);
-          *(uint16_t*)(dsimg + ql * KB * 2 + chunk * 16 + (kl & 7) * 2) = f2bf(dp[a][f][r]);
-        }
+      for (int f = 0; f < 2; ++f) {
+        const v4u w = __builtin_bit_cast(v4u, sf[f]);
+        *(__attribute__((address_space(3))) v2u*)(dsimg + dsw0 + 1024 * f) = v2u{w[0], w[1]};
+        *(__attribute__((address_space(3))) v2u*)(dsimg + dsw1 + 1024 * f) = v2u{w[2], w[3]};
+      }
+    }
     }  // active
     // dS visible to every wave; a raw barrier, so the next block's DMAs stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 2*NE output fragments split over the waves
+    // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 2*NE output fragments split over the waves.
+    // Both operands by transposed reads (dS^T rows 32ks + 8g + q4 (+4), queries 16a + 4p4; K rows
+    // the same keys, dims 16e + 4p4), four key slices per LDS wait; the stores are buffer ops, so
+    // queries past N drop in the range check and every wave issues exactly 4 per fragment.
     int kfr = 0;
     for (int fr = wave; fr < 2 * C::NE; fr += NW, ++kfr) {
       const int a = fr / C::NE, e = fr % C::NE;
       v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-      const int ql = 16 * a + li;
-      for (int ks = 0; ks < nks_dq; ks += 2) {  // two key slices per LDS wait
-        const bool two = ks + 1 < nks_dq;
-        v4s lo0, hi0, lo1, hi1;
-        frag_tr_async(kimg, KB, 32 * ks + 8 * g, 32 * ks + 8 * g + 4, 16 * e, lane, lo0, hi0);
-        if (two) frag_tr_async(kimg, KB, 32 * (ks + 1) + 8 * g, 32 * (ks + 1) + 8 * g + 4, 16 * e, lane, lo1, hi1);
-        const v8s af0 = ds_read_b128(dsimg + ql * KB * 2 + (((ks * 4 + g) ^ (ql & (ds_cpr - 1) & 15)) * 16));
-        const v8s af1 = two ? ds_read_b128(dsimg + ql * KB * 2 + ((((ks + 1) * 4 + g) ^ (ql & (ds_cpr - 1) & 15)) * 16))
-                            : v8s{0, 0, 0, 0, 0, 0, 0, 0};
+      const char* kt0 = kimg + lds_off(KB, 8 * g + q4, 2 * e + (p4 >> 1)) + 8 * (p4 & 1);
+      const char* kt1 = kimg + lds_off(KB, 8 * g + q4 + 4, 2 * e + (p4 >> 1)) + 8 * (p4 & 1);
+      const char* dt0 = dsimg + ds_off(8 * g + q4, 4 * a + p4);
+      const char* dt1 = dsimg + ds_off(8 * g + q4 + 4, 4 * a + p4);
+      auto batch = [&](auto k0c) {
+        constexpr int k0 = decltype(k0c)::value;
+        v4s klo[4], khi[4], slo[4], shi[4];
+        static_for<0, 4>([&](auto jc) {
+          constexpr int ks = k0 + decltype(jc)::value;
+          klo[ks - k0] = ds_read_tr_async_at<4096 * ks>(kt0);
+          khi[ks - k0] = ds_read_tr_async_at<4096 * ks>(kt1);
+          slo[ks - k0] = ds_read_tr_async_at<2048 * ks>(dt0);
+          shi[ks - k0] = ds_read_tr_async_at<2048 * ks>(dt1);
+        });
         lds_wait();
-        acc = mfma16(af0, cat44(lo0, hi0), acc);
-        if (two) acc = mfma16(af1, cat44(lo1, hi1), acc);
-      }
-      float cs = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (k0 + j < nks_dq) acc = mfma16(cat44(slo[j], shi[j]), cat44(klo[j], khi[j]), acc);
+      };
+      batch(std::integral_constant<int, 0>{});
+      if (nks_dq > 4) batch(std::integral_constant<int, 4>{});
+      const uint32_t vq = (uint32_t)(q0 + 16 * a + 4 * g), col = (uint32_t)(h * DH + 16 * e + li);
+      float cs = 0.f;  // queries past N have dS = 0, so their dQ is exactly 0
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int q = q0 + 16 * a + 4 * g + r;
-        if (q < N) {
-          const float val = acc[r] * scale;
-          cs += val;
-          if (dq_acc)
-            atomicAdd(dq_acc + ((int64_t)b * N + q) * D + h * DH + 16 * e + li, val);
-          else
-            dqkv[((int64_t)b * N + q) * ld_dq + h * DH + 16 * e + li] = f2bf(val);
-        }
+        const float val = acc[r] * scale;
+        cs += val;
+        if (dq_acc)
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dqrs, ((vq + r) * (uint32_t)ld_dq + col) * 2, 0, 0);
       }
       if (kfr == 0) dqb0 += cs;  // q-bias gradient: this fragment's column sums across query blocks
       else dqb1 += cs;           // (at most two fragments per wave: host guarantees 2*NE <= 2*NW)
