@@ -742,6 +742,11 @@ def all_checks() -> List[Callable]:
         lambda: check_gemm_fwd(5000, 2304, 768, 13, True, True),   # persistent: several tiles per CU
         lambda: check_gemm_fwd(9000, 768, 128, 13, True, False),   # nk = 2: next-tile DMAs start at phase 3
         lambda: check_gemm_gelu(6000, 3072, 768, 13),
+        # persistent, 2-3 tiles per workgroup: full tiles keep their epilogue stores in flight across
+        # the tile boundary (plain / residual / GELU epilogues), the partial last row of tiles drains
+        lambda: check_gemm_fwd(12608, 2304, 768, 13, True, False),
+        lambda: check_gemm_fwd(12608, 2304, 768, 13, True, True),
+        lambda: check_gemm_gelu(12608, 3072, 768, 13),
         lambda: check_gemm_gelu_dropout(5000, 3072, 768),
         lambda: check_gemm_dropout(3000, 768, 128, 0.1, 13),
         lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
