@@ -414,7 +414,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
                                                         float* __restrict__ dbias, int N, int H, int D, float scale,
-                                                        int key_off, int key_end) {
+                                                        int key_off, int key_end, int dq_mode) {
   using C = Hd<DH>;
   constexpr int QB = 32;
   constexpr int RB = 128 * C::NH;  // LDS bytes per staged head row
@@ -712,6 +712,40 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       wv.y = pack2bf(dv[e][f][2], dv[e][f][3]);
       *(uint2*)(row + D + h * DH + 16 * e + 4 * g) = wk;
       *(uint2*)(row + 2 * D + h * DH + 16 * e + 4 * g) = wv;
+    }
+  }
+  // dq_mode 1 / 2 (the last launch, one workgroup per (batch, head)): the other key blocks' dQ
+  // atomics landed before this launch started and this workgroup's own are acknowledged after the
+  // wait below, so it converts the pair's accumulated dQ rows to bf16 (no separate pass over the
+  // whole accumulator) and, in mode 2, zeroes them again for the next use of a persistent workspace
+  if (dq_mode && dq_acc) {
+    // (no agent-scope fence: it would write back the whole L2. This workgroup's atomics performed in
+    // its XCD's L2, which its loads below go through; the CU's L1 holds no line of these rows.)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // 8 independent 16-B loads in flight per thread, then their stores (buffer ops: rows past N drop)
+    constexpr int C4 = DH / 4, U = 8;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef uint32_t v2u_ __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t ors_q = make_rsrc(dqkv + (int64_t)b * N * ld_dq + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_dq + DH) * 2));
+    const int n4 = N * C4;
+    for (int i0 = 0; i0 < n4; i0 += U * (int)blockDim.x) {
+      v4u v[U];
+      uint32_t ao[U], oo[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * (int)blockDim.x + (int)threadIdx.x;
+        const int q = i < n4 ? i / C4 : N, c = 4 * (i - (i / C4) * C4);
+        ao[u] = ((uint32_t)q * (uint32_t)D + (uint32_t)(h * DH + c)) * 4;
+        oo[u] = ((uint32_t)q * (uint32_t)ld_dq + (uint32_t)c) * 2;
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(dqrs, ao[u], 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const v4f f = __builtin_bit_cast(v4f, v[u]);
+        __builtin_amdgcn_raw_buffer_store_b64(v2u_{pack2bf(f[0], f[1]), pack2bf(f[2], f[3])}, ors_q, oo[u], 0, 0);
+        if (dq_mode == 2) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, dqrs, ao[u], 0, 0);
+      }
     }
   }
 }
@@ -1949,13 +1983,14 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
 
-__global__ void __launch_bounds__(256) dq_convert_kernel(const float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
-                                                          int64_t rows, int D) {
+__global__ void __launch_bounds__(256) dq_convert_kernel(float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
+                                                          int64_t rows, int D, int rezero) {
   const int64_t n = rows * D;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t r = i / D;
     const int d = (int)(i % D);
     dqkv[r * ld_dq + d] = f2bf(acc[i]);
+    if (rezero) acc[i] = 0.f;
   }
 }
 
@@ -2248,7 +2283,7 @@ static bool attn_bwd_pipe_ok(int B, int N, int H, int D, int64_t ld, int64_t ld_
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                  float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
+                                  int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
   if (DH == 64 && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][128] partials
     return attn_bwd_pipe(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
@@ -2268,11 +2303,11 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     attr = true;
   }
   // K image | 2 x (Q | dO | O) blocks | dS | 2 x 1 KiB lse DMA slots
-  auto launch = [&](int nw, int k0, int k1) {
+  auto launch = [&](int nw, int k0, int k1, int dq_mode) {
     const int kb = nw * 32;
     const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
     hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout, ld_do, out,
-                       ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1);
+                       ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1, dq_mode);
   };
   const bool tail_split = attn_bwd_tail_split();
   const int rem = N % KB;
@@ -2282,7 +2317,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     const int kb = NW * 32, k1 = N - 1;
     const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
     hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 + kb - 1) / kb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, out,
-                       ld_o, lse, dqkv, ld_dq, nullptr, nullptr, N, H, D, scale, 0, k1);
+                       ld_o, lse, dqkv, ld_dq, nullptr, nullptr, N, H, D, scale, 0, k1, 0);
     hipLaunchKernelGGL(attn_bwd_lastkey_kernel<DH>, dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq,
                        N, H, D, scale);
     return hipGetLastError();
@@ -2294,16 +2329,18 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     // CLS token of 224/14) is cheaper left interleaved in the one grid: as its own launch of 1-wave
     // workgroups it serialises 9 query-block staging round trips per pair (975 vs 915 us at H/14
     // b128; scripts/attn_shape_probe.py)
-    launch(NW, 0, N - rem);
-    launch(pvr_attn_bwd_waves(rem), N - rem, N);
-  } else {
-    launch(NW, 0, N);
+    // the tail launch has one workgroup per (batch, head) and runs after the body: it also turns
+    // the pair's accumulated dQ into bf16 (and re-zeroes a persistent accumulator)
+    launch(NW, 0, N - rem, 0);
+    launch(pvr_attn_bwd_waves(rem), N - rem, N, dq_rezero ? 2 : 1);
+    return hipGetLastError();
   }
+  launch(NW, 0, N, 0);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
     int64_t blocks = (rows * D + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dq_acc, dqkv, ld_dq, rows, D);
+    hipLaunchKernelGGL(dq_convert_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dq_acc, dqkv, ld_dq, rows, D, dq_rezero);
   }
   return hipGetLastError();
 }
@@ -2317,7 +2354,8 @@ extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, in
   return attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq) ? 1 : 0;
 }
 
-// dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head).
+// dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head);
+// dq_rezero = 1 leaves it zeroed again afterwards (a persistent workspace reused across calls).
 // dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
 // every element is written), whose row sum is the in_proj bias gradient; on the pipelined path
 // (pvr_attn_bwd_uses_pipe) the per-block partials described there.
@@ -2325,13 +2363,13 @@ extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, in
 // whole-head backward (which does not fuse the bias gradient: dbias forces the single kernel).
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                    int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                   float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
+                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
   switch (D / H) {
-    case 64: return attn_bwd_launch<64>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 80: return attn_bwd_launch<80>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 96: return attn_bwd_launch<96>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
-    case 128: return attn_bwd_launch<128>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dbias, B, N, H, D, scale, s);
+#define PVR_BWD_DH(DH) \
+  case DH: return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale, s);
+    PVR_BWD_DH(64) PVR_BWD_DH(80) PVR_BWD_DH(96) PVR_BWD_DH(128)
+#undef PVR_BWD_DH
     default: return hipErrorInvalidValue;
   }
 }

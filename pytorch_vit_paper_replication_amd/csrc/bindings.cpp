@@ -1,6 +1,7 @@
 // pybind11 / ATen bindings for the gfx950 kernels. Every entry point launches on PyTorch's current
 // HIP stream (so it composes with torch streams, events and hipGraph capture) and validates dtypes,
 // shapes and strides before touching device memory.
+#include <map>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -46,7 +47,7 @@ int pvr_attn_bwd_needs_dq_acc(int, int, int);
 int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
-hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, float*, int, int, int, int, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float, hipStream_t);
 }
 
 namespace {
@@ -461,6 +462,27 @@ void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor d
   db.select(0, 2).add_(r.select(1, 2));
 }
 
+// Persistent f32 dQ accumulator of the multi-key-block attention backward, one per (device, stream),
+// zero-initialised once: the backward converts the accumulated dQ and zeroes it again, so no
+// per-call zero fill (a 151 MB memset per layer at ViT-L/16 384 px). Deliberately never freed (a
+// static tensor's destructor would run after the HIP runtime's teardown). PVR_ATTN_DQ_WS=0: a fresh
+// zeroed tensor per call instead (A/B).
+torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts) {
+  static const bool on = [] {
+    const char* e = getenv("PVR_ATTN_DQ_WS");
+    return !(e && e[0] == '0');
+  }();
+  if (!on) return torch::Tensor();
+  static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
+  const auto key = std::make_pair((int)opts.device().index(), stream());
+  torch::Tensor*& t = cache[key];
+  if (!t || t->numel() < numel) {
+    delete t;  // stream-ordered reuse of its memory by the caching allocator
+    t = new torch::Tensor(torch::zeros({numel}, opts.dtype(torch::kFloat32)));
+  }
+  return *t;
+}
+
 // pipelined backward taken for the standard layouts of this shape (qkv [T][3D], dO / O [T][D])
 bool attn_bwd_pipe_path(int64_t B, int64_t N, int64_t H, int64_t D) {
   return pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D) != 0;
@@ -475,9 +497,13 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   auto dqkv = torch::empty_like(qkv);
   auto delta = torch::empty_like(lse);  // rowsum(dO * O) workspace of the two-kernel backward
   torch::Tensor dq_acc;
+  int dq_rezero = 0;
   const bool has_db = dbias.has_value() && dbias->defined();
-  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)(D / H), has_db ? 1 : 0))
-    dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
+  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)(D / H), has_db ? 1 : 0)) {
+    dq_acc = dq_workspace(B * N * D, qkv.options());
+    dq_rezero = dq_acc.defined() ? 1 : 0;
+    if (!dq_acc.defined()) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
+  }
   // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
   torch::Tensor dbias_part;
   const bool want_db = dbias.has_value() && dbias->defined();
@@ -501,7 +527,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   }
   check(pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"), ld_of(dout, "dout"),
                      f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"), ld_of(dqkv, "dqkv"),
-                     dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr,
+                     dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
                      dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
                      (float)scale, stream()),
         "attn_bwd");

@@ -795,6 +795,11 @@ def all_checks() -> List[Callable]:
         lambda: check_attn_bwd(1, 64, 1, 64, True),
         lambda: check_attn_bwd(1, 257, 2, 64, True),
         lambda: check_attn_bwd(1, 577, 2),
+        # again: the persistent dQ accumulator must have been re-zeroed by the tail launch's
+        # conversion (577 = 2 x 256 + 65) and by the separate conversion pass (400 = 256 + 144)
+        lambda: check_attn_bwd(2, 577, 3),
+        lambda: check_attn_bwd(2, 400, 3),
+        lambda: check_attn_bwd(2, 400, 3),
         lambda: check_attn_fwd(2, 257, 3, 80),
         lambda: check_attn_fwd(1, 33, 2, 80),
         lambda: check_attn_bwd(2, 257, 3, 80),
