@@ -23,6 +23,10 @@
 #include "common.h"
 #include <type_traits>
 
+#ifndef PVR_ATTN_FWD_KT64
+#define PVR_ATTN_FWD_KT64 0
+#endif
+
 namespace pvr {
 namespace {
 
@@ -122,7 +126,10 @@ template <int DH>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
                                                         int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale) {
   using C = Hd<DH>;
-  constexpr int KT = 64;                         // keys per tile
+  // keys per tile: 64, or 32 for two-image head rows (dh > 64), so that the two K/V stages stay at
+  // 32 KiB and four workgroups share a CU (PVR_ATTN_FWD_KT64=1 build: 64 keys throughout)
+  constexpr int KT = C::NH == 1 || PVR_ATTN_FWD_KT64 ? 64 : 32;
+  constexpr int NFR = KT / 16;                   // 16-key S fragments per tile
   constexpr int TILE_BYTES = KT * 128 * C::NH;   // one K or V tile image (8 or 16 KiB)
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [stage][K|V]
   const int lane = threadIdx.x & 63;
@@ -174,11 +181,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     }
     if (active) {
       const int kbase = t * KT;
-      const int nf = min(4, (N - kbase + 15) >> 4);  // 16-key fragments holding a valid key (uniform)
+      const int nf = min(NFR, (N - kbase + 15) >> 4);  // 16-key fragments holding a valid key (uniform)
       // S^T[key][q] for the key fragments
-      v4f s[4];
+      v4f s[NFR];
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < NFR; ++f) {
         s[f] = v4f{0.f, 0.f, 0.f, 0.f};
         if (f < nf) {
 #pragma unroll
@@ -187,14 +194,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
       }
       if (kbase + KT > N) {  // tail tile: mask keys >= N
 #pragma unroll
-        for (int f = 0; f < 4; ++f)
+        for (int f = 0; f < NFR; ++f)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (kbase + 16 * f + 4 * g + r >= N) s[f][r] = -INFINITY;
       }
       float tmax = s[0][0];
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+      for (int f = 0; f < NFR; ++f)
 #pragma unroll
         for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[f][r]);
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
@@ -203,7 +210,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float psum = 0.f;
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+      for (int f = 0; f < NFR; ++f)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float pv = __builtin_amdgcn_exp2f(fmaf(s[f][r], c, -m_new));
@@ -216,7 +223,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
       for (int e = 0; e < C::NE; ++e) o[e] *= alpha;
       // O^T[d][q] += V^T[d][key] P^T[key][q]
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < NFR / 2; ++kk) {
         if (kk * 2 < nf) {
           // asm transpose reads: the next tile's K/V DMA stays in flight under them
           v4s vlo[C::NE], vhi[C::NE];
