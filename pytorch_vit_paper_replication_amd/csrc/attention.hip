@@ -2001,8 +2001,49 @@ __global__ void __launch_bounds__(256) dq_convert_kernel(float* __restrict__ acc
   }
 }
 
+// In_proj bias gradient from the pipelined backward's per-(batch, head, 32-query block) partials
+// part[(b*H + h)*NQ + nq][192] (q sums of the two 16-query halves | v sums), deterministic in two
+// passes: (1) grid (H, S): rows s*R .. of head h's B*NQ partial rows -> ws[s][h][128] (q | v);
+// (2) grid H: dbias[q slice of h] += sum_s, dbias[v slice of h] += sum_s (the k bias gradient is 0).
+__global__ void __launch_bounds__(128) dbias_part_kernel(const float* __restrict__ part, float* __restrict__ ws, int B, int H,
+                                                         int NQ, int R) {
+  const int h = blockIdx.x, sidx = blockIdx.y, t = threadIdx.x;
+  const int rows = B * NQ, r0 = sidx * R, r1 = min(rows, r0 + R);
+  float a = 0.f;
+#pragma unroll 8
+  for (int r = r0; r < r1; ++r) {  // unrolled: eight rows' loads in flight, not one dependent load per row
+    const int b = r / NQ, nq = r - b * NQ;
+    const float* row = part + ((int64_t)(b * H + h) * NQ + nq) * 192;
+    a += t < 64 ? row[t] + row[64 + t] : row[64 + t];
+  }
+  ws[((int64_t)sidx * H + h) * 128 + t] = a;
+}
+
+__global__ void __launch_bounds__(128) dbias_final_kernel(const float* __restrict__ ws, float* __restrict__ dbias, int H, int D, int S) {
+  const int h = blockIdx.x, t = threadIdx.x;
+  float a = 0.f;
+  for (int sidx = 0; sidx < S; ++sidx) a += ws[((int64_t)sidx * H + h) * 128 + t];
+  if (t < 64)
+    dbias[h * 64 + t] += a;
+  else
+    dbias[2 * D + h * 64 + (t - 64)] += a;
+}
+
 }  // namespace
 }  // namespace pvr
+
+// ws: f32 [S][H][128] scratch, S = pvr_attn_dbias_splits(B, NQ)
+extern "C" int pvr_attn_dbias_splits(int B, int NQ) { return B * NQ < 128 ? B * NQ : 128; }
+
+extern "C" hipError_t pvr_attn_dbias_reduce(const float* part, float* ws, float* dbias, int B, int H, int NQ, int D, hipStream_t s) {
+  using namespace pvr;
+  const int S = pvr_attn_dbias_splits(B, NQ);
+  if (S <= 0) return hipSuccess;
+  const int R = (B * NQ + S - 1) / S;
+  hipLaunchKernelGGL(dbias_part_kernel, dim3(H, S), dim3(128), 0, s, part, ws, B, H, NQ, R);
+  hipLaunchKernelGGL(dbias_final_kernel, dim3(H), dim3(128), 0, s, ws, dbias, H, D, S);
+  return hipGetLastError();
+}
 
 static int device_cus() {
   static const int n = [] {

@@ -47,6 +47,8 @@ int pvr_attn_bwd_needs_dq_acc(int, int, int);
 int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
+int pvr_attn_dbias_splits(int, int);
+hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, int, hipStream_t);
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float, hipStream_t);
 }
 
@@ -455,11 +457,15 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int
 // dbias[3D] += the in_proj bias gradient from the pipelined backward's [B*H][NQ][192] partials
 // (per query block: dQ column sums of two query halves | dO column sums; the k slice gets none)
 void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor dbias) {
-  TORCH_CHECK(part.is_contiguous() && part.numel() % (B * H * 192) == 0, "attn_dbias_reduce: [B*H][NQ][192] partials");
-  auto r = part.view({B, H, -1, 3, 64}).sum(at::IntArrayRef{0, 2});  // [H][3][64]
-  auto db = dbias.view({3, H, 64});
-  db.select(0, 0).add_(r.select(1, 0) + r.select(1, 1));
-  db.select(0, 2).add_(r.select(1, 2));
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32 && part.is_contiguous() && part.numel() % (B * H * 192) == 0,
+              "attn_dbias_reduce: f32 [B*H][NQ][192] partials");
+  TORCH_CHECK(dbias.is_cuda() && dbias.scalar_type() == torch::kFloat32 && dbias.is_contiguous() && dbias.numel() == 3 * H * 64,
+              "attn_dbias_reduce: f32 [3D] bias gradient, D = 64 H");
+  const int64_t NQ = part.numel() / (B * H * 192);
+  auto ws = torch::empty({(int64_t)pvr_attn_dbias_splits((int)B, (int)NQ) * H * 128}, part.options());
+  check(pvr_attn_dbias_reduce(part.data_ptr<float>(), ws.data_ptr<float>(), dbias.data_ptr<float>(), (int)B, (int)H, (int)NQ,
+                              (int)(64 * H), stream()),
+        "attn_dbias_reduce");
 }
 
 // Persistent f32 dQ accumulator of the multi-key-block attention backward, one per (device, stream),
