@@ -1,5 +1,6 @@
 #!/bin/bash
-# Kernel-time profiles of the other BASELINE configs: ViT-L/16 384 px bf16 (b64), ViT-H/14 224 px fp8 (b128).
+# Kernel-time profiles of the BASELINE configs: ViT-B/16 224 px bf16 (b256, headline), ViT-L/16 384 px bf16 (b64),
+# ViT-H/14 224 px fp8 (b128).
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; export TMPDIR=/tmp
 O="$R/gpurun_out/${1:-models}"; mkdir -p "$O"
 run() {  # tag, bench args...
@@ -11,6 +12,7 @@ run() {  # tag, bench args...
   cd "$R"; S=$(find "$O/prof_$tag" -name "*kernel_stats.csv" | head -n1)
   python scripts/summarize_prof.py "$S" 6 "kernel stats $tag" > "$O/kernel_stats_$tag.md" 2>&1; head -20 "$O/kernel_stats_$tag.md"
 }
+run b16_b256 || exit $?
 run l16_384 --model vit_l16 --image-size 384 --batch 64 || exit $?
 run h14_fp8 --model vit_h14 --batch 128 --dtype fp8 || exit $?
 exit 0
