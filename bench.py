@@ -49,8 +49,25 @@ def parse():
     return p.parse_args()
 
 
+def _relaunch_distributed(n: int) -> int:
+    """``python bench.py --gpus N`` without a torchrun environment: run the same command under
+    ``torch.distributed.run`` (one rank per GPU, rendezvous on 127.0.0.1) as a CHILD process and return
+    its exit code. Nothing has touched the GPU yet in this process."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_relaunch_distributed(args.gpus))
     if args.impl == "torch":
         os.environ["PVR_DISABLE_FUSED"] = "1"
     import torch
@@ -61,9 +78,9 @@ def main():
     from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
     from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    n = max(args.gpus, world_env)
     rank, world, device = init_distributed()
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU (torch.distributed.run)")
     if (args.force_ddp or args.pg_only) and not torch.distributed.is_initialized():
         import datetime
 
