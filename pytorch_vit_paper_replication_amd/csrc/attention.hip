@@ -2021,8 +2021,21 @@ __global__ void __launch_bounds__(128) dbias_part_kernel(const float* __restrict
 
 __global__ void __launch_bounds__(128) dbias_final_kernel(const float* __restrict__ ws, float* __restrict__ dbias, int H, int D, int S) {
   const int h = blockIdx.x, t = threadIdx.x;
-  float a = 0.f;
-  for (int sidx = 0; sidx < S; ++sidx) a += ws[((int64_t)sidx * H + h) * 128 + t];
+  // four independent partial sums, 16 loads in flight per thread: the one-accumulator loop waited one
+  // memory latency per split (32 us for 128 splits at ViT-B/16 b256); fixed order, so deterministic
+  const float* col = ws + (int64_t)h * 128 + t;
+  const int64_t step = (int64_t)H * 128;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int sidx = 0;
+#pragma unroll 4
+  for (; sidx + 4 <= S; sidx += 4) {
+    a0 += col[(sidx + 0) * step];
+    a1 += col[(sidx + 1) * step];
+    a2 += col[(sidx + 2) * step];
+    a3 += col[(sidx + 3) * step];
+  }
+  for (; sidx < S; ++sidx) a0 += col[sidx * step];
+  const float a = (a0 + a1) + (a2 + a3);
   if (t < 64)
     dbias[h * 64 + t] += a;
   else

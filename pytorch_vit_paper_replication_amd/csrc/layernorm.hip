@@ -90,8 +90,29 @@ PVR_DEV void load8(const uint16_t* p, float* o) {
   }
 }
 
-// Grid-stride over rows: each wave keeps its lanes' dgamma/dbeta partials in registers.
-template <int MAXCH>
+// W consecutive bf16 of a row (W = 8: one 16-B access, W = 4: one 8-B access)
+template <int W>
+struct RowVec;
+template <>
+struct RowVec<8> {
+  uint32_t u[4];
+  PVR_DEV void load(const uint16_t* p) { const uint4 q = *(const uint4*)p; u[0] = q.x; u[1] = q.y; u[2] = q.z; u[3] = q.w; }
+  PVR_DEV void store(uint16_t* p) const { *(uint4*)p = make_uint4(u[0], u[1], u[2], u[3]); }
+  PVR_DEV void zero() { u[0] = u[1] = u[2] = u[3] = 0u; }
+};
+template <>
+struct RowVec<4> {
+  uint32_t u[2];
+  PVR_DEV void load(const uint16_t* p) { const uint2 q = *(const uint2*)p; u[0] = q.x; u[1] = q.y; }
+  PVR_DEV void store(uint16_t* p) const { *(uint2*)p = make_uint2(u[0], u[1]); }
+  PVR_DEV void zero() { u[0] = u[1] = 0u; }
+};
+
+// Grid-stride over rows: each wave keeps its lanes' dgamma/dbeta partials in registers. A lane owns
+// MAXCH chunks of W columns (chunk c = lane + 64 i). W = 4 where D / 8 is not a multiple of 64 but
+// D / 4 is (D = 768: 3 chunks of 4 per lane instead of 1.5 of 8, so no lane idles on the last chunk
+// and the smaller register footprint doubles the waves in flight: 4 per SIMD instead of 2).
+template <int MAXCH, int W>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict__ dy, int64_t dy_stride,
                                                       const uint16_t* __restrict__ x, int64_t x_stride,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -102,68 +123,71 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       uint16_t* __restrict__ dz, int64_t dz_stride,
                                                       const uint64_t* __restrict__ seed_ptr, uint64_t seed_off, uint32_t thr,
                                                       float dscale, int rows, int D) {
-  __shared__ float red[4][MAXCH * 64 * 8 > 1280 ? 1280 : MAXCH * 64 * 8];  // one partial at a time
+  __shared__ float red[4][MAXCH * 64 * W > 1280 ? 1280 : MAXCH * 64 * W];  // one partial at a time
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nch = D >> 3;
-  float gw[MAXCH][8], gb[MAXCH][8], gs[MAXCH][8];
+  const int nch = D / W;
+  float gw[MAXCH][W], gb[MAXCH][W], gs[MAXCH][W];
 #pragma unroll
   for (int i = 0; i < MAXCH; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gw[i][j] = gb[i][j] = gs[i][j] = 0.f;
+    for (int j = 0; j < W; ++j) gw[i][j] = gb[i][j] = gs[i][j] = 0.f;
 
   // Rows are software-pipelined: the x / dy / dres vectors of the wave's next row are loaded
   // before the current row's two wave reductions, so HBM latency overlaps the shuffles.
   const int stride = gridDim.x * 4;
-  uint4 cx[MAXCH], cdy[MAXCH], cr[MAXCH];
+  RowVec<W> cx[MAXCH], cdy[MAXCH], cr[MAXCH];
   // unconditional (clamped) loads: the compiler can then count them instead of waiting vmcnt(0)
-  auto load_row = [&](int row, uint4 (&qx)[MAXCH], uint4 (&qd)[MAXCH], uint4 (&qr)[MAXCH]) {
+  auto load_row = [&](int row, RowVec<W> (&qx)[MAXCH], RowVec<W> (&qd)[MAXCH], RowVec<W> (&qr)[MAXCH]) {
     const int rr = min(row, rows - 1);
 #pragma unroll
     for (int i = 0; i < MAXCH; ++i) {
       const int c = min(lane + 64 * i, nch - 1);
-      qx[i] = *(const uint4*)(x + (int64_t)rr * x_stride + c * 8);
-      qd[i] = *(const uint4*)(dy + (int64_t)rr * dy_stride + c * 8);
-      qr[i] = dres ? *(const uint4*)(dres + (int64_t)rr * dres_stride + c * 8) : make_uint4(0, 0, 0, 0);
+      qx[i].load(x + (int64_t)rr * x_stride + c * W);
+      qd[i].load(dy + (int64_t)rr * dy_stride + c * W);
+      if (dres)
+        qr[i].load(dres + (int64_t)rr * dres_stride + c * W);
+      else
+        qr[i].zero();
     }
   };
   // gamma is loop-invariant: keep this lane's columns in registers (a per-row reload would be
   // waited with vmcnt(0), which also drains the next row's prefetch)
-  float wreg[MAXCH][8];
+  float wreg[MAXCH][W];
 #pragma unroll
   for (int i = 0; i < MAXCH; ++i) {
     const int c = min(lane + 64 * i, nch - 1);
-    const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
-    wreg[i][0] = w0.x; wreg[i][1] = w0.y; wreg[i][2] = w0.z; wreg[i][3] = w0.w;
-    wreg[i][4] = w1.x; wreg[i][5] = w1.y; wreg[i][6] = w1.z; wreg[i][7] = w1.w;
+#pragma unroll
+    for (int j = 0; j < W; j += 4) {
+      const float4 w4 = *(const float4*)(w + c * W + j);
+      wreg[i][j] = w4.x; wreg[i][j + 1] = w4.y; wreg[i][j + 2] = w4.z; wreg[i][j + 3] = w4.w;
+    }
   }
   const uint64_t seed = dz ? *seed_ptr + seed_off : 0ull;
   int row = blockIdx.x * 4 + wave;
   load_row(row, cx, cdy, cr);
   float cmu = row < rows ? mean[row] : 0.f, crs = row < rows ? rstd[row] : 0.f;
   for (; row < rows; row += stride) {
-    uint4 nx[MAXCH], ndy[MAXCH], nr[MAXCH];
+    RowVec<W> nx[MAXCH], ndy[MAXCH], nr[MAXCH];
     load_row(row + stride, nx, ndy, nr);
     const int rn = min(row + stride, rows - 1);
     const float nmu = mean[rn], nrs = rstd[rn];
     const float mu = cmu, rs = crs;
-    float xh[MAXCH][8], g[MAXCH][8];
+    // xhat and g = dy * gamma are recomputed from the packed row in the second pass instead of kept
+    // in registers between the two wave reductions (fewer VGPRs: more waves, more bytes in flight)
+    auto xhat = [&](int i, int j) { return (bf2f(j & 1 ? cx[i].u[j >> 1] >> 16 : cx[i].u[j >> 1] & 0xFFFF) - mu) * rs; };
+    auto dyv = [&](int i, int j) { return bf2f(j & 1 ? cdy[i].u[j >> 1] >> 16 : cdy[i].u[j >> 1] & 0xFFFF); };
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXCH; ++i) {
       const int c = lane + 64 * i;
       if (c < nch) {
-        const uint32_t ux[4] = {cx[i].x, cx[i].y, cx[i].z, cx[i].w};
-        const uint32_t ud[4] = {cdy[i].x, cdy[i].y, cdy[i].z, cdy[i].w};
-        const float* ww = wreg[i];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xv = bf2f(j & 1 ? ux[j >> 1] >> 16 : ux[j >> 1] & 0xFFFF);
-          const float dv = bf2f(j & 1 ? ud[j >> 1] >> 16 : ud[j >> 1] & 0xFFFF);
-          xh[i][j] = (xv - mu) * rs;
-          g[i][j] = dv * ww[j];
-          s1 += g[i][j];
-          s2 += g[i][j] * xh[i][j];
-          gw[i][j] += dv * xh[i][j];
+        for (int j = 0; j < W; ++j) {
+          const float xh = xhat(i, j), dv = dyv(i, j);
+          const float g = dv * wreg[i][j];
+          s1 += g;
+          s2 += g * xh;
+          gw[i][j] += dv * xh;
           gb[i][j] += dv;
         }
       }
@@ -173,32 +197,31 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
     for (int i = 0; i < MAXCH; ++i) {
       const int c = lane + 64 * i;
       if (c < nch) {
-        float o[8];
+        float o[W];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (g[i][j] - c1 - xh[i][j] * c2) * rs;
+        for (int j = 0; j < W; ++j) o[j] = (dyv(i, j) * wreg[i][j] - c1 - xhat(i, j) * c2) * rs;
         if (dres) {
-          const uint32_t ur[4] = {cr[i].x, cr[i].y, cr[i].z, cr[i].w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += bf2f(j & 1 ? ur[j >> 1] >> 16 : ur[j >> 1] & 0xFFFF);
+          for (int j = 0; j < W; ++j) o[j] += bf2f(j & 1 ? cr[i].u[j >> 1] >> 16 : cr[i].u[j >> 1] & 0xFFFF);
         }
-        uint4 q;
-        q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
-        q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
-        *(uint4*)(dx + (int64_t)row * dx_stride + c * 8) = q;
+        RowVec<W> q;
+#pragma unroll
+        for (int j = 0; j < W; j += 2) q.u[j >> 1] = pack2bf(o[j], o[j + 1]);
+        q.store(dx + (int64_t)row * dx_stride + c * W);
         if (dz) {  // uniform: dropout backward of the producing layer
 #pragma unroll
-          for (int j = 0; j < 8; j += 2) {
+          for (int j = 0; j < W; j += 2) {
             bool k0, k1;
-            rng_keep2(seed, (uint64_t)row * D + c * 8 + j, thr, k0, k1);
+            rng_keep2(seed, (uint64_t)row * D + c * W + j, thr, k0, k1);
             o[j] = k0 ? o[j] * dscale : 0.f;
             o[j + 1] = k1 ? o[j + 1] * dscale : 0.f;
           }
-          q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
-          q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
-          *(uint4*)(dz + (int64_t)row * dz_stride + c * 8) = q;
+#pragma unroll
+          for (int j = 0; j < W; j += 2) q.u[j >> 1] = pack2bf(o[j], o[j + 1]);
+          q.store(dz + (int64_t)row * dz_stride + c * W);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) gs[i][j] += o[j];  // column sums of dx (or dz): a fused bias gradient
+        for (int j = 0; j < W; ++j) gs[i][j] += o[j];  // column sums of dx (or dz): a fused bias gradient
       }
     }
 #pragma unroll
@@ -223,7 +246,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
       const int c = lane + 64 * i;
       if (c < nch) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) red[wave][c * 8 + j] = qn == 0 ? gw[i][j] : (qn == 1 ? gb[i][j] : gs[i][j]);
+        for (int j = 0; j < W; ++j) red[wave][c * W + j] = qn == 0 ? gw[i][j] : (qn == 1 ? gb[i][j] : gs[i][j]);
       }
     }
     __syncthreads();
@@ -234,6 +257,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
 
 }  // namespace
 }  // namespace pvr
+
+static int device_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    return cus;
+  }();
+  return n;
+}
 
 extern "C" hipError_t pvr_layernorm_fwd(const uint16_t* x, int64_t x_stride, const float* w, const float* b,
                                         uint16_t* y, int64_t y_stride, float* mean, float* rstd, int rows, int D,
@@ -260,22 +294,46 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
-  static const int cap = [] {  // PVR_LN_BWD_BLOCKS: grid cap (A/B of row pipelining vs atomics per column)
+  static const int cap_env = [] {  // PVR_LN_BWD_BLOCKS: grid cap (A/B of row pipelining vs atomics per column)
     const char* e = getenv("PVR_LN_BWD_BLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 1024;
+    return e ? atoi(e) : 0;
   }();
+  // PVR_LN_BWD_W4 (A/B): 0 = 16-B chunks always; 1 = 4-column chunks where they tile the row exactly.
+  // ViT-B/16 b256 (profiles/r2s/ln_bwd_w4_ab.log): 79 -> 64 us per call (91 -> 79 with the linked
+  // dropout backward), step neutral-to-+0.3 %; forcing 4 waves/SIMD (<= 128 VGPRs) spilled 18 VGPRs and
+  // took 114 us.
+  static const int w4 = [] {
+    const char* e = getenv("PVR_LN_BWD_W4");
+    return e ? atoi(e) : 1;
+  }();
+  // 4-column chunks when they tile the row over the 64 lanes exactly and 8-column ones do not
+  const bool use_w4 = w4 && (D / 4) % 64 == 0 && (D / 8) % 64 != 0 && D / 4 <= 64 * 5;
+  // D = 768 on 4-column chunks (146 VGPRs, 3 blocks per CU): one grid of exactly the resident blocks,
+  // so no block starts late; otherwise 1024
+  const int cap = cap_env > 0 ? cap_env : (use_w4 && D == 768 ? device_cus() * 3 : 1024);
   int nblk = (rows + 3) / 4;
   // 1024 blocks (4 per CU, ~12 pipelined rows per wave): in-step 0.2 % ahead of 512 and 768
   // (profiles/ln_bwd_grid_step_ab_r2.log); 2048 was 22 % slower in isolation, its 2048 x 3 x D column
   // atomics contending on the same addresses (profiles/kbench_ln_grid.log)
   if (nblk > cap) nblk = cap;
   const dim3 grid(nblk), block(256);
-  const int maxch = (D / 8 + 63) / 64;
-  switch (maxch) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D); break;
+#define PVR_LN_BWD(MC, W)                                                                                                   \
+  hipLaunchKernelGGL((ln_bwd_kernel<MC, W>), grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, \
+                     dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D)
+  if (use_w4) {
+    switch (D / 256) {
+      case 3: PVR_LN_BWD(3, 4); break;  // D = 768
+      case 5: PVR_LN_BWD(5, 4); break;  // D = 1280
+      default: PVR_LN_BWD(1, 4); break;  // D = 256
+    }
+  } else {
+    const int maxch = (D / 8 + 63) / 64;
+    switch (maxch) {
+      case 1: PVR_LN_BWD(1, 8); break;
+      case 2: PVR_LN_BWD(2, 8); break;
+      default: PVR_LN_BWD(3, 8); break;
+    }
   }
+#undef PVR_LN_BWD
   return hipGetLastError();
 }

@@ -221,6 +221,35 @@ def check_layernorm(T, D):
     return (f"layernorm T{T} D{D}", max(e1, e2, e3 / 10, e4 / 10), 2e-2)
 
 
+def check_layernorm_linked(T, D, p=0.1):
+    """LayerNorm backward with everything the encoder block fuses into it: residual gradient,
+    dgamma/dbeta, the producing layer's dropout backward (dz) and its bias gradient (column sums of
+    dz). dz's mask must be the colsum kernel's mask for the same (seed, offset) — one hash everywhere."""
+    ext = _ext.ext()
+    x = bf(rnd(T, D) * 2 + 0.5)
+    w, b = rnd(D) * 0.5 + 1, rnd(D) * 0.1
+    y, mean, rstd = ext.layernorm_fwd(x, w, b, 1e-5, T, D)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (D,), wr, br, 1e-5)
+    dy, dres = bf(rnd(T, D)), bf(rnd(T, D))
+    ref.backward(dy.float())
+    seed = torch.tensor([31337], dtype=torch.int64, device=DEV)
+    off = 11 << 32
+    dx, dz = torch.empty_like(x), torch.empty_like(x)
+    dw, db, dsum = (torch.zeros(D, device=DEV) for _ in range(3))
+    ext.layernorm_bwd(dy, D, x, D, mean, rstd, w, dres, D, dx, D, dw, db, T, dsum, dz, seed, off, p)
+    dx_ref = xr.grad + dres.float()
+    keep = torch.empty_like(x)
+    G.bias_grad(bf(torch.ones(T, D, device=DEV)), torch.zeros(D, device=DEV), drop=(seed, off, p), dz=keep)
+    keep = keep.float() != 0
+    dz_ref = torch.where(keep, dx.float() / (1 - p), torch.zeros_like(dx.float()))
+    e = max(rel_err(dx, dx_ref), rel_err(dw, wr.grad) / 10, rel_err(db, br.grad) / 10, rel_err(dz, dz_ref),
+            rel_err(dsum, dz.float().sum(0)) / max(1.0, T / 64))
+    rate = 1 - keep.float().mean().item()
+    return (f"layernorm bwd + dropout dz + dsum T{T} D{D} (rate {rate:.3f})", e + abs(rate - p), 2e-2)
+
+
 # ----------------------------------------------------------------------------- attention
 def _attn_ref(qkv, B, N, H):
     D = qkv.shape[1] // 3
@@ -768,6 +797,11 @@ def all_checks() -> List[Callable]:
         lambda: check_layernorm(394, 768),
         lambda: check_layernorm(100, 1024),
         lambda: check_layernorm(33, 1280),
+        lambda: check_layernorm(5000, 768),       # 4-column chunks, grid of resident blocks, grid-stride rows
+        lambda: check_layernorm(3000, 1280),
+        lambda: check_layernorm_linked(5000, 768),
+        lambda: check_layernorm_linked(777, 1280),
+        lambda: check_layernorm_linked(1000, 1024),
         lambda: check_attn_fwd(2, 197, 3),
         lambda: check_attn_fwd(1, 17, 2),
         lambda: check_attn_fwd(1, 577, 2),
