@@ -333,3 +333,64 @@ def test_side_stream_matches_serial_weight_gradients(monkeypatch):
         assert torch.allclose(a, b, rtol=1e-3, atol=1e-6), (a - b).abs().max().item()
     for a, b in zip(pa, pb):
         assert torch.allclose(a, b, rtol=1e-3, atol=1e-5)
+
+
+def _gloo_gpu_worker(rank, world, port, out_dir):
+    """One rank of a 2-process DDP run whose ranks SHARE cuda:0 (gloo carries the gradients: RCCL
+    needs one GPU per rank). Exercises the fused path's cross-rank bucket protocol exactly as a
+    multi-GPU run does: weight gradients on the side stream, gradient-ready notifications, buckets
+    launched in index order on every rank, end-of-backward join, all on a high-priority main stream."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(100 + rank)  # different init per rank: the rank-0 broadcast must fix it
+    m = ViT(**dict(CFG, mlp_dropout=0.0, embedding_dropout=0.0)).to(dev)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.1)
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(4 * world, 3, 64, 64, generator=g)
+    y = torch.randint(0, 10, (4 * world,), generator=g)
+    xs, ys = x[4 * rank:4 * rank + 4].to(dev), y[4 * rank:4 * rank + 4].to(dev)
+    main = torch.cuda.Stream(device=dev, priority=-1)
+    main.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(main):
+        for _ in range(2):  # the second step re-arms the buckets
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.grad.zero_()
+            cross_entropy(ddp(xs), ys).backward()
+    torch.cuda.synchronize()
+    torch.save({"state": {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                "grads": {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()},
+                "nbuckets": len(ddp._buckets), "x": x, "y": y}, os.path.join(out_dir, f"g{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_two_ranks_fused_path_matches_single_process(tmp_path):
+    import torch.multiprocessing as mp
+
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+
+    world = 2
+    mp.spawn(_gloo_gpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"g{i}.pt", weights_only=True) for i in range(world)]
+    assert r[0]["nbuckets"] > 2
+    for k in r[0]["state"]:
+        assert torch.equal(r[0]["state"][k], r[1]["state"][k]), f"params differ after broadcast: {k}"
+    for n in r[0]["grads"]:
+        assert torch.equal(r[0]["grads"][n], r[1]["grads"][n]), f"averaged gradient differs across ranks: {n}"
+    dev = torch.device("cuda:0")
+    ref = ViT(**dict(CFG, mlp_dropout=0.0, embedding_dropout=0.0)).to(dev)
+    ref.load_state_dict(r[0]["state"])
+    cross_entropy(ref(r[0]["x"].to(dev)), r[0]["y"].to(dev)).backward()
+    torch.cuda.synchronize()
+    for n, p in ref.named_parameters():
+        a, b = r[0]["grads"][n].float(), p.grad.detach().cpu().float()
+        err = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        assert err < 2e-2, f"{n}: DDP(2 ranks) vs single-process gradient rel err {err:.3e}"
