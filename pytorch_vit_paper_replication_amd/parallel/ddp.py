@@ -6,7 +6,9 @@ Design, MI355X-first rather than a copy of torch 
     collective is one large message (xGMI links are point-to-point: few, big transfers);
   * parameters are broadcast from rank 0 with ONE collective over the flat master buffer (C1);
   * buckets are formed in reverse registration order (= backward order, last encoder block first),
-    ``bucket_cap_mb`` each (default ≈ one ViT-B encoder block: 28 MB of fp32 gradients);
+    ``bucket_cap_mb`` each (default ≈ one ViT-B encoder block: 28 MB of fp32 gradients), except that
+    the first-registered parameters (the embedding, whose gradients come last) form a final bucket of
+    at most 4 MB: the first block's bucket then overlaps the embedding backward;
   * the fused backward Functions (or autograd hooks on the PyTorch path) report parameters as final;
     a full bucket is all-reduced immediately with ``async_op=True`` — RCCL runs it on its own stream
     ordered after the gradient kernels already queued, so it overlaps the remaining backward;
@@ -109,11 +111,24 @@ class DistributedDataParallel(nn.Module):
             store.refresh_shadow(force=True)
         if self.comm_dtype is not None and self.comm_dtype != store.grad_flat.dtype:
             self._comm_buf = torch.empty(store.numel, dtype=self.comm_dtype, device=store.grad_flat.device)
-        # buckets: reverse parameter order, contiguous flat ranges of about bucket_cap bytes
+        # The parameters registered first (ViT: class token, position embedding, patch conv) receive
+        # their gradients LAST, after the whole encoder backward: they get a small bucket of their own
+        # (<= 4 MB), so the bucket before it (the first encoder block) is all-reduced while the
+        # embedding backward still runs and only a few MB of collective remain after backward.
+        tail_cap = min(self.bucket_cap, 4 << 20)
+        tail: List[int] = []
+        tail_bytes = 0
+        for i in range(len(store.params)):
+            nb = store.params[i].numel() * 4
+            if tail and tail_bytes + nb > tail_cap:
+                break
+            tail.append(i)
+            tail_bytes += nb
+        # the rest: reverse parameter order, contiguous flat ranges of about bucket_cap bytes
         buckets = []
         cur: List[int] = []
         cur_bytes = 0
-        for i in reversed(range(len(store.params))):
+        for i in reversed(range(len(tail), len(store.params))):
             cur.append(i)
             cur_bytes += store.params[i].numel() * 4
             if cur_bytes >= self.bucket_cap:
@@ -121,6 +136,8 @@ class DistributedDataParallel(nn.Module):
                 cur, cur_bytes = [], 0
         if cur:
             buckets.append(cur)
+        if tail:
+            buckets.append(list(reversed(tail)))
         self._buckets = []
         self._bucket_of = {}
         for bi, idxs in enumerate(buckets):

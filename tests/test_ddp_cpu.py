@@ -96,3 +96,31 @@ def test_engine_under_ddp_consistent_across_ranks(tmp_path):
     a, b = (torch.load(tmp_path / f"e{i}.pt", weights_only=True) for i in range(world))
     assert a["res"] == b["res"]
     assert torch.equal(a["w"], b["w"]), "replicas diverged"
+
+
+def test_embedding_gets_a_small_final_bucket():
+    """The first-registered parameters (class token, position embedding, patch conv) receive their
+    gradients last: they must sit in a small bucket of their own, so the first encoder block's bucket
+    is all-reduced while the embedding backward runs and only a few MB remain after backward."""
+    from pytorch_vit_paper_replication_amd.models import vit
+    from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        m = vit("vit_b16")
+        ddp = DistributedDataParallel(m, bucket_cap_mb=28.0)
+        st = ddp._setup(torch.device("cpu"))
+        names = {id(p): n for n, p in m.named_parameters()}
+        last = {names[id(st.params[i])] for i in ddp._buckets[-1][2]}
+        lo, hi, _ = ddp._buckets[-1]
+        assert (hi - lo) * 4 <= 4 << 20
+        assert {"patch_embedding_block.class_token", "patch_embedding_block.position_embedding",
+                "patch_embedding_block.patch_and_flatten.0.weight"} <= last
+        before = {names[id(st.params[i])] for i in ddp._buckets[-2][2]}
+        assert not any(n.startswith("patch_embedding_block") for n in before)
+        # buckets tile the flat gradient buffer exactly, in reverse registration order
+        spans = sorted((lo, hi) for lo, hi, _ in ddp._buckets)
+        assert spans[0][0] == 0 and spans[-1][1] == st.numel
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    finally:
+        dist.destroy_process_group()
