@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
     p.add_argument("--bucket-mb", type=float, default=28.0)
     p.add_argument("--graph", action="store_true", help="replay the whole training step as one captured hipGraph")
+    p.add_argument("--infer", action="store_true",
+                   help="serving throughput instead: eval-mode forward under inference_mode (no backward / optimizer)")
     p.add_argument("--main-prio", type=int, default=int(os.environ.get("PVR_MAIN_PRIO", "-1")),
                    help="run the step on a stream of this priority: -1 (default) puts the dgrad chain above the weight-gradient side stream; 0 = default stream")
     return p.parse_args()
@@ -108,6 +110,11 @@ def main():
     x = torch.rand(per_gpu, 3, args.image_size, args.image_size, device=device, generator=g)
     y = torch.randint(0, args.num_classes, (per_gpu,), device=device, generator=g)
 
+    def infer_step():
+        amp = torch.autocast("cuda", dtype=torch.bfloat16) if args.impl == "torch" else contextlib.nullcontext()
+        with torch.inference_mode(), amp:
+            return model(x).float().logsumexp(-1).mean()
+
     def step():
         net.train()
         if args.impl == "fused":
@@ -127,6 +134,11 @@ def main():
         sched.step()
         return loss
 
+    if args.infer:
+        if args.graph:
+            raise SystemExit("--infer: eager forward only")
+        model.eval()
+        step = infer_step  # noqa: F811
     if args.graph:
         if args.impl != "fused" or use_ddp:
             raise SystemExit("--graph: single-process fused path only")
@@ -172,7 +184,8 @@ def main():
     seq = (args.image_size // int(model.config["patch_size"])) ** 2 + 1
     if rank == 0:
         out = {
-            "metric": ("images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
+            "metric": (f"inference images/sec (whole node) {name} {args.image_size}px {args.dtype}" if args.infer else
+                       "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
                        if (name, args.image_size, args.dtype) == ("ViT-B/16", 224, "bf16")
                        else f"images/sec (whole node) {name} {args.image_size}px {args.dtype}"),
             "value": round(ips, 2),
@@ -193,8 +206,10 @@ def main():
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
                        "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl + ("+hipgraph" if args.graph else ""),
                        "grad_transport": net.transport if use_ddp else "none",
-                       "optimizer": "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
-                       "dropout": "0.1 (mlp, embedding)", "final_loss": round(final_loss, 4)},
+                       "optimizer": "none (inference: eval forward under inference_mode)" if args.infer else
+                       "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
+                       "dropout": "off (eval)" if args.infer else "0.1 (mlp, embedding)",
+                       "final_loss": round(final_loss, 4)},
         }
         print(json.dumps(out), flush=True)
     if use_ddp:

@@ -128,7 +128,7 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   if (resid.has_value() && resid->defined()) { p.resid = bf(*resid, "resid"); p.ld_resid = ld_of(*resid, "resid"); }
   if (addend.has_value() && addend->defined()) { p.addend = f32(*addend, "addend"); p.addend_period = (int)addend_period; TORCH_CHECK(addend_period > 0, "addend_period"); }
   if (aux.has_value() && aux->defined()) { p.aux = const_cast<uint16_t*>(bf(*aux, "aux")); p.ld_aux = ld_of(*aux, "aux"); }
-  if (epi == 1 || epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm: GELU epilogues need aux");
+  if (epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm: the dGELU epilogue needs aux");  // GELU: aux optional (inference)
   p.row_group = (int)row_group; p.row_stride_group = (int)row_stride_group; p.row_offset = (int)row_offset;
   if (drop_p > 0.0) {
     TORCH_CHECK(seed.has_value() && seed->defined() && seed->scalar_type() == torch::kInt64, "dropout needs an int64 seed tensor");

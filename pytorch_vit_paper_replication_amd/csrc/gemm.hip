@@ -217,8 +217,10 @@ PVR_DEV void epilogue(const GemmParams& p, v4f (&acc)[FM][FN], int mb, int nb, i
               v[r] = gv * sc;
               gp[r] = gd * sc;
             }
-            uint2 a; a.x = pack2bf(gp[0], gp[1]); a.y = pack2bf(gp[2], gp[3]);
-            *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = a;
+            if (p.aux) {  // no aux: inference (nothing to save for a backward)
+              uint2 a; a.x = pack2bf(gp[0], gp[1]); a.y = pack2bf(gp[2], gp[3]);
+              *(uint2*)(p.aux + (int64_t)m * p.ld_aux + n) = a;
+            }
             uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
             *(uint2*)((uint16_t*)p.C + orow * p.ldc + n) = o;
           } else if constexpr (EPI == EPI_DGELU) {
@@ -1025,7 +1027,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
     }
     const uint64_t idx0 = (uint64_t)mrow0 * p.N + n, idx_step = 8ull * p.N;
     uint16_t* c0 = (uint16_t*)p.C + (int64_t)mrow0 * p.ldc + n;
-    uint16_t* x0 = EPI == EPI_GELU ? p.aux + (int64_t)mrow0 * p.ld_aux + n : nullptr;
+    uint16_t* x0 = EPI == EPI_GELU && p.aux ? p.aux + (int64_t)mrow0 * p.ld_aux + n : nullptr;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int r = (tid >> 6) + 8 * k;
@@ -1065,7 +1067,7 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
           g01 *= s01; g23 *= s23; d01 *= s01; d23 *= s23;
           v[0] = g01.x; v[1] = g01.y; v[2] = g23.x; v[3] = g23.y;
           uint2 ax; ax.x = pack2bf(d01.x, d01.y); ax.y = pack2bf(d23.x, d23.y);
-          if (ok) *(uint2*)(x0 + (int64_t)k * (8 * p.ld_aux)) = ax;
+          if (ok && p.aux) *(uint2*)(x0 + (int64_t)k * (8 * p.ld_aux)) = ax;  // no aux: inference
         }
       } else if constexpr (EPI == EPI_DGELU) {
         const uint2 gg = pin[k];

@@ -249,6 +249,7 @@ class ViT(nn.Module):
         store.ensure_transposed()
         training = self.training
         grad = torch.is_grad_enabled()
+        store.grad_enabled = grad  # the fused Functions' forward runs with grad mode off: tell them
         if grad:
             store.prepare_grads()
         need_seed = training and (c["mlp_dropout"] > 0 or c["embedding_dropout"] > 0)

@@ -42,7 +42,8 @@ class ViT(_FullViT):
             store._vit_t_registered = True
         store.ensure_transposed()
         training = self.training
-        if torch.is_grad_enabled():
+        store.grad_enabled = torch.is_grad_enabled()  # the fused Functions' forward runs with grad mode off
+        if store.grad_enabled:
             store.prepare_grads()
         need_seed = training and (c["mlp_dropout"] > 0 or c["embedding_dropout"] > 0)
         seed = self._dropout_seed(dev) if need_seed else None

@@ -174,14 +174,19 @@ class EncoderBlockFn(torch.autograd.Function):
         ctx.f8d = f8 if f8 is not None and f8[0].dgrad else None
         M = w1.shape[0]
         scale = 1.0 / math.sqrt(D // H)
-        u = torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
+        # inference (grad mode off at the model call: eval under no_grad / inference_mode; a Function's
+        # forward itself always runs with grad mode off, and ctx.needs_input_grad ignores the caller's
+        # mode): the fc1 epilogue stores no GELU derivative and nothing is saved for a backward
+        need_bwd = getattr(store, "grad_enabled", True) and any(ctx.needs_input_grad)
+        u = (torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
+             if need_bwd or f8 is not None else None)
         xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
         if f8 is None:
             qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
             o, lse = ext.attn_fwd(qkv, B, N, H, scale)
             x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=x)
             xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
-            h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=drop1)
+            h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, gelu=True, drop=drop1)
             x2 = gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=drop2)
         else:
             # fp8 forward GEMMs (e4m3 x e4m3, per-tensor delayed scaling); everything the backward
@@ -201,7 +206,8 @@ class EncoderBlockFn(torch.autograd.Function):
             h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1)
             a, s_ = st.act_quant(h, blk, 3)
             x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
-        ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
+        if need_bwd:
+            ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
         ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
         return x2
 

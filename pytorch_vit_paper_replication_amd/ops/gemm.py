@@ -56,18 +56,20 @@ def _drop_args(drop: Drop):
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
                resid: Optional[torch.Tensor] = None, drop: Drop = None, gelu_aux: Optional[torch.Tensor] = None,
+               gelu: bool = False,
                addend: Optional[torch.Tensor] = None, addend_period: int = 0,
                row_remap: Tuple[int, int, int] = (0, 0, 0), out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = resid + dropout(x.w^T + bias + addend[row % period]).
 
     GELU variant (``gelu_aux`` given): u = x.w^T + bias, y = dropout(gelu(u)) and gelu_aux receives
-    mask * scale * gelu'(u) — exactly the factor ``linear_dgrad(..., dgelu_aux=)`` multiplies by."""
+    mask * scale * gelu'(u) — exactly the factor ``linear_dgrad(..., dgelu_aux=)`` multiplies by.
+    ``gelu=True`` without ``gelu_aux``: the GELU epilogue for inference (no derivative stored)."""
     T, K = x.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty(T, N, dtype=torch.bfloat16, device=x.device)
     seed, soff, p = _drop_args(drop)
-    epi = EPI_GELU if gelu_aux is not None else EPI_BF16
+    epi = EPI_GELU if (gelu or gelu_aux is not None) else EPI_BF16
     _ext.ext().gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
                     row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, _tile(T, N, K, "fwd", epi == EPI_GELU))
     return out

@@ -668,6 +668,38 @@ def check_vit_fused_vs_reference(B=4, train=False, **over):
     return (f"vit fused vs fp32 ref (fwd {e_fwd:.2e}, worst grad {worst})", max(e_fwd, e_g / 3), 5e-2)
 
 
+def check_vit_inference(B=5):
+    """Inference path (eval under no_grad / inference_mode): the fc1 epilogue skips the GELU
+    derivative and nothing is saved; logits must equal the grad-mode fused forward bit for bit and
+    match the fp32 reference; a later training step on the same model still gets gradients."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+
+    torch.manual_seed(0)
+    cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=128, mlp_size=256,
+               num_classes=10)
+    m = ViT(**cfg).to(DEV).eval()
+    mr = ViT(**cfg).to(DEV).eval()
+    mr.load_state_dict(m.state_dict())
+    x = torch.rand(B, 3, 64, 64, device=DEV)
+    lg = m(x)
+    with torch.no_grad():
+        ln = m(x)
+    with torch.inference_mode():
+        li = m(x)
+    os.environ["PVR_DISABLE_FUSED"] = "1"
+    try:
+        with torch.no_grad():
+            lr = mr(x)
+    finally:
+        os.environ["PVR_DISABLE_FUSED"] = "0"
+    same = torch.equal(lg.detach(), ln) and torch.equal(ln, li)
+    m.train()
+    F.cross_entropy(m(x), torch.randint(0, 10, (B,), device=DEV)).backward()
+    has_grad = all(p.grad is not None and torch.isfinite(p.grad).all().item() for p in m.parameters())
+    err = rel_err(li, lr) + (0 if same else 1) + (0 if has_grad else 1)
+    return (f"vit inference (no_grad / inference_mode) == grad-mode logits {same}, vs fp32 ref", err, 5e-2)
+
+
 def check_vit_block_link(B=3):
     """Dropout on: the fc2 dropout backward + bias gradient fused into the next block's LayerNorm
     backward (BlockLink) vs each block's own column-sum pass, same dropout masks."""
@@ -862,6 +894,7 @@ def all_checks() -> List[Callable]:
         lambda: check_xent(3, 3),
         lambda: check_adam(),
         lambda: check_vit_fused_vs_reference(4, False),
+        check_vit_inference,
         lambda: check_vit_fused_vs_reference(3, True),
         lambda: check_vit_block_link(),
         lambda: check_vit_micro(),
