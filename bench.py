@@ -135,11 +135,28 @@ def main():
         return loss
 
     if args.infer:
-        if args.graph:
-            raise SystemExit("--infer: eager forward only")
         model.eval()
         step = infer_step  # noqa: F811
-    if args.graph:
+        if args.graph:
+            # serving at small batch: the eval forward captured once as a hipGraph, replayed per batch
+            if args.impl != "fused":
+                raise SystemExit("--infer --graph: fused path only")
+            side = torch.cuda.Stream(device=device)
+            side.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    infer_step()
+            torch.cuda.current_stream(device).wait_stream(side)
+            torch.cuda.synchronize()
+            ig = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ig):
+                static_out = infer_step()
+
+            def step():  # noqa: F811
+                ig.replay()
+                return static_out
+            args.warmup = max(args.warmup, 1)
+    if args.graph and not args.infer:
         if args.impl != "fused" or use_ddp:
             raise SystemExit("--graph: single-process fused path only")
         from pytorch_vit_paper_replication_amd.runtime.graph import GraphedTrainStep
