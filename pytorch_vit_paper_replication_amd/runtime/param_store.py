@@ -46,6 +46,9 @@ class ParamStore:
             params.append(p)
             names.append(n)
         self.device = _norm_device(device)
+        # grad mode at the model call, set by the model's fused forward: the autograd Functions' own
+        # forward always runs with grad mode off, so an inference call is told here (no saved tensors)
+        self.grad_enabled = True
         self.params = params
         self.names = names
         self.offsets: List[int] = []
