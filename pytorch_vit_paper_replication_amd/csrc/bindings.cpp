@@ -48,6 +48,8 @@ int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
 int pvr_attn_dbias_splits(int, int);
+hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float*, const uint16_t*, int64_t, int, uint16_t*, int64_t,
+                               hipStream_t);
 hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, int, hipStream_t);
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float, hipStream_t);
 }
@@ -208,6 +210,28 @@ void splitk_reduce(torch::Tensor ws, int64_t S, torch::Tensor out, bool accumula
               "splitk_reduce: layouts");
   check(pvr_splitk_reduce(f32(ws, "ws"), (int)S, ws.stride(0), f32_mut(out, "out"), out.numel(), accumulate ? 1 : 0, stream()),
         "splitk_reduce");
+}
+
+// out = bf16(epilogue(ws.sum(0))) for a split-K workspace ws [S, M, N]: + bias, GELU (inference: no
+// derivative), + resid (the small-M forward GEMM's reduction pass)
+void splitk_epilogue(torch::Tensor ws, int64_t S, torch::Tensor out, c10::optional<torch::Tensor> bias,
+                     c10::optional<torch::Tensor> resid, bool gelu) {
+  TORCH_CHECK(ws.dim() == 3 && ws.size(0) >= S && S >= 1 && ws.stride(2) == 1 && ws.stride(1) == ws.size(2),
+              "splitk_epilogue: ws must be [S, M, N] with contiguous rows");
+  const int64_t M = ws.size(1), N = ws.size(2);
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && N % 4 == 0, "splitk_epilogue: out shape");
+  const int64_t ldc = ld_of(out, "out");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() >= N && bias->is_contiguous(), "splitk_epilogue: bias");
+    bp = f32(*bias, "bias");
+  }
+  const uint16_t* rp = nullptr;
+  int64_t ldr = 0;
+  if (resid.has_value() && resid->defined()) { rp = bf(*resid, "resid"); ldr = ld_of(*resid, "resid"); }
+  check(pvr_splitk_epilogue(f32(ws, "ws"), (int)S, ws.stride(0), (int)M, (int)N, bp, rp, ldr, gelu ? 1 : 0, bf_mut(out, "out"), ldc,
+                            stream()),
+        "splitk_epilogue");
 }
 
 void cast_f32_bf16(torch::Tensor in, torch::Tensor out) {
@@ -574,6 +598,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none(),
         py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("splitk_epilogue", &splitk_epilogue);
   m.def("attn_bwd_pipe_path", &attn_bwd_pipe_path);
   m.def("attn_dbias_reduce", &attn_dbias_reduce);
   m.def("splitk_reduce", &splitk_reduce);

@@ -441,3 +441,71 @@ extern "C" hipError_t pvr_patch_bwd(const uint16_t* dE, int B, int ntok, int D, 
 }
 
 extern "C" int pvr_patch_bwd_groups(int B) { return (B + pvr::PB_BAT - 1) / pvr::PB_BAT; }
+
+// Second half of the small-M split-K forward GEMM (few output tiles: serving-size batches): sum the
+// S fp32 partial products ws[s][m][n] in a fixed order (deterministic) and apply the forward
+// epilogue: + bias, exact-erf GELU (no derivative saved: inference), + residual, bf16 store.
+// One thread per 4 consecutive columns of a row (N % 4 == 0).
+namespace pvr {
+namespace {
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float* __restrict__ ws, int S, int64_t stride, int M, int N,
+                                                              const float* __restrict__ bias, const uint16_t* __restrict__ resid,
+                                                              int64_t ld_resid, int gelu, uint16_t* __restrict__ out, int64_t ldc) {
+  const int n4 = N / 4;
+  const int64_t total = (int64_t)M * n4;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / n4), n = (int)(i % n4) * 4;
+    const float* src = ws + (int64_t)m * N + n;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {  // 4 independent loads in flight per trip
+      const float4 b0 = *(const float4*)(src + (int64_t)s * stride);
+      const float4 b1 = *(const float4*)(src + (int64_t)(s + 1) * stride);
+      const float4 b2 = *(const float4*)(src + (int64_t)(s + 2) * stride);
+      const float4 b3 = *(const float4*)(src + (int64_t)(s + 3) * stride);
+      a.x += (b0.x + b1.x) + (b2.x + b3.x);
+      a.y += (b0.y + b1.y) + (b2.y + b3.y);
+      a.z += (b0.z + b1.z) + (b2.z + b3.z);
+      a.w += (b0.w + b1.w) + (b2.w + b3.w);
+    }
+    for (; s < S; ++s) {
+      const float4 b = *(const float4*)(src + (int64_t)s * stride);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    if (bias) {
+      const float4 b = *(const float4*)(bias + n);
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    if (gelu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float g, gp;
+        gelu_and_grad(v[r], g, gp);
+        v[r] = g;
+      }
+    }
+    if (resid) {
+      const uint2 rr = *(const uint2*)(resid + (int64_t)m * ld_resid + n);
+      v[0] += bf2f(rr.x & 0xFFFF); v[1] += bf2f(rr.x >> 16);
+      v[2] += bf2f(rr.y & 0xFFFF); v[3] += bf2f(rr.y >> 16);
+    }
+    uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
+    *(uint2*)(out + (int64_t)m * ldc + n) = o;
+  }
+}
+}  // namespace
+}  // namespace pvr
+
+extern "C" hipError_t pvr_splitk_epilogue(const float* ws, int S, int64_t stride, int M, int N, const float* bias,
+                                          const uint16_t* resid, int64_t ld_resid, int gelu, uint16_t* out, int64_t ldc,
+                                          hipStream_t s) {
+  using namespace pvr;
+  if (M <= 0 || N <= 0) return hipSuccess;
+  if (N % 4 || S < 1) return hipErrorInvalidValue;
+  int64_t blocks = ((int64_t)M * (N / 4) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, S, stride, M, N, bias, resid, ld_resid,
+                     gelu, out, ldc);
+  return hipGetLastError();
+}

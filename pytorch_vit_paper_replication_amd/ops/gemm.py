@@ -48,6 +48,25 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
     return 0
 
 
+# Small-M forward GEMMs (serving-size batches) split K when the 256x256 output tiles cannot fill the
+# chip: PVR_SMALL_SPLITK=0 keeps them on one tile per workgroup (A/B)
+_SMALL_SPLITK = os.environ.get("PVR_SMALL_SPLITK", "1") == "1"
+
+
+def _small_splitk(T: int, N: int, K: int) -> int:
+    """K splits for a forward GEMM on 256x256 tiles (T >= 2048) with fewer than 128 output tiles
+    (0: do not split). Each split keeps at least two 64-deep K-tiles; the splits aim at ~256
+    workgroups. Measured (profiles/r2s/small_splitk_ab.log): eval forward at batch 32 +5 %; below
+    2048 rows the 128x128 one-pass tiles are faster (batch 1: 1.32 ms unsplit vs 1.89 split)."""
+    if not _SMALL_SPLITK or K % 128 or N % 4 or T < 2048:
+        return 0
+    tiles = math.ceil(T / 256) * math.ceil(N / 256)
+    if tiles >= 128:
+        return 0
+    s = min(K // 128, max(2, 256 // tiles))
+    return s if s >= 2 else 0
+
+
 def _drop_args(drop: Drop):
     if drop is None or drop[2] <= 0.0:
         return None, 0, 0.0
@@ -70,6 +89,17 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
         out = torch.empty(T, N, dtype=torch.bfloat16, device=x.device)
     seed, soff, p = _drop_args(drop)
     epi = EPI_GELU if (gelu or gelu_aux is not None) else EPI_BF16
+    S = _small_splitk(T, N, K) if (p == 0.0 and gelu_aux is None and addend is None and row_remap[0] == 0) else 0
+    if S:
+        # serving-size batch: split K over workgroups (fp32 partials, tile 14), then one pass sums
+        # them and applies bias / GELU / residual
+        ksplit = math.ceil(math.ceil(K / S) / 64) * 64
+        nsplit = math.ceil(K / ksplit)
+        ws = _workspace(nsplit * T * N, x.device)[:nsplit * T * N].view(nsplit, T, N)
+        ext = _ext.ext()
+        ext.gemm(x, True, w, True, ws, T, N, K, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0, None, 0, 0.0, ksplit, 14)
+        ext.splitk_epilogue(ws, nsplit, out, bias, resid, epi == EPI_GELU)
+        return out
     _ext.ext().gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
                     row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, _tile(T, N, K, "fwd", epi == EPI_GELU))
     return out

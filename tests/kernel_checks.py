@@ -93,6 +93,22 @@ def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13)):
     return (f"gemm_gelu+dropout M{M} N{N} K{K} tiles{tiles} (drop rate {rate:.4f})", err, 1e-2)
 
 
+def check_gemm_small_splitk(M, N, K, resid=False, gelu=False):
+    """Serving-size forward GEMM (few output tiles): split-K fp32 partials + the reduction pass with
+    bias / exact GELU / residual, vs a PyTorch fp32 reference."""
+    S = G._small_splitk(M, N, K)
+    x, w, b = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05)), rnd(N)
+    r = bf(rnd(M, N)) if resid else None
+    y = G.linear_fwd(x, w, b, resid=r, gelu=gelu)
+    ref = x.float() @ w.float().t() + b
+    if gelu:
+        ref = F.gelu(ref)
+    if resid:
+        ref = ref + r.float()
+    return (f"gemm small-M split-K M{M} N{N} K{K} S{S} resid{int(resid)} gelu{int(gelu)}",
+            rel_err(y, ref) + (0 if S >= 2 else 1), 2e-2)
+
+
 def check_gemm_dgrad(M, N, K, tile=0, transposed=False):
     dy, w = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05))
     old = G._FORCE_TILE
@@ -895,6 +911,9 @@ def all_checks() -> List[Callable]:
         lambda: check_adam(),
         lambda: check_vit_fused_vs_reference(4, False),
         check_vit_inference,
+        lambda: check_gemm_small_splitk(6304, 768, 3072, resid=True),   # b32: 75 tiles
+        lambda: check_gemm_small_splitk(6304, 768, 768, resid=True),
+        lambda: check_gemm_small_splitk(2100, 3072, 768, gelu=True),    # 9 x 12 tiles, partial last row tile
         lambda: check_vit_fused_vs_reference(3, True),
         lambda: check_vit_block_link(),
         lambda: check_vit_micro(),
