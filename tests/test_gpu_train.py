@@ -93,6 +93,45 @@ def test_fused_training_tracks_fp32_reference():
     assert cos > 0.9, f"fused vs fp32 update direction cosine {cos:.3f}"
 
 
+def test_full_size_vit_b16_steps_track_fp32_reference():
+    """ViT-B/16 at 224 px (the headline model): 8 training steps of the fused path against the
+    PyTorch fp32 path from the same init on the same batches. scripts/convergence_check.py measured
+    the two losses within 0.005 of each other for the first ~190 steps (profiles/conv/convergence_b16.md)."""
+    from pytorch_vit_paper_replication_amd.models import vit
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay
+
+    torch.manual_seed(0)
+    kw = dict(num_classes=10, mlp_dropout=0.0, embedding_dropout=0.0)
+    mf, mr = vit("vit_b16", **kw).cuda(), vit("vit_b16", **kw).cuda()
+    mr.load_state_dict(mf.state_dict())
+    of = FusedAdam(param_groups_weight_decay(mf, 0.03), lr=1e-4)
+    orf = torch.optim.Adam(param_groups_weight_decay(mr, 0.03), lr=1e-4)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xs = torch.rand(8, 16, 3, 224, 224, device="cuda", generator=g)
+    ys = torch.randint(0, 10, (8, 16), device="cuda", generator=g)
+    lf, lr_ = [], []
+    for x, y in zip(xs, ys):
+        loss = cross_entropy(mf(x), y)
+        of.zero_grad()
+        loss.backward()
+        of.step(clip_norm=1.0)
+        lf.append(loss.item())
+        os.environ["PVR_DISABLE_FUSED"] = "1"
+        try:
+            l2 = F.cross_entropy(mr(x), y)
+        finally:
+            os.environ["PVR_DISABLE_FUSED"] = "0"
+        orf.zero_grad()
+        l2.backward()
+        torch.nn.utils.clip_grad_norm_(mr.parameters(), 1.0)
+        orf.step()
+        lr_.append(l2.item())
+    diffs = [abs(a - b) for a, b in zip(lf, lr_)]
+    print(f"fused {lf}\nfp32  {lr_}\nmax |dloss| {max(diffs):.5f}")
+    assert max(diffs) < 2e-2, (lf, lr_)
+
+
 @pytest.mark.parametrize("comm", ["native", "torch"])
 def test_ddp_rccl_world1_matches_local(comm):
     import torch.distributed as dist
