@@ -37,14 +37,17 @@ def run(path, args, init_sd, data):
     from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
     from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
 
-    os.environ["PVR_DISABLE_FUSED"] = "0" if path == "fused" else "1"
+    fused = path.startswith("fused")
+    os.environ["PVR_DISABLE_FUSED"] = "0" if fused else "1"
     amp = torch.autocast("cuda", dtype=torch.bfloat16, enabled=path == "reference_bf16")
     dev = torch.device("cuda")
     model = vit(args.model, image_size=args.image_size, num_classes=args.classes,
                 mlp_dropout=args.dropout, embedding_dropout=args.dropout).to(dev)
     model.load_state_dict(init_sd)
+    if path == "fused_fp8":
+        model.enable_fp8()  # e4m3 forward, e5m2-gradient dgrad + wgrad GEMMs, delayed scaling
     groups = param_groups_weight_decay(model, 0.03)
-    opt = FusedAdam(groups, lr=args.lr) if path == "fused" else torch.optim.Adam(groups, lr=args.lr)
+    opt = FusedAdam(groups, lr=args.lr) if fused else torch.optim.Adam(groups, lr=args.lr)
     sched = warmup_linear_decay(opt, args.steps, 0.05)
     (xtr, ytr), (xte, yte) = data
     losses = []
@@ -54,7 +57,7 @@ def run(path, args, init_sd, data):
         lo = (s * args.batch) % xtr.shape[0]
         x, y = xtr[lo:lo + args.batch], ytr[lo:lo + args.batch]
         model.train()
-        if path == "fused":
+        if fused:
             loss = cross_entropy(model(x), y)
             opt.zero_grad()
             loss.backward()
@@ -97,6 +100,7 @@ def main():
     p.add_argument("--train-size", type=int, default=2048)
     p.add_argument("--test-size", type=int, default=512)
     p.add_argument("--log", type=int, default=10)
+    p.add_argument("--fp8", action="store_true", help="also train the fused path with enable_fp8() (fp8 GEMMs)")
     args = p.parse_args()
 
     from pytorch_vit_paper_replication_amd import _ext
@@ -131,6 +135,11 @@ def main():
         "max_abs_loss_diff_first10": max(abs(a - b) for a, b in zip(lf[:10], lr_[:10])),
         "mean_abs_loss_diff": sum(abs(a - b) for a, b in zip(lf, lr_)) / len(lf),
     }
+    if args.fp8:
+        f8 = run("fused_fp8", args, init_sd, data)
+        summary["fused_fp8"] = {"first": f8["losses"][0], "last10pct_mean": sum(f8["losses"][-k:]) / k,
+                                "test_loss": f8["test_loss"], "test_acc": f8["test_acc"], "train_s": f8["train_s"],
+                                "max_abs_loss_diff_vs_fused_first50": max(abs(a - b) for a, b in zip(f8["losses"][:50], lf[:50]))}
     print(json.dumps(summary), flush=True)
 
 
