@@ -219,7 +219,7 @@ void splitk_epilogue(torch::Tensor ws, int64_t S, torch::Tensor out, c10::option
   TORCH_CHECK(ws.dim() == 3 && ws.size(0) >= S && S >= 1 && ws.stride(2) == 1 && ws.stride(1) == ws.size(2),
               "splitk_epilogue: ws must be [S, M, N] with contiguous rows");
   const int64_t M = ws.size(1), N = ws.size(2);
-  TORCH_CHECK(out.size(0) == M && out.size(1) == N && N % 4 == 0, "splitk_epilogue: out shape");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && N % 4 == 0, "splitk_epilogue: out shape");
   const int64_t ldc = ld_of(out, "out");
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
@@ -228,7 +228,11 @@ void splitk_epilogue(torch::Tensor ws, int64_t S, torch::Tensor out, c10::option
   }
   const uint16_t* rp = nullptr;
   int64_t ldr = 0;
-  if (resid.has_value() && resid->defined()) { rp = bf(*resid, "resid"); ldr = ld_of(*resid, "resid"); }
+  if (resid.has_value() && resid->defined()) {
+    TORCH_CHECK(resid->dim() == 2 && resid->size(0) >= M && resid->size(1) >= N, "splitk_epilogue: resid must cover [M, N]");
+    rp = bf(*resid, "resid");
+    ldr = ld_of(*resid, "resid");
+  }
   check(pvr_splitk_epilogue(f32(ws, "ws"), (int)S, ws.stride(0), (int)M, (int)N, bp, rp, ldr, gelu ? 1 : 0, bf_mut(out, "out"), ldc,
                             stream()),
         "splitk_epilogue");
