@@ -88,6 +88,24 @@ def run(path, args, init_sd, data):
             "train_s": round(elapsed, 2)}
 
 
+def _with_reference(args, init_sd, data, fused, k):
+    ref = run("reference", args, init_sd, data)
+    ref16 = run("reference_bf16", args, init_sd, data)
+    lf, lr_ = fused["losses"], ref["losses"]
+    return {
+        "model": args.model, "steps": args.steps, "batch": args.batch, "lr": args.lr, "dropout": args.dropout,
+        "fused": {"first": lf[0], "last10pct_mean": sum(lf[-k:]) / k, "test_loss": fused["test_loss"],
+                  "test_acc": fused["test_acc"], "train_s": fused["train_s"]},
+        "reference_fp32": {"first": lr_[0], "last10pct_mean": sum(lr_[-k:]) / k, "test_loss": ref["test_loss"],
+                           "test_acc": ref["test_acc"], "train_s": ref["train_s"]},
+        "reference_autocast_bf16": {"first": ref16["losses"][0], "last10pct_mean": sum(ref16["losses"][-k:]) / k,
+                                    "test_loss": ref16["test_loss"], "test_acc": ref16["test_acc"],
+                                    "train_s": ref16["train_s"]},
+        "max_abs_loss_diff_first10": max(abs(a - b) for a, b in zip(lf[:10], lr_[:10])),
+        "mean_abs_loss_diff": sum(abs(a - b) for a, b in zip(lf, lr_)) / len(lf),
+    }
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--model", default="vit_b16")
@@ -101,6 +119,8 @@ def main():
     p.add_argument("--test-size", type=int, default=512)
     p.add_argument("--log", type=int, default=10)
     p.add_argument("--fp8", action="store_true", help="also train the fused path with enable_fp8() (fp8 GEMMs)")
+    p.add_argument("--no-reference", action="store_true",
+                   help="skip the two PyTorch paths (large models: fused bf16 vs fused fp8 only)")
     args = p.parse_args()
 
     from pytorch_vit_paper_replication_amd import _ext
@@ -119,22 +139,14 @@ def main():
     init_sd = {k: v.clone() for k, v in vit(args.model, image_size=args.image_size, num_classes=args.classes,
                                           mlp_dropout=args.dropout, embedding_dropout=args.dropout).state_dict().items()}
     fused = run("fused", args, init_sd, data)
-    ref = run("reference", args, init_sd, data)
-    ref16 = run("reference_bf16", args, init_sd, data)
-    lf, lr_ = fused["losses"], ref["losses"]
+    lf = fused["losses"]
     k = max(1, args.steps // 10)
-    summary = {
-        "model": args.model, "steps": args.steps, "batch": args.batch, "lr": args.lr, "dropout": args.dropout,
-        "fused": {"first": lf[0], "last10pct_mean": sum(lf[-k:]) / k, "test_loss": fused["test_loss"],
-                  "test_acc": fused["test_acc"], "train_s": fused["train_s"]},
-        "reference_fp32": {"first": lr_[0], "last10pct_mean": sum(lr_[-k:]) / k, "test_loss": ref["test_loss"],
-                           "test_acc": ref["test_acc"], "train_s": ref["train_s"]},
-        "reference_autocast_bf16": {"first": ref16["losses"][0], "last10pct_mean": sum(ref16["losses"][-k:]) / k,
-                                    "test_loss": ref16["test_loss"], "test_acc": ref16["test_acc"],
-                                    "train_s": ref16["train_s"]},
-        "max_abs_loss_diff_first10": max(abs(a - b) for a, b in zip(lf[:10], lr_[:10])),
-        "mean_abs_loss_diff": sum(abs(a - b) for a, b in zip(lf, lr_)) / len(lf),
-    }
+    if args.no_reference:
+        summary = {"model": args.model, "steps": args.steps, "batch": args.batch, "lr": args.lr, "dropout": args.dropout,
+                   "fused": {"first": lf[0], "last10pct_mean": sum(lf[-k:]) / k, "test_loss": fused["test_loss"],
+                             "test_acc": fused["test_acc"], "train_s": fused["train_s"]}}
+    else:
+        summary = _with_reference(args, init_sd, data, fused, k)
     if args.fp8:
         f8 = run("fused_fp8", args, init_sd, data)
         summary["fused_fp8"] = {"first": f8["losses"][0], "last10pct_mean": sum(f8["losses"][-k:]) / k,
