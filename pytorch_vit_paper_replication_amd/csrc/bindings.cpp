@@ -58,6 +58,19 @@ namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// compute units of the current device (the persistent kernels' grid)
+int num_cus() {
+  static std::map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  hipDeviceProp_t prop;
+  int n = hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  cache[dev] = n;
+  return n;
+}
+
 void check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "pvr kernel '", what, "' failed: ", hipGetErrorString(e));
 }
@@ -94,8 +107,10 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
           int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> addend,
           int64_t addend_period, c10::optional<torch::Tensor> aux, int64_t row_group, int64_t row_stride_group,
           int64_t row_offset, c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, int64_t k_split,
-          int64_t tile_cfg, c10::optional<torch::Tensor> dbg, c10::optional<torch::Tensor> colsum) {
+          int64_t tile_cfg, c10::optional<torch::Tensor> dbg, c10::optional<torch::Tensor> colsum,
+          int64_t epi_staged) {
   pvr::GemmParams p{};
+  p.epi_staged = (int)epi_staged;
   if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
   if (dbg.has_value() && dbg->defined()) p.dbg = reinterpret_cast<uint64_t*>(dbg->data_ptr());
   p.drop_scale = 1.f;
@@ -595,7 +610,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),
         py::arg("addend_period"), py::arg("aux"), py::arg("row_group"), py::arg("row_stride_group"),
         py::arg("row_offset"), py::arg("seed"), py::arg("seed_offset"), py::arg("drop_p"), py::arg("k_split"),
-        py::arg("tile_cfg"), py::arg("dbg") = py::none(), py::arg("colsum") = py::none());
+        py::arg("tile_cfg"), py::arg("dbg") = py::none(), py::arg("colsum") = py::none(),
+        py::arg("epi_staged") = 0);
+  m.def("num_cus", &num_cus);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("dy_stride"), py::arg("x"), py::arg("x_stride"),
         py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),

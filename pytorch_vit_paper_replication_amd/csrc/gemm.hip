@@ -932,6 +932,179 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
   pp_barrier();
 }
 
+// Register-direct epilogue of the ping-pong kernels (SWAP layout, bf16-output epilogues, no row
+// remap / position addend, N % 8 == 0). Each wave finishes its own 128x64 output block straight
+// from the accumulators: no LDS staging, no barriers (DGELU colsum excepted), so a wave whose main
+// loop ended early starts storing while its SIMD partner still runs MFMAs.
+//   lane (li = l & 15, g = l >> 4) holds C[mb + 16i + li][nb + 16j + 4g + r] in acc[i][j][r];
+//   one v_permlane16_swap per dword of fragments (j0, j1) = (2jp, 2jp+1) (rows 1, 3 of j0 <-> rows
+//   0, 2 of j1) leaves every lane 8 contiguous columns c0 = nb + 32jp + {0, 16, 8, 24}[g] .. +7,
+// so bias / residual / dGELU-factor loads and output / GELU-derivative stores are 16 B per lane,
+// 16 rows x 64 B per wave instruction (16 stores per wave and output instead of 32 x 8 B through
+// LDS). Buffer resources start at the wave's first row: rows past M read 0 and are not written;
+// lanes whose columns are past N use an out-of-range offset. Same fp32 math as `epilogue` above.
+// epilogue_direct's preconditions: plain row mapping, 16-B column groups, 31-bit buffer offsets
+__host__ __device__ inline bool direct_ok(const GemmParams& p) {
+  const int64_t l1 = p.ldc > p.ld_resid ? p.ldc : p.ld_resid;
+  const int64_t ld = l1 > p.ld_aux ? l1 : p.ld_aux;
+  return !p.addend && !p.row_group && (p.N & 7) == 0 && (int64_t)p.M * ld * 2 < (1ll << 31);
+}
+
+template <int EPI, bool RES>
+PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, int mb, int nb, int wm, int wn, int lane) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const int li = lane & 15, g = lane >> 4;
+  const float deq = p.scale_a ? (*p.scale_a) * (*p.scale_b) : 1.f;
+  // rows [mb, min(M, mb + 128)) of C (and of the residual / aux tensors) from the wave's first row
+  const int rows = max(0, min(128, p.M - mb));
+  const uint32_t OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t crs = make_rsrc((const uint16_t*)p.C + (int64_t)mb * p.ldc, rows ? (uint32_t)(((int64_t)(rows - 1) * p.ldc + p.N) * 2) : 0);
+  __amdgpu_buffer_rsrc_t xrs = crs;  // residual (BF16) / aux (GELU store, DGELU load)
+  int64_t ldx = p.ldc;
+  if constexpr (EPI == EPI_BF16 && RES) {
+    xrs = make_rsrc(p.resid + (int64_t)mb * p.ld_resid, rows ? (uint32_t)(((int64_t)(rows - 1) * p.ld_resid + p.N) * 2) : 0);
+    ldx = p.ld_resid;
+  } else if constexpr (EPI == EPI_GELU || EPI == EPI_DGELU) {
+    const bool has = p.aux != nullptr;
+    xrs = make_rsrc(has ? p.aux + (int64_t)mb * p.ld_aux : p.aux, has && rows ? (uint32_t)(((int64_t)(rows - 1) * p.ld_aux + p.N) * 2) : 0);
+    ldx = p.ld_aux;
+  }
+  const __amdgpu_buffer_rsrc_t brs = make_rsrc(p.bias, p.bias ? (uint32_t)p.N * 4 : 0);
+  int c0[2];
+  uint32_t vc[2], vx[2];
+  float bias[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    c0[jp] = nb + 32 * jp + ((g & 1) << 4) + ((g & 2) << 2);
+    const bool okc = c0[jp] < p.N;
+    vc[jp] = okc ? (uint32_t)((li * p.ldc + c0[jp]) * 2) : OOB;
+    vx[jp] = okc ? (uint32_t)((li * ldx + c0[jp]) * 2) : OOB;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[jp][e] = 0.f;
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+      const uint32_t vb = okc ? (uint32_t)(c0[jp] * 4) : OOB;
+      const v4f b0 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(brs, vb, 0, 0));
+      const v4f b1 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(brs, vb + 16, 0, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bias[jp][e] = b0[e]; bias[jp][4 + e] = b1[e]; }
+    }
+  }
+  const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
+  const uint32_t key = p.drop_thr ? rng_key(seed) : 0u;
+  const bool idx32 = (uint64_t)p.M * (uint64_t)p.N + 8 <= 0xFFFFFFFFull;
+  float csum[2][8];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[jp][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    // this fragment row's 16 rows, added to the VGPR offset: the SGPR offset of a buffer access is
+    // outside its range check, so rows past M would be written
+    const uint32_t so_c = (uint32_t)(i * 16 * (int)p.ldc * 2), so_x = (uint32_t)(i * 16 * (int)ldx * 2);
+    const int m = mb + 16 * i + li;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      v4u xin = {0u, 0u, 0u, 0u};
+      if constexpr ((EPI == EPI_BF16 && RES) || EPI == EPI_DGELU) xin = __builtin_amdgcn_raw_buffer_load_b128(xrs, vx[jp] + so_x, 0, 0);
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // inline asm: hipcc merged the four builtin swaps of a fragment pair into one (wrong values)
+        float a = acc[i][2 * jp][r], b = acc[i][2 * jp + 1][r];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+        v[r] = a * deq;
+        v[4 + r] = b * deq;
+      }
+      bool keep[8] = {true, true, true, true, true, true, true, true};
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias[jp][e];
+        if (p.drop_thr) {
+          const uint64_t idx = (uint64_t)m * p.N + c0[jp];
+          if (idx32) {
+            bool k0[4], k1[4];
+            rng_keep4_32(key, (uint32_t)idx, p.drop_thr, k0);
+            rng_keep4_32(key, (uint32_t)idx + 4, p.drop_thr, k1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { keep[e] = k0[e]; keep[4 + e] = k1[e]; }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) rng_keep2(seed, idx + e, p.drop_thr, keep[e], keep[e + 1]);
+          }
+        }
+      }
+      v4u out;
+      if constexpr (EPI == EPI_BF16) {
+        if (p.drop_thr) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = keep[e] ? v[e] * p.drop_scale : 0.f;
+        }
+        if constexpr (RES) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] += bf2f(xin[q] & 0xFFFF);
+            v[2 * q + 1] += bf2f(xin[q] >> 16);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+      } else if constexpr (EPI == EPI_GELU) {
+        v4u ax;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const v2f s2 = {keep[2 * q] ? p.drop_scale : 0.f, keep[2 * q + 1] ? p.drop_scale : 0.f};
+          v2f g2, d2;
+          gelu_and_grad2((v2f){v[2 * q], v[2 * q + 1]}, g2, d2);
+          g2 *= s2;
+          d2 *= s2;
+          out[q] = pack2bf(g2.x, g2.y);
+          ax[q] = pack2bf(d2.x, d2.y);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(ax, xrs, vx[jp] + so_x, 0, 0);  // no aux (inference): 0-byte resource
+      } else {  // EPI_DGELU
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] *= bf2f(xin[q] & 0xFFFF);
+          v[2 * q + 1] *= bf2f(xin[q] >> 16);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[jp][e] += v[e];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(out, crs, vc[jp] + so_c, 0, 0);
+    }
+  }
+  if constexpr (EPI == EPI_DGELU) {
+    if (p.colsum) {
+      // column sums over the wave's 128 rows (16 lanes of a row x 8 fragment rows: rows past M
+      // and columns past N hold zeros), then the two wave groups (same columns) combine in LDS
+      // and one atomic per column per workgroup
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[jp][e] = row16_sum(csum[jp][e]);
+      float* red = (float*)smem;  // [4 wave columns][64 columns]
+      __syncthreads();            // every wave is past its last LDS read of the main loop
+      if (wm == 1 && li == 0) {
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) red[wn * 64 + (c0[jp] - nb) + e] = csum[jp][e];
+      }
+      __syncthreads();
+      if (wm == 0 && li == 0) {
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp)
+          if (c0[jp] < p.N)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicAdd(p.colsum + c0[jp] + e, csum[jp][e] + red[wn * 64 + (c0[jp] - nb) + e]);
+      }
+    }
+  }
+}
+
 // LDS-staged epilogue of the ping-pong kernel (SWAP layout, bf16-output epilogues): the fp32
 // accumulators cross LDS in two 128-row halves (the 128 KiB of K-tile buffers are free by then),
 // and every thread then owns 4 consecutive columns of rows t/64 + 8k, so each wave instruction
@@ -1190,7 +1363,12 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
     else
       epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
   } else if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
-    if (!p.addend && !p.row_group && (p.N & 3) == 0) {
+    if (!p.epi_staged && direct_ok(p)) {
+      if (p.resid)
+        epilogue_direct<EPI, true>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
+      else
+        epilogue_direct<EPI, false>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
+    } else if (!p.addend && !p.row_group && (p.N & 3) == 0) {
       if (p.resid)
         epilogue_staged<EPI, 128, true>(p, acc, smem, m0, n0, wm, wn, lane);
       else
@@ -1272,7 +1450,7 @@ PVR_DEV PppTile ppp_tile(const GemmParams& p, int v, int ntiles, int ntn) {
 
 // Phase of the continuous stream: reads / MFMAs of K-tile (current buffer) and the DMA of global
 // half-tile `h_issue`, which belongs to this tile (K-tile kt_i) or to the next one.
-template <int QM, int QN, int RD_A, int RD_B, bool SWAP>
+template <int QM, int QN, int RD_A, int RD_B, bool SWAP, int VM = 8>
 PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, char* smem, const PppTile& cur,
                        const PppTile& nxt, int G_issue, int kind, int tile_first_G, int nk, const GemmParams& p, int wave, int lane,
                        int wm, int wn) {
@@ -1295,7 +1473,7 @@ PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], co
     const int kt = same ? rel : rel - nk;
     ppp_issue_kind(kind, t.ars, t.brs, smem + (G_issue & 1) * PP_BUF, p.lda, p.ldb, kt * 128, wave, lane);
   }
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
   pp_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_setprio(1);
@@ -1315,8 +1493,12 @@ PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], co
   pp_barrier();
 }
 
-template <bool SWAP, int EPI>
+template <bool SWAP, int EPI, bool DIRECT>
 __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
+  // epilogue stores per wave left in flight across the tile boundary (0: drain): the register-direct
+  // BF16 epilogue issues 16 x 16 B, GELU 32 (output + derivative); dGELU (column-sum atomics and an
+  // LDS exchange) drains
+  constexpr int INFL = !DIRECT ? 0 : EPI == EPI_BF16 ? 16 : EPI == EPI_GELU ? 32 : 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1347,7 +1529,21 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
       for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
     v8s af[4][2], bf[2][2][2];
     if (wm == 1) pp_barrier();  // group 1 runs one barrier behind
-    for (int kt = 0; kt < nk; ++kt) {
+    int kt = 0;
+    if constexpr (INFL > 0) {
+      if (G0 > 0) {
+        // first K-tile after a register-direct epilogue: its INFL stores per wave are younger than
+        // the four half-tiles this K-tile waits for, so every wait leaves them in flight (counted);
+        // the first wait for a half-tile issued after them (next K-tile) retires them
+        const char* buf = smem + (G0 & 1) * PP_BUF;
+        ppp_phase<0, 0, 1, 1, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 2, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<0, 1, 0, 1, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 3, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<1, 1, 1, 0, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 0, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<1, 0, 0, 0, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 1, G0, nk, p, wave, lane, wm, wn);
+        kt = 1;
+      }
+    }
+    for (; kt < nk; ++kt) {
       const int G = G0 + kt;
       const char* buf = smem + (G & 1) * PP_BUF;
       ppp_phase<0, 0, 1, 1, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 1, 2, G0, nk, p, wave, lane, wm, wn);
@@ -1356,19 +1552,29 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
       ppp_phase<1, 0, 0, 0, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
     }
     if (wm == 0) pp_barrier();  // re-align the groups for the epilogue
-    // The next tile's first DMAs are in flight into the K-tile buffers; the epilogue stages in the
+    // The next tile's first DMAs are in flight into the K-tile buffers; the epilogue works from
+    // registers (DIRECT; the DGELU column-sum exchange uses the separate region) or stages in the
     // separate region behind them.
-    if (p.resid)
-      epilogue_staged<EPI, 32, true>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
-    else
-      epilogue_staged<EPI, 32, false>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+    if constexpr (DIRECT) {
+      if (p.resid)
+        epilogue_direct<EPI, true>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
+      else
+        epilogue_direct<EPI, false>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
+    } else {
+      if (p.resid)
+        epilogue_staged<EPI, 32, true>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+      else
+        epilogue_staged<EPI, 32, false>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+    }
     v += gridDim.x;
     if (v >= ntiles) break;
     G0 += nk;
     cur = nxt;
     nxt = ppp_tile(p, v + gridDim.x, ntiles, ntn);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step 1: drain (stores + the K-tiles already issued)
-    __syncthreads();
+    if constexpr (INFL == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain (stores + the K-tiles already issued)
+      __syncthreads();
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
@@ -1376,13 +1582,17 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
 template <bool SWAP, int EPI>
 hipError_t launch_ppp(const GemmParams& p, hipStream_t s) {
   constexpr int SMEM = 2 * PP_BUF + 32 * 1024;
-  auto kern = gemm_ppp_kernel<SWAP, EPI>;
+  auto kd = gemm_ppp_kernel<SWAP, EPI, true>;
+  auto ks = gemm_ppp_kernel<SWAP, EPI, false>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    hipError_t e = hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  const bool direct = !p.epi_staged && direct_ok(p);
+  auto kern = direct ? kd : ks;
   const int ntiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   int cus = 256;
   {

@@ -27,6 +27,7 @@ struct GemmParams {
   int elem8, fmt_a, fmt_b;
   // EPI_F32_STORE with split-K (tile 14): split z writes its partial to C + z * split_stride
   int64_t split_stride;
+  int epi_staged;  // A/B: ping-pong bf16 epilogues through LDS (1) instead of register-direct (0)
 };
 
 }  // namespace pvr

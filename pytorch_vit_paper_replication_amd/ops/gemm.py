@@ -19,18 +19,29 @@ EPI_BF16, EPI_GELU, EPI_DGELU, EPI_F32_ATOMIC, EPI_F32_STORE = range(5)
 
 # tile configs: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves), 2 = 128x256 (8 waves)
 _FORCE_TILE = os.environ.get("PVR_GEMM_TILE")
-_PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "0") == "1"  # A/B: 12 faster once its epilogue loads were fixed
-_GELU_TILE = int(os.environ.get("PVR_GELU_TILE", "13"))  # tile config of the fc1 GELU forward (A/B)
+_PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "0") == "1"  # persistent ping-pong for every fwd / dgrad GEMM
+
+
+def _n_cus() -> int:
+    global _N_CUS
+    if _N_CUS is None:
+        _N_CUS = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count if torch.cuda.is_available() else 256
+    return _N_CUS
+
+
+_N_CUS = None
+# A/B: bf16 epilogues of the ping-pong GEMM staged through LDS (1) instead of register-direct (0)
+_EPI_STAGED = int(os.environ.get("PVR_EPI_STAGED", "0"))
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
 
 def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
     """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
-    k-contiguous forward/dgrad at ViT sizes -> persistent 256x256 8-wave ping-pong (13; K % 64 == 0,
-    else the 4-stage BK=32 ring 6); token-reduced wgrad (both operands mn-contiguous, split-K
-    atomics) -> the same ping-pong with transposed LDS reads when the token count is large,
-    128x128 (0) otherwise."""
+    k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave ping-pong, persistent (13) when there
+    are at least two output tiles per CU, one tile per workgroup (12) otherwise (K % 64 != 0: the
+    4-stage BK=32 ring, 6); token-reduced wgrad (both operands mn-contiguous, split-K) -> the same
+    ping-pong with transposed LDS reads when the token count is large, 128x128 (0) otherwise."""
     if _FORCE_TILE is not None:
         return int(_FORCE_TILE)
     if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
@@ -40,9 +51,13 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
         # It pays for the VALU-heavy GELU epilogue (fc1 fwd 0.377 vs 0.457 ms at ViT-B/16 b256,
         # profiles/kbench_epilogues.log); epilogues that load per-row inputs (residual, dGELU
         # factor) drain the in-flight DMAs there and stay on the one-tile-per-workgroup form (12).
-        if gelu:
-            return _GELU_TILE if K >= 128 else 12
-        return 13 if K >= 128 and _PERSISTENT else 12
+        # persistent ping-pong (13) once there are at least two tiles per CU: the next tile's
+        # K-tiles stream in under the register-direct epilogue, whose stores stay in flight under
+        # the next tile's first K-tile (qkv fwd 0.171-0.179 vs 0.183-0.185 ms, fc1 GELU fwd 0.347-0.352
+        # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log)
+        if K >= 128 and (_PERSISTENT or math.ceil(M / 256) * math.ceil(N / 256) >= 2 * _n_cus()):
+            return 13
+        return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
         return 12
     return 0
@@ -65,6 +80,10 @@ def _small_splitk(T: int, N: int, K: int) -> int:
         return 0
     s = min(K // 128, max(2, 256 // tiles))
     return s if s >= 2 else 0
+
+
+def _gemm(*args, tile: int, colsum=None):
+    _ext.ext().gemm(*args, tile, colsum=colsum, epi_staged=_EPI_STAGED)
 
 
 def _drop_args(drop: Drop):
@@ -100,8 +119,8 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
         ext.gemm(x, True, w, True, ws, T, N, K, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0, None, 0, 0.0, ksplit, 14)
         ext.splitk_epilogue(ws, nsplit, out, bias, resid, epi == EPI_GELU)
         return out
-    _ext.ext().gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
-                    row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, _tile(T, N, K, "fwd", epi == EPI_GELU))
+    _gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
+          row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, tile=_tile(T, N, K, "fwd", epi == EPI_GELU))
     return out
 
 
@@ -120,8 +139,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
     if colsum is not None and dgelu_aux is None:
         raise ValueError("colsum is fused only into the GELU-backward epilogue")
     if wt is not None and N % 64 == 0:
-        _ext.ext().gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-                        seed, soff, p, 0, _tile(T, K, N, "dgrad_t"), colsum=colsum)
+        _gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
+              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t"), colsum=colsum)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
                         seed, soff, p, 0, _tile(T, K, N, "dgrad") if tile is None else tile, colsum=colsum)

@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--tiles", default="0,1,2")
     ap.add_argument("--only", default="gemm,attn,ln")
     ap.add_argument("--attn-shape", default="197,12,64", help="N,H,dh of the attention cases (batch: --batch)")
+    ap.add_argument("--epi-tiles", default="12,13,15", help="tile configs of the per-epilogue cases (--only epi)")
+    ap.add_argument("--gelu-tiles", default="9,10,11,6,13,15", help="tile configs of the fc1 GELU case (--only epi)")
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the epilogue cases (interleaved A/B)")
     a = ap.parse_args()
     dev = "cuda"
     T = a.batch * 197
@@ -102,19 +105,25 @@ def main():
         wqkv = (torch.randn(M3, D, device=dev) * 0.02).to(torch.bfloat16)
         bqkv = torch.randn(M3, device=dev)
         w1t = w1.t().contiguous()
-        for t in (12, 13):  # one tile per workgroup vs persistent, per epilogue kind
+        wot = wo.t().contiguous()
+        dq3, wqkvt = torch.randn(T, M3, device=dev, dtype=torch.bfloat16), wqkv.t().contiguous()
+        for _round in range(a.rounds):
+          for t in [int(v) for v in a.epi_tiles.split(",")]:  # one tile per workgroup / persistent / stream-K
             G._FORCE_TILE = str(t)
             for name, fl, fn in [
                 ("qkv fwd  bias            ", 2.0 * T * M3 * D, lambda: G.linear_fwd(x, wqkv, bqkv)),
                 ("out fwd  bias+resid      ", 2.0 * T * D * D, lambda: G.linear_fwd(x, wo, b2, resid=r)),
+                ("fc1 fwd  GELU+drop+aux   ", 2.0 * T * M * D, lambda: G.linear_fwd(x, w1, b1, gelu_aux=u, drop=(seed, 3 << 32, 0.1))),
                 ("fc2 fwd  bias+drop+resid ", 2.0 * T * M * D, lambda: G.linear_fwd(h, w2, b2, resid=r, drop=(seed, 4 << 32, 0.1))),
+                ("out dgrad plain (wT)     ", 2.0 * T * D * D, lambda: G.linear_dgrad(r, wo, wt=wot)),
+                ("qkv dgrad plain (wT)     ", 2.0 * T * M3 * D, lambda: G.linear_dgrad(dq3, wqkv, wt=wqkvt)),
                 ("fc1 dgrad plain (wT)     ", 2.0 * T * M * D, lambda: G.linear_dgrad(u, w1, wt=w1t)),
                 ("fc2 dgrad dGELU+colsum   ", 2.0 * T * M * D, lambda: G.linear_dgrad(r, w2, dgelu_aux=u, wt=w2t, colsum=cs)),
             ]:
                 tt = timeit(fn)
                 print(f"epi   {name} tile{t} {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF", flush=True)
             G._FORCE_TILE = None
-        for t in (9, 10, 11, 6, 13):  # other tile structures for the GELU epilogue (2 workgroups/CU, persistent)
+        for t in [int(v) for v in a.gelu_tiles.split(",") if v]:  # other structures for the GELU epilogue
             G._FORCE_TILE = str(t)
             tt = timeit(lambda: G.linear_fwd(x, w1, b1, gelu_aux=u, drop=(seed, 3 << 32, 0.1)))
             G._FORCE_TILE = None
