@@ -37,6 +37,8 @@ int pvr_norm_partial_blocks();
 hipError_t pvr_grad_norm(const float*, int64_t, float, float*, float*, hipStream_t);
 hipError_t pvr_adam(float*, const float*, float*, float*, uint16_t*, int64_t, const int64_t*, const int*, int, const pvr::AdamGroup*, const float*, int, hipStream_t);
 hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
+hipError_t pvr_adam_t(float*, const float*, float*, float*, uint16_t*, uint16_t*, const int64_t*, int, int, const int64_t*, int, int64_t,
+                      const pvr::AdamGroup*, const float*, int, hipStream_t);
 hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, int, const float*, unsigned*, int, hipStream_t);
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
@@ -350,6 +352,29 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c1
         "adam");
 }
 
+// Adam + bf16 shadow + transposed bf16 shadow (W^T of the registered 2-D weights) in one launch.
+// tmeta int64 [nmat][6] {flat offset, shadow_t offset, R, C, first tile, group} (R, C % 64 == 0),
+// fmeta int64 [nflat][4] {flat start, elements % 4 == 0, group, first float4} for everything else.
+void adam_t(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor shadow, torch::Tensor shadow_t,
+            torch::Tensor tmeta, int64_t ntiles, torch::Tensor fmeta, int64_t flat4, torch::Tensor groups,
+            c10::optional<torch::Tensor> clip, bool skip_nonfinite) {
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel() && shadow.numel() == p.numel(),
+              "adam_t: size mismatch");
+  TORCH_CHECK(groups.scalar_type() == torch::kFloat32 && groups.size(-1) == 8, "adam_t: groups must be float32 [G, 8]");
+  TORCH_CHECK(tmeta.is_cuda() && tmeta.scalar_type() == torch::kInt64 && tmeta.dim() == 2 && tmeta.size(1) == 6 && tmeta.is_contiguous(),
+              "adam_t: tmeta int64 [n][6]");
+  TORCH_CHECK(fmeta.is_cuda() && fmeta.scalar_type() == torch::kInt64 && fmeta.dim() == 2 && fmeta.size(1) == 4 && fmeta.is_contiguous(),
+              "adam_t: fmeta int64 [n][4]");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous() && shadow.is_contiguous() &&
+                  shadow_t.is_contiguous(),
+              "adam_t: contiguous buffers");
+  check(pvr_adam_t(f32_mut(p, "p"), f32(g, "g"), f32_mut(m, "m"), f32_mut(v, "v"), bf_mut(shadow, "shadow"), bf_mut(shadow_t, "shadow_t"),
+                   tmeta.data_ptr<int64_t>(), (int)tmeta.size(0), (int)ntiles, fmeta.data_ptr<int64_t>(), (int)fmeta.size(0), flat4,
+                   reinterpret_cast<const pvr::AdamGroup*>(groups.data_ptr<float>()), opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0,
+                   stream()),
+        "adam_t");
+}
+
 void scale_by_clip(torch::Tensor g, torch::Tensor clip) {
   check(pvr_scale_by_clip(f32_mut(g, "g"), g.numel(), f32(clip, "clip"), stream()), "scale_by_clip");
 }
@@ -516,7 +541,9 @@ void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor d
 // per-call zero fill (a 151 MB memset per layer at ViT-L/16 384 px). Deliberately never freed (a
 // static tensor's destructor would run after the HIP runtime's teardown). PVR_ATTN_DQ_WS=0: a fresh
 // zeroed tensor per call instead (A/B).
-torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts) {
+// drop = true: forget the cached accumulator of this (device, stream) (after a failed backward, whose
+// partial sums it may still hold); the next call re-creates it with torch::zeros.
+torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts, bool drop = false) {
   static const bool on = [] {
     const char* e = getenv("PVR_ATTN_DQ_WS");
     return !(e && e[0] == '0');
@@ -525,6 +552,11 @@ torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts) {
   static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
   const auto key = std::make_pair((int)opts.device().index(), stream());
   torch::Tensor*& t = cache[key];
+  if (drop) {
+    delete t;
+    t = nullptr;
+    return torch::Tensor();
+  }
   if (!t || t->numel() < numel) {
     delete t;  // stream-ordered reuse of its memory by the caching allocator
     t = new torch::Tensor(torch::zeros({numel}, opts.dtype(torch::kFloat32)));
@@ -574,12 +606,15 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
     else if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
       dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
-  check(pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"), ld_of(dout, "dout"),
-                     f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"), ld_of(dqkv, "dqkv"),
-                     dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
-                     dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
-                     (float)scale, stream()),
-        "attn_bwd");
+  const hipError_t err = pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"),
+                                      ld_of(dout, "dout"), f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"),
+                                      ld_of(dqkv, "dqkv"), dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
+                                      dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
+                                      (float)scale, stream());
+  // a persistent accumulator is re-zeroed only by a completed backward: after a failed launch it
+  // may hold stale partial sums, so it is dropped (re-created zeroed by the next call)
+  if (err != hipSuccess && dq_rezero) dq_workspace(0, qkv.options(), true);
+  check(err, "attn_bwd");
   if (want_db) {
     if (pipe)
       attn_dbias_reduce(dbias_part, B, H, *dbias);
@@ -633,6 +668,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_norm", &grad_norm);
   m.def("norm_partial_blocks", []() { return pvr_norm_partial_blocks(); });
   m.def("adam", &adam);
+  m.def("adam_t", &adam_t);
   m.def("scale_by_clip", &scale_by_clip);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A"), py::arg("fmt_a"), py::arg("B"), py::arg("fmt_b"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("scale_a"), py::arg("scale_b"), py::arg("bias") = py::none(),

@@ -268,6 +268,9 @@ PVR_DEV float wave_sum(float v) {
 PVR_DEV float wave_max(float v) {
   return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
+// NaN-propagating max (fmaxf returns the non-NaN operand): a NaN on either side wins
+PVR_DEV float nan_max(float a, float b) { return (a > b || a != a) ? a : b; }
+PVR_DEV float wave_max_nan(float v) { return wave_reduce(v, nan_max); }
 
 // Bijective XCD-aware remap: blocks dealt round-robin over 8 XCDs (b, b+8 share one) are given
 // contiguous logical tile ranges so neighbouring tiles share the XCD's L2.

@@ -85,11 +85,11 @@ __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__
   // one same-address atomic per BLOCK: those serialise at L2 (~12 ns each), so the grid is capped
   // at 256 blocks and the 4 waves reduce through LDS first
   __shared__ float wm[4];
-  m = wave_max(m);
+  m = wave_max_nan(m);
   if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float b = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    const float b = nan_max(nan_max(wm[0], wm[1]), nan_max(wm[2], wm[3]));
     // |x| bits order like uints; Inf (0x7f800000) and NaN (> 0x7f800000) sort above every finite
     if (!(b <= 0.f)) atomicMax(amax, __float_as_uint(b));
   }
@@ -147,11 +147,11 @@ __global__ void __launch_bounds__(256) quant_multi_kernel(const int64_t* __restr
     }
     if constexpr (AMAX) {
       __shared__ float wm[4];
-      m = wave_max(m);
+      m = wave_max_nan(m);
       if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
       __syncthreads();
       if (threadIdx.x == 0) {
-        const float b = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+        const float b = nan_max(nan_max(wm[0], wm[1]), nan_max(wm[2], wm[3]));
         if (!(b <= 0.f)) atomicMax(amax + slot, __float_as_uint(b));
       }
       __syncthreads();

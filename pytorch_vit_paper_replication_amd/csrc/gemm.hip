@@ -950,11 +950,11 @@ __host__ __device__ inline bool direct_ok(const GemmParams& p) {
   return !p.addend && !p.row_group && (p.N & 7) == 0 && (int64_t)p.M * ld * 2 < (1ll << 31);
 }
 
-template <int EPI, bool RES>
+template <int EPI, bool RES, bool SCALED = false>
 PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, int mb, int nb, int wm, int wn, int lane) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const int li = lane & 15, g = lane >> 4;
-  const float deq = p.scale_a ? (*p.scale_a) * (*p.scale_b) : 1.f;
+  const float deq = SCALED ? (*p.scale_a) * (*p.scale_b) : 1.f;  // fp8 operands: per-tensor dequant
   // rows [mb, min(M, mb + 128)) of C (and of the residual / aux tensors) from the wave's first row
   const int rows = max(0, min(128, p.M - mb));
   const uint32_t OOB = 0x80000000u;
@@ -997,24 +997,35 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   for (int jp = 0; jp < 2; ++jp)
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[jp][e] = 0.f;
+  // every row input (residual / dGELU factor) of the wave's 128 rows is requested up front (64
+  // VGPRs, free now that the main loop's fragments are dead): the loads' latency overlaps instead
+  // of being paid per fragment row. Row offsets go into the VGPR offset: the SGPR offset of a
+  // buffer access is outside its range check, so rows past M would be accessed.
+  constexpr bool HAS_IN = (EPI == EPI_BF16 && RES) || EPI == EPI_DGELU;
+  v4u xin_all[HAS_IN ? 8 : 1][2];
+  if constexpr (HAS_IN) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp)
+        xin_all[i][jp] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vx[jp] + (uint32_t)(i * 16 * (int)ldx * 2), 0, 0);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    // this fragment row's 16 rows, added to the VGPR offset: the SGPR offset of a buffer access is
-    // outside its range check, so rows past M would be written
     const uint32_t so_c = (uint32_t)(i * 16 * (int)p.ldc * 2), so_x = (uint32_t)(i * 16 * (int)ldx * 2);
     const int m = mb + 16 * i + li;
 #pragma unroll
     for (int jp = 0; jp < 2; ++jp) {
       v4u xin = {0u, 0u, 0u, 0u};
-      if constexpr ((EPI == EPI_BF16 && RES) || EPI == EPI_DGELU) xin = __builtin_amdgcn_raw_buffer_load_b128(xrs, vx[jp] + so_x, 0, 0);
+      if constexpr (HAS_IN) xin = xin_all[i][jp];
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         // inline asm: hipcc merged the four builtin swaps of a fragment pair into one (wrong values)
         float a = acc[i][2 * jp][r], b = acc[i][2 * jp + 1][r];
         asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-        v[r] = a * deq;
-        v[4 + r] = b * deq;
+        v[r] = SCALED ? a * deq : a;
+        v[4 + r] = SCALED ? b * deq : b;
       }
       bool keep[8] = {true, true, true, true, true, true, true, true};
       if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU) {
@@ -1077,29 +1088,36 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
     }
   }
   if constexpr (EPI == EPI_DGELU) {
-    if (p.colsum) {
+    {  // without colsum the atomics go to a 0-byte resource: the store count stays fixed
       // column sums over the wave's 128 rows (16 lanes of a row x 8 fragment rows: rows past M
-      // and columns past N hold zeros), then the two wave groups (same columns) combine in LDS
-      // and one atomic per column per workgroup
+      // and columns past N hold zeros). The two wave groups hold the same 64 columns: group g
+      // hands its other column half (jp = 1 - g) to its partner through LDS and adds the
+      // partner's half jp = g, then 8 buffer atomics per wave (lanes li = 0; columns past N are
+      // out of range). Every wave issues exactly 8: the persistent kernel counts them.
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp)
 #pragma unroll
         for (int e = 0; e < 8; ++e) csum[jp][e] = row16_sum(csum[jp][e]);
-      float* red = (float*)smem;  // [4 wave columns][64 columns]
-      __syncthreads();            // every wave is past its last LDS read of the main loop
-      if (wm == 1 && li == 0) {
+      float* red = (float*)smem;  // [2 column halves][4 wave columns][32 columns]
+      if (li == 0) {
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) red[wn * 64 + (c0[jp] - nb) + e] = csum[jp][e];
+        for (int e = 0; e < 8; ++e) {
+          const float give = wm == 0 ? csum[1][e] : csum[0][e];
+          red[(1 - wm) * 128 + wn * 32 + (c0[1 - wm] - nb - 32 * (1 - wm)) + e] = give;
+        }
       }
-      __syncthreads();
-      if (wm == 0 && li == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // raw barrier: no vmcnt drain of the in-flight stores
+      asm volatile("" ::: "memory");
+      const __amdgpu_buffer_rsrc_t srs = make_rsrc(p.colsum, p.colsum ? (uint32_t)p.N * 4 : 0);
+      if (li == 0) {
+        const int jp = wm;
+        const uint32_t vo = c0[jp] < p.N ? (uint32_t)c0[jp] * 4 : OOB;
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp)
-          if (c0[jp] < p.N)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) atomicAdd(p.colsum + c0[jp] + e, csum[jp][e] + red[wn * 64 + (c0[jp] - nb) + e]);
+        for (int e = 0; e < 8; ++e) {
+          const float mine = wm == 0 ? csum[0][e] : csum[1][e];
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(mine + red[jp * 128 + wn * 32 + (c0[jp] - nb - 32 * jp) + e], srs, vo + 4 * e, 0, 0);
+        }
       }
     }
   }
@@ -1365,9 +1383,9 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   } else if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
     if (!p.epi_staged && direct_ok(p)) {
       if (p.resid)
-        epilogue_direct<EPI, true>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
+        epilogue_direct<EPI, true, ES == 1>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
       else
-        epilogue_direct<EPI, false>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
+        epilogue_direct<EPI, false, ES == 1>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
     } else if (!p.addend && !p.row_group && (p.N & 3) == 0) {
       if (p.resid)
         epilogue_staged<EPI, 128, true>(p, acc, smem, m0, n0, wm, wn, lane);
@@ -1496,9 +1514,9 @@ PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], co
 template <bool SWAP, int EPI, bool DIRECT>
 __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   // epilogue stores per wave left in flight across the tile boundary (0: drain): the register-direct
-  // BF16 epilogue issues 16 x 16 B, GELU 32 (output + derivative); dGELU (column-sum atomics and an
-  // LDS exchange) drains
-  constexpr int INFL = !DIRECT ? 0 : EPI == EPI_BF16 ? 16 : EPI == EPI_GELU ? 32 : 0;
+  // BF16 epilogue issues 16 x 16 B, GELU 32 (output + derivative), dGELU 16 + 8 column-sum atomics
+  // (to a 0-byte resource without colsum)
+  constexpr int INFL = !DIRECT ? 0 : EPI == EPI_BF16 ? 16 : EPI == EPI_GELU ? 32 : 24;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -18,8 +18,9 @@ delayed-scaling slots) x e4m3 transposed weights (``linear_dgrad_fp8``); with ``
 the default) the four weight-gradient GEMMs too: e5m2 gradients^T x e4m3 activations^T from
 transposing quantize passes (``linear_wgrad_fp8``, split-K over tokens). LayerNorm, softmax,
 attention, residual adds and the optimizer stay in bf16 / fp32.
-Non-finite values: a NaN/Inf element makes its tensor's amax non-finite; the scale update then
-leaves that slot's history and scales unchanged (csrc/fp8.hip), and FusedAdam skips the step.
+Non-finite values: an Inf element makes its tensor's amax non-finite and a NaN element propagates
+through the NaN-aware amax reduction (csrc/fp8.hip); the scale update then leaves that slot's
+history and scales unchanged, and FusedAdam's non-finite check skips the step.
 """
 from __future__ import annotations
 
@@ -87,6 +88,7 @@ class Fp8State:
         self._wsrc: Dict[int, torch.Tensor] = {}   # key -> the bf16 shadow view it is quantized from
         self._batch: Optional[Tuple[torch.Tensor, int, int]] = None  # (segment table, chunks, keys)
         self._batch_gen: Optional[int] = None
+        self._layout = None
         self.device = device
 
     def begin_step(self, training: bool) -> None:
@@ -111,13 +113,23 @@ class Fp8State:
         n = self.ACT_PER_BLOCK
         return linear_wgrad_fp8(dy, self.grad, block * n + which_grad, x, self.act, block * n + which_act, out)
 
-    def weight(self, w16: torch.Tensor, key: int, generation: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    def weight(self, w16: torch.Tensor, key: int, generation: int, layout=None) -> Tuple[torch.Tensor, torch.Tensor]:
         """fp8 (e4m3, current scaling) copy of a bf16 weight shadow, cached per store generation.
 
         The first generation quantizes each weight on first use (two launches each) and records it;
         from then on a new generation re-quantizes EVERY recorded weight at once: one multi-tensor
         amax launch, one scale update, one multi-tensor quantize launch (instead of two launches per
-        weight and direction, 512 per ViT-H/14 step)."""
+        weight and direction, 512 per ViT-H/14 step).
+
+        ``layout`` identifies the buffers every recorded source view lives in (the store's bf16 and
+        transposed shadows): when it changes, the recorded views and the batched segment table are
+        dropped, so no weight is ever re-quantized from a reallocated (stale) buffer."""
+        if layout is not None and layout != self._layout:
+            self._layout = layout
+            self._wsrc.clear()
+            self._wcache.clear()
+            self._batch = None
+            self._batch_gen = None
         hit = self._wcache.get(key)
         if hit is not None and hit[0] == generation:
             return hit[1], hit[2]
@@ -154,8 +166,8 @@ class Fp8State:
             for k in keys:
                 w16, q = self._wsrc[k], self._wcache[k][1]
                 n = w16.numel()
-                if n % 16 or not (w16.is_contiguous() and q.is_contiguous()):
-                    return  # not batchable: the per-weight path handles this generation
+                if n % 16 or w16.data_ptr() % 16 or q.data_ptr() % 16 or not (w16.is_contiguous() and q.is_contiguous()):
+                    return  # not batchable (16-B vector accesses): the per-weight path handles this generation
                 rows.append([w16.data_ptr(), q.data_ptr(), n, self._wslot[k], chunk0])
                 chunk0 += (n + per - 1) // per
             self._batch = (torch.tensor(rows, dtype=torch.int64, device=self.device), chunk0, len(keys))

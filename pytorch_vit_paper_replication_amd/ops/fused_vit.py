@@ -195,7 +195,8 @@ class EncoderBlockFn(torch.autograd.Function):
 
             st, blk = f8
             gen = store.generation
-            wq = [st.weight(store.bf16(w), id(w), gen) for w in (wqkv, wo, w1, w2)]
+            lay = store.layout_key()
+            wq = [st.weight(store.bf16(w), id(w), gen, lay) for w in (wqkv, wo, w1, w2)]
             a, s_ = st.act_quant(xn1, blk, 0)
             qkv = F8.linear_fwd_fp8(a, s_, *wq[0], bqkv)
             o, lse = ext.attn_fwd(qkv, B, N, H, scale)
@@ -268,7 +269,7 @@ class EncoderBlockFn(torch.autograd.Function):
 
                 st, blk = f8d
                 gq, gs = st.grad_quant(dy, blk, which)
-                wq, ws = st.weight(wt, ~id(w), store.generation)
+                wq, ws = st.weight(wt, ~id(w), store.generation, store.layout_key())
                 out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum)
             else:
                 out = gemm.linear_dgrad(dy, store.bf16(w), dgelu_aux=dgelu_aux, wt=wt, colsum=colsum)

@@ -36,10 +36,10 @@ _EPI_STAGED = int(os.environ.get("PVR_EPI_STAGED", "0"))
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
 
-def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
+def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = False) -> int:
     """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
     k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave ping-pong, persistent (13) when there
-    are at least two output tiles per CU, one tile per workgroup (12) otherwise (K % 64 != 0: the
+    are at least four output tiles per CU, one tile per workgroup (12) otherwise (K % 64 != 0: the
     4-stage BK=32 ring, 6); token-reduced wgrad (both operands mn-contiguous, split-K) -> the same
     ping-pong with transposed LDS reads when the token count is large, 128x128 (0) otherwise."""
     if _FORCE_TILE is not None:
@@ -51,11 +51,12 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False) -> int:
         # It pays for the VALU-heavy GELU epilogue (fc1 fwd 0.377 vs 0.457 ms at ViT-B/16 b256,
         # profiles/kbench_epilogues.log); epilogues that load per-row inputs (residual, dGELU
         # factor) drain the in-flight DMAs there and stay on the one-tile-per-workgroup form (12).
-        # persistent ping-pong (13) once there are at least two tiles per CU: the next tile's
+        # persistent ping-pong (13) once there are at least four tiles per CU: the next tile's
         # K-tiles stream in under the register-direct epilogue, whose stores stay in flight under
         # the next tile's first K-tile (qkv fwd 0.171-0.179 vs 0.183-0.185 ms, fc1 GELU fwd 0.347-0.352
-        # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log)
-        if K >= 128 and (_PERSISTENT or math.ceil(M / 256) * math.ceil(N / 256) >= 2 * _n_cus()):
+        # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log). The dGELU
+        # dgrad (column-sum exchange at every tile end) stays on 12: 0.300 vs 0.325 ms (profiles/r3/gemm_ab.log)
+        if K >= 128 and not dgelu and (_PERSISTENT or math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus()):
             return 13
         return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
@@ -140,7 +141,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
         raise ValueError("colsum is fused only into the GELU-backward epilogue")
     if wt is not None and N % 64 == 0:
         _gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t"), colsum=colsum)
+              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t", dgelu=dgelu_aux is not None), colsum=colsum)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
                         seed, soff, p, 0, _tile(T, K, N, "dgrad") if tile is None else tile, colsum=colsum)

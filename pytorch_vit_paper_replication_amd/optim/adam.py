@@ -5,7 +5,8 @@ weight decay, betas (0.9, 0.999), eps 1e-8) and for AdamW (``decoupled_weight_de
 
 On the fused GPU path all parameters live in one ``ParamStore``; a step is
   [optional] global-norm clip:  two deterministic reduction kernels -> {norm, coef, nonfinite} on device
-  Adam:                          one kernel: g*coef (+wd*p) -> m, v -> p -> bf16 shadow
+  Adam:                          one kernel: g*coef (+wd*p) -> m, v -> p -> bf16 shadow (and the
+                                 transposed bf16 shadow W^T of the 2-D encoder weights)
 so clip_grad_norm_ + optimizer.step() (SURVEY.md K14+K15, ~1000 small launches) become 3 launches
 with no host synchronisation. Elsewhere (CPU, or parameters outside a store) it falls back to the
 exact torch.optim.Adam single-tensor math.
@@ -19,6 +20,9 @@ import numpy as np
 import torch
 
 from .. import _ext
+
+# Adam writes the transposed bf16 weight shadow itself (PVR_FUSED_WT=0: separate transpose pass, A/B)
+_FUSED_WT = __import__("os").environ.get("PVR_FUSED_WT", "1") == "1"
 
 
 def _store_of(params):
@@ -103,7 +107,41 @@ class FusedAdam(torch.optim.Optimizer):
         ws = torch.empty(_ext.ext().norm_partial_blocks(), dtype=torch.float32, device=dev)
         clip = torch.zeros(3, dtype=torch.float32, device=dev)
         self._fused = (store, m, v, seg_start, seg_group, ws, clip)
+        self._tmeta_key = None
         return self._fused
+
+    def _transposed_tables(self, store):
+        """Tables of the fused Adam + W^T pass (csrc/optim.hip adam_t_kernel), rebuilt when the
+        store's transposed layout changes; None if the store keeps no (64-aligned) W^T shadow."""
+        lay = store.transposed_layout()
+        if lay is None:
+            return None
+        tparams, tmeta_dev = lay
+        key = (id(tmeta_dev), store.shadow_t.data_ptr())
+        if self._tmeta_key == key:
+            return self._ttables
+        group_of = {}
+        for gi, g in enumerate(self.param_groups):
+            for p in g["params"]:
+                group_of[id(p)] = gi
+        meta = tmeta_dev.cpu().tolist()
+        trows, tiles = [], 0
+        for p, (soff, toff, R, C, _) in zip(tparams, meta):
+            trows.append([soff, toff, R, C, tiles, group_of.get(id(p), -1) if p.requires_grad else -1])
+            tiles += (R // 64) * (C // 64)
+        tids = {id(p) for p in tparams}
+        frows, f4 = [], 0
+        for p, off in zip(store.params, store.offsets):
+            if id(p) in tids:
+                continue
+            n = (p.numel() + 3) // 4 * 4  # the store pads every segment (zeros stay zero)
+            frows.append([off, n, group_of.get(id(p), -1) if p.requires_grad else -1, f4])
+            f4 += n // 4
+        dev = store.device
+        self._ttables = (torch.tensor(trows, dtype=torch.int64, device=dev), tiles,
+                         torch.tensor(frows, dtype=torch.int64, device=dev), f4)
+        self._tmeta_key = key
+        return self._ttables
 
     def _group_array(self, step: int, arr: Optional[np.ndarray] = None) -> np.ndarray:
         G = len(self.param_groups)
@@ -211,9 +249,17 @@ class FusedAdam(torch.optim.Optimizer):
                 _ext.ext().grad_norm(store.grad_flat, 0.0, ws, clip)  # max_norm 0 -> coef 1, flag only
                 use_clip = True
             table = self._group_table(step, store.device)
-            _ext.ext().adam(store.flat, store.grad_flat, m, v, store.shadow, seg_start, seg_group, table,
-                            clip if use_clip else None, self.skip_nonfinite)
-            store.mark_shadow_fresh()
+            tt = self._transposed_tables(store) if _FUSED_WT else None
+            if tt is not None and tt[3] > 0:
+                # master, m, v, bf16 shadow and the dgrad GEMMs' W^T shadow in one pass
+                store.ensure_transposed()  # only if something else changed the weights since
+                _ext.ext().adam_t(store.flat, store.grad_flat, m, v, store.shadow, store.shadow_t, tt[0], tt[1], tt[2], tt[3],
+                                  table, clip if use_clip else None, self.skip_nonfinite)
+                store.mark_shadow_fresh(transposed=True)
+            else:
+                _ext.ext().adam(store.flat, store.grad_flat, m, v, store.shadow, seg_start, seg_group, table,
+                                clip if use_clip else None, self.skip_nonfinite)
+                store.mark_shadow_fresh()
             self._pending_clip = False
             return loss
         # ---------------- reference math (torch.optim.Adam, single-tensor, maximize=False)

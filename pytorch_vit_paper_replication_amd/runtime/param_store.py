@@ -124,11 +124,23 @@ class ParamStore:
             self._t_dirty = True
             self.generation += 1
 
-    def mark_shadow_fresh(self) -> None:
-        """Called by the fused optimizer after it rewrote master + shadow in one pass."""
+    def mark_shadow_fresh(self, transposed: bool = False) -> None:
+        """Called by the fused optimizer after it rewrote master + shadow in one pass (and, with
+        ``transposed``, the W^T shadow of every registered weight too)."""
         self._shadow_key = self._version_key()
-        self._t_dirty = True
+        if not transposed:
+            self._t_dirty = True
         self.generation += 1
+
+    def transposed_layout(self):
+        """(registered weights, [flat offset, shadow_t offset, R, C, first 64x64 tile] rows) of the
+        W^T shadow, or None when a weight's shape is not a multiple of 64 (then only the separate
+        transpose pass handles it). Clean (not dirty) W^T is required by the optimizer's fused write."""
+        if not self._t_params or self._t_meta is None:
+            return None
+        if any(p.shape[0] % 64 or p.shape[1] % 64 for p in self._t_params):
+            return None
+        return self._t_params, self._t_meta
 
     # ------------------------------------------------------------------ transposed bf16 weights
     def register_transposed(self, params: Iterable[torch.nn.Parameter]) -> None:
@@ -162,6 +174,10 @@ class ParamStore:
                 for p in self._t_params:
                     self._t_views[id(p)].copy_(self.bf16(p).t())
         self._t_dirty = False
+
+    def layout_key(self):
+        """Identity of the bf16 shadow buffers (changes when register_transposed reallocates)."""
+        return (self.shadow.data_ptr(), self.shadow_t.data_ptr() if self.shadow_t is not None else 0)
 
     def bf16_t(self, p: torch.nn.Parameter) -> Optional[torch.Tensor]:
         return self._t_views.get(id(p))

@@ -677,6 +677,42 @@ def check_adam():
     return ("fused adam+clip vs torch.optim.Adam", err + (0 if sh < 1e-2 else 1), 1e-5)
 
 
+def check_adam_transposed():
+    """Adam writing the transposed bf16 shadow (adam_t_kernel): parameters vs torch.optim.Adam, and
+    every registered W^T view bit-equal to the transpose of the updated bf16 shadow."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay
+    from pytorch_vit_paper_replication_amd.runtime.param_store import get_store
+
+    torch.manual_seed(0)
+    cfg = dict(image_size=32, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=128, mlp_size=256, num_classes=10)
+    m1, m2 = ViT(**cfg).to(DEV), ViT(**cfg).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    m1.transformer_encoder[1].mlp_block.mlp[0].weight.requires_grad_(False)  # a frozen registered weight
+    m2.transformer_encoder[1].mlp_block.mlp[0].weight.requires_grad_(False)
+    st = get_store(m1, torch.device(DEV))
+    ws = [w for blk in m1.transformer_encoder for w in blk.fused_params()[2:12:2] if w.dim() == 2]
+    st.register_transposed(ws)
+    st.ensure_transposed()
+    o1 = FusedAdam(param_groups_weight_decay(m1, 0.03), lr=1e-2)
+    o2 = torch.optim.Adam(param_groups_weight_decay(m2, 0.03), lr=1e-2)
+    for it in range(3):
+        for p1, p2 in zip(m1.parameters(), m2.parameters()):
+            if not p1.requires_grad:
+                continue
+            g = torch.randn_like(p1) * (it + 1)
+            p1.grad.copy_(g)
+            p2.grad = g.clone()
+        o1.step(clip_norm=1.0)
+        torch.nn.utils.clip_grad_norm_([p for p in m2.parameters() if p.requires_grad], 1.0)
+        o2.step()
+    fused = o1._tmeta_key is not None and not st._t_dirty
+    err = max(rel_err(p1, p2) for p1, p2 in zip(m1.parameters(), m2.parameters()))
+    wt_exact = all(torch.equal(st.bf16_t(w), st.bf16(w).t()) for w in ws)
+    return (f"fused adam + W^T shadow vs torch.optim.Adam (fused path {fused}, W^T exact {wt_exact})",
+            err + (0 if fused and wt_exact else 1), 1e-5)
+
+
 def check_vit_fused_vs_reference(B=4, train=False, **over):
     """Whole-model forward logits and parameter gradients, fused bf16 vs PyTorch fp32 (dropout 0)."""
     from pytorch_vit_paper_replication_amd.models import ViT
@@ -937,6 +973,7 @@ def all_checks() -> List[Callable]:
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
         lambda: check_adam(),
+        check_adam_transposed,
         lambda: check_vit_fused_vs_reference(4, False),
         check_vit_inference,
         check_gemm_patch_embed_epilogue,
