@@ -43,6 +43,10 @@ def parse():
     p.add_argument("--pg-only", action="store_true", help="initialise a world-1 RCCL process group but do not wrap in DDP (A/B)")
     p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
     p.add_argument("--bucket-mb", type=float, default=28.0)
+    p.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
+                   help="gradient wire format of the DDP all-reduce (bf16: persistent bf16 mirror of the buckets)")
+    p.add_argument("--metrics-jsonl", default=None,
+                   help="per-step JSONL (step ms, img/s, lr, loss, grad-norm, per-bucket all-reduce ms) of the timed steps")
     p.add_argument("--graph", action="store_true", help="replay the whole training step as one captured hipGraph")
     p.add_argument("--infer", action="store_true",
                    help="serving throughput instead: eval-mode forward under inference_mode (no backward / optimizer)")
@@ -77,7 +81,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_vit_paper_replication_amd.models import vit
     from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
-    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import backward, cross_entropy
     from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
 
     rank, world, device = init_distributed()
@@ -104,7 +108,9 @@ def main():
         opt = torch.optim.Adam(groups, lr=1e-3, betas=(0.9, 0.999))
     sched = warmup_linear_decay(opt, max(total_steps, 20), 0.05)
     use_ddp = world > 1 or args.force_ddp
-    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, comm=args.comm) if use_ddp else model
+    net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, comm=args.comm,
+                                  comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None,
+                                  timing=bool(args.metrics_jsonl)) if use_ddp else model
 
     g = torch.Generator(device=device).manual_seed(rank)
     x = torch.rand(per_gpu, 3, args.image_size, args.image_size, device=device, generator=g)
@@ -121,7 +127,7 @@ def main():
             logits = net(x)
             loss = cross_entropy(logits, y)
             opt.zero_grad()
-            loss.backward()
+            backward(loss)
             opt.step(clip_norm=1.0)
         else:
             with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -176,10 +182,23 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    logger = None
+    if args.metrics_jsonl:
+        from pytorch_vit_paper_replication_amd.utils.metrics import StepLogger
+
+        # resolved after the timed region (no flush, hence no host sync, inside it)
+        logger = StepLogger(args.metrics_jsonl, flush_every=args.steps + 1, rank=rank, world=world, device=device)
     t0 = time.perf_counter()
     with stream_ctx:
         for _ in range(args.steps):
+            if logger is None:
+                loss = step()
+                continue
+            lr = opt.param_groups[0]["lr"]
+            logger.begin()
             loss = step()
+            logger.end(batch=per_gpu, loss=loss, grad_norm=getattr(opt, "last_grad_norm", None), lr=lr,
+                       ddp=net if use_ddp else None)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -189,6 +208,8 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item())
+    if logger is not None:
+        logger.close()
 
     if args.profile_out and rank == 0:
         from pytorch_vit_paper_replication_amd.utils.profiling import profile_steps
@@ -222,7 +243,7 @@ def main():
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
                        "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl + ("+hipgraph" if args.graph else ""),
-                       "grad_transport": net.transport if use_ddp else "none",
+                       "grad_transport": (net.transport + f" {args.comm_dtype} wire") if use_ddp else "none",
                        "optimizer": "none (inference: eval forward under inference_mode)" if args.infer else
                        "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
                        "dropout": "off (eval)" if args.infer else "0.1 (mlp, embedding)",

@@ -7,6 +7,7 @@ reference-style baseline is benchmarked). On CPU the PyTorch reference path alwa
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -67,8 +68,23 @@ def fallback_allowed() -> bool:
     return os.environ.get("PVR_ALLOW_TORCH_FALLBACK", "0") == "1"
 
 
+_FORCE_REFERENCE = 0
+
+
 def fused_disabled() -> bool:
-    return os.environ.get("PVR_DISABLE_FUSED", "0") == "1"
+    return _FORCE_REFERENCE > 0 or os.environ.get("PVR_DISABLE_FUSED", "0") == "1"
+
+
+@contextlib.contextmanager
+def reference_path():
+    """Run the module-by-module PyTorch path inside the block, even on the GPU (used by
+    :func:`utils.summary.summary`, whose per-module hooks the fused encoder would bypass)."""
+    global _FORCE_REFERENCE
+    _FORCE_REFERENCE += 1
+    try:
+        yield
+    finally:
+        _FORCE_REFERENCE -= 1
 
 
 def use_fused(t: torch.Tensor) -> bool:

@@ -32,6 +32,15 @@ hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hip
 hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 int pvr_patch_bwd_groups(int);
+hipError_t pvr_head_fwd(const uint16_t*, int64_t, int, int, const float*, const float*, float, const float*, const float*, int, float*, float*,
+                        float*, hipStream_t);
+hipError_t pvr_head_bwd(const float*, const float*, const float*, const float*, const float*, const float*, int, int, int, int, float*,
+                        float*, float*, float*, float*, uint16_t*, hipStream_t);
+hipError_t pvr_scale_by(const float*, const float*, float*, int64_t, hipStream_t);
+hipError_t pvr_mean(const float*, int, float*, hipStream_t);
+hipError_t pvr_metrics_accum(float*, const float*, const int*, int, hipStream_t);
+hipError_t pvr_rng_next(int64_t*, int64_t*, hipStream_t);
+hipError_t pvr_zero_f32(float*, int64_t, hipStream_t);
 hipError_t pvr_xent(const float*, int64_t, const int64_t*, int, int, float*, float*, int*, float, hipStream_t);
 int pvr_norm_partial_blocks();
 hipError_t pvr_grad_norm(const float*, int64_t, float, float*, float*, hipStream_t);
@@ -320,16 +329,24 @@ void patch_bwd(torch::Tensor dE, int64_t B, int64_t ntok, int64_t D, c10::option
         "patch_bwd");
 }
 
-// returns per-row losses; writes dlogits (if given) and increments correct[0]
+// returns per-row losses; writes dlogits (if given)
+// correct (optional): int32 [B], receives 1 where argmax(logits) == label. mean (optional): f32 [1],
+// receives the batch mean of the row losses (a second, one-workgroup launch).
 torch::Tensor xent(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> dlogits, c10::optional<torch::Tensor> correct,
-                   double grad_scale) {
+                   double grad_scale, c10::optional<torch::Tensor> mean) {
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits must be [B, C] row-major");
   TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous(), "xent: labels must be contiguous int64");
   const int64_t B = logits.size(0), C = logits.size(1);
+  if (correct.has_value() && correct->defined())
+    TORCH_CHECK(correct->is_cuda() && correct->numel() >= B && correct->scalar_type() == torch::kInt32, "xent: correct int32 [B]");
+  if (dlogits.has_value() && dlogits->defined())
+    TORCH_CHECK(dlogits->is_contiguous() && dlogits->numel() == B * C && dlogits->scalar_type() == torch::kFloat32, "xent: dlogits f32 [B][C]");
+  if (mean.has_value() && mean->defined()) TORCH_CHECK(mean->numel() >= 1, "xent: mean [1]");
   auto loss = torch::empty({B}, logits.options().dtype(torch::kFloat32));
   check(pvr_xent(f32(logits, "logits"), logits.stride(0), labels.data_ptr<int64_t>(), (int)B, (int)C, loss.data_ptr<float>(),
                  opt_ptr<float>(dlogits), opt_ptr<int>(correct), (float)grad_scale, stream()),
         "xent");
+  if (mean.has_value() && mean->defined()) check(pvr_mean(loss.data_ptr<float>(), (int)B, f32_mut(*mean, "mean"), stream()), "xent mean");
   return loss;
 }
 
@@ -373,6 +390,78 @@ void adam_t(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, 
                    reinterpret_cast<const pvr::AdamGroup*>(groups.data_ptr<float>()), opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0,
                    stream()),
         "adam_t");
+}
+
+// Classifier head forward: LayerNorm of each image's CLS row (token 0 of tokens [B*N][D] bf16) and
+// logits = LN(x) . W^T + bias in fp32. Returns {logits [B][C], xhat [B][D], rstd [B]} (the latter two
+// saved for head_bwd).
+std::vector<torch::Tensor> head_fwd(torch::Tensor tokens, int64_t B, int64_t N, torch::Tensor gamma, torch::Tensor beta, double eps,
+                                    torch::Tensor W, c10::optional<torch::Tensor> bias) {
+  const int64_t D = tokens.size(1);
+  TORCH_CHECK(tokens.dim() == 2 && tokens.size(0) == B * N && tokens.is_contiguous(), "head_fwd: tokens [B*N][D] contiguous");
+  TORCH_CHECK(D % 16 == 0 && D <= 1536, "head_fwd: D % 16 == 0, D <= 1536");
+  TORCH_CHECK(W.dim() == 2 && W.size(1) == D && W.is_contiguous() && gamma.numel() == D && beta.numel() == D, "head_fwd: shapes");
+  const int64_t C = W.size(0);
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) { TORCH_CHECK(bias->numel() == C && bias->is_contiguous(), "head_fwd: bias [C]"); bp = f32(*bias, "bias"); }
+  auto f = tokens.options().dtype(torch::kFloat32);
+  auto logits = torch::empty({B, C}, f);
+  auto xhat = torch::empty({B, D}, f);
+  auto rstd = torch::empty({B}, f);
+  check(pvr_head_fwd(bf(tokens, "tokens"), N * D, (int)B, (int)D, f32(gamma, "gamma"), f32(beta, "beta"), (float)eps, f32(W, "W"), bp,
+                     (int)C, xhat.data_ptr<float>(), rstd.data_ptr<float>(), logits.data_ptr<float>(), stream()),
+        "head_fwd");
+  return {logits, xhat, rstd};
+}
+
+// Classifier head backward: dW / db / dgamma / dbeta accumulate (+=) into the given fp32 gradients
+// (each optional), returns d(tokens) [B*N][D] bf16: the LayerNorm backward in every CLS row, zeros
+// elsewhere (written by the same launch).
+torch::Tensor head_bwd(torch::Tensor dlogits, torch::Tensor xhat, torch::Tensor rstd, torch::Tensor gamma, torch::Tensor beta,
+                       torch::Tensor W, int64_t B, int64_t N, c10::optional<torch::Tensor> dW, c10::optional<torch::Tensor> db,
+                       c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta) {
+  const int64_t C = W.size(0), D = W.size(1);
+  TORCH_CHECK(dlogits.dim() == 2 && dlogits.size(0) == B && dlogits.size(1) == C && dlogits.is_contiguous(), "head_bwd: dlogits [B][C]");
+  TORCH_CHECK(xhat.numel() == B * D && rstd.numel() == B && W.is_contiguous(), "head_bwd: saved tensors");
+  float* pdw = opt_ptr<float>(dW);
+  if (pdw) TORCH_CHECK(dW->numel() == C * D && dW->is_contiguous() && dW->scalar_type() == torch::kFloat32, "head_bwd: dW");
+  auto dy = torch::empty({B, D}, xhat.options());
+  auto dtok = torch::empty({B * N, D}, xhat.options().dtype(torch::kBFloat16));
+  check(pvr_head_bwd(f32(dlogits, "dlogits"), f32(xhat, "xhat"), f32(rstd, "rstd"), f32(gamma, "gamma"), f32(beta, "beta"), f32(W, "W"),
+                     (int)B, (int)C, (int)D, (int)N, pdw, opt_ptr<float>(db), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
+                     dy.data_ptr<float>(), reinterpret_cast<uint16_t*>(dtok.data_ptr()), stream()),
+        "head_bwd");
+  return dtok;
+}
+
+// y = x * s[0] (s a 1-element device tensor): the cross-entropy backward's upstream-gradient scale
+torch::Tensor scale_by(torch::Tensor x, torch::Tensor s) {
+  TORCH_CHECK(x.is_contiguous() && s.numel() >= 1, "scale_by: contiguous x, scalar s");
+  auto y = torch::empty_like(x);
+  check(pvr_scale_by(f32(x, "x"), f32(s, "s"), y.data_ptr<float>(), x.numel(), stream()), "scale_by");
+  return y;
+}
+
+// sums[0] += loss[0]; sums[1] += sum(correct) / B with correct = xent's per-row flags [B] (per-batch
+// metrics accumulated on the device)
+void metrics_accum(torch::Tensor sums, torch::Tensor loss, torch::Tensor correct) {
+  TORCH_CHECK(sums.numel() >= 2 && correct.scalar_type() == torch::kInt32 && correct.is_contiguous(),
+              "metrics_accum: sums [2] f32, correct int32 [B]");
+  check(pvr_metrics_accum(f32_mut(sums, "sums"), f32(loss, "loss"), correct.data_ptr<int>(), (int)correct.numel(), stream()),
+        "metrics_accum");
+}
+
+void rng_next(torch::Tensor rng, torch::Tensor seed) {
+  TORCH_CHECK(rng.is_cuda() && seed.is_cuda() && rng.scalar_type() == torch::kInt64 && seed.scalar_type() == torch::kInt64 &&
+                  rng.numel() >= 1 && seed.numel() >= 1,
+              "rng_next: int64 device tensors");
+  check(pvr_rng_next(rng.data_ptr<int64_t>(), seed.data_ptr<int64_t>(), stream()), "rng_next");
+}
+
+void zero_f32(torch::Tensor x) {
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 4 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "zero_f32: contiguous, 16-B aligned, numel % 4 == 0");
+  check(pvr_zero_f32(f32_mut(x, "x"), x.numel(), stream()), "zero_f32");
 }
 
 void scale_by_clip(torch::Tensor g, torch::Tensor clip) {
@@ -664,12 +753,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cls_rows", &cls_rows);
   m.def("patch_bwd", &patch_bwd);
   m.def("cu_mask_stream", &cu_mask_stream);
-  m.def("xent", &xent);
+  m.def("xent", &xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"), py::arg("correct"), py::arg("grad_scale"),
+        py::arg("mean") = py::none());
   m.def("grad_norm", &grad_norm);
   m.def("norm_partial_blocks", []() { return pvr_norm_partial_blocks(); });
   m.def("adam", &adam);
   m.def("adam_t", &adam_t);
   m.def("scale_by_clip", &scale_by_clip);
+  m.def("head_fwd", &head_fwd);
+  m.def("head_bwd", &head_bwd, py::arg("dlogits"), py::arg("xhat"), py::arg("rstd"), py::arg("gamma"), py::arg("beta"), py::arg("W"),
+        py::arg("B"), py::arg("N"), py::arg("dW") = py::none(), py::arg("db") = py::none(), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
+  m.def("scale_by", &scale_by);
+  m.def("metrics_accum", &metrics_accum);
+  m.def("rng_next", &rng_next);
+  m.def("zero_f32", &zero_f32);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A"), py::arg("fmt_a"), py::arg("B"), py::arg("fmt_b"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("scale_a"), py::arg("scale_b"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("aux") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0,

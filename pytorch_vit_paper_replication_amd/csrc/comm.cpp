@@ -4,7 +4,7 @@
 // MI355X-native DP transport the framework adds:
 //   * one communicator per process (one process per GPU), bootstrapped from an ncclUniqueId that
 //     rank 0 creates and the Python side broadcasts over the torch.distributed store;
-//   * every collective runs on the communicator's own high-priority HIP stream, ordered after the
+//   * every collective runs on the communicator's own (normal-priority) HIP stream, ordered after the
 //     work already queued on the caller's stream by an event (no host synchronisation), so bucket
 //     all-reduces overlap the rest of the backward pass;
 //   * completion is joined back into the caller's stream with hipStreamWaitEvent — the optimizer
@@ -147,7 +147,7 @@ class Communicator {
  public:
   Communicator(const std::string& uid_bytes, int rank, int world, int device)
       : rank_(rank), world_(world), device_(device),
-        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)) {
+        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/false, (c10::DeviceIndex)device)) {
     const Api& a = need_api();
     TORCH_CHECK(uid_bytes.size() == sizeof(ncclUniqueId), "bad unique id size ", uid_bytes.size());
     TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world ", rank, "/", world);
@@ -202,16 +202,27 @@ class Communicator {
     check_tensor(t);
     TORCH_CHECK(t.scalar_type() == torch::kFloat32, "mesh all-reduce: fp32 tensors");
     const size_t n = (size_t)t.numel();
-    const size_t need = (size_t)(world_ > 1 ? world_ - 1 : 0) * max_chunk(n, world_);
-    if (need > 0 && (!scratch_.defined() || (size_t)scratch_.numel() < need)) {
-      // grown rarely: earlier collectives on the (in-order) comm stream may still read the old one
-      hip_check(hipStreamSynchronize(stream_.stream()), "hipStreamSynchronize");
-      scratch_ = torch::empty({(int64_t)need}, torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device_));
-    }
+    const size_t need = mesh_scratch_elems(n);
+    // sized once at setup (reserve_mesh): growing here would need a stream sync mid-backward, since
+    // earlier collectives on the in-order comm stream may still read the old scratch
+    TORCH_CHECK(need == 0 || (scratch_.defined() && (size_t)scratch_.numel() >= need),
+                "mesh all-reduce of ", n, " elements needs reserve_mesh(>= ", n, ") first");
     const int64_t h = gate();
     RcclTransport tr(comm_, stream_.stream(), rank_, world_);
     mesh_all_reduce(tr, t.data_ptr<float>(), n, need ? scratch_.data_ptr<float>() : nullptr, average);
     return finish(h);
+  }
+
+  size_t mesh_scratch_elems(size_t n) const { return (size_t)(world_ > 1 ? world_ - 1 : 0) * max_chunk(n, world_); }
+
+  // Allocate the mesh all-reduce scratch for messages of up to max_numel elements (call at setup,
+  // before any collective is in flight: no synchronisation is needed then).
+  void reserve_mesh(int64_t max_numel) {
+    const size_t need = mesh_scratch_elems((size_t)max_numel);
+    if (need > 0 && (!scratch_.defined() || (size_t)scratch_.numel() < need)) {
+      hip_check(hipStreamSynchronize(stream_.stream()), "hipStreamSynchronize");  // setup only
+      scratch_ = torch::empty({(int64_t)need}, torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device_));
+    }
   }
 
   // out[world * n] <- all ranks' in[n] (stream-ordered like all_reduce_async)
@@ -336,6 +347,7 @@ void register_comm(pybind11::module& m) {
            py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
       .def("all_reduce_async", &Communicator::all_reduce_async, py::arg("tensor"), py::arg("average") = true)
       .def("all_reduce_mesh_async", &Communicator::all_reduce_mesh_async, py::arg("tensor"), py::arg("average") = true)
+      .def("reserve_mesh", &Communicator::reserve_mesh, py::arg("max_numel"))
       .def("all_gather_async", &Communicator::all_gather_async)
       .def("reduce_scatter_async", &Communicator::reduce_scatter_async, py::arg("input"), py::arg("output"),
            py::arg("average") = true)

@@ -1,6 +1,6 @@
 // Fused softmax cross-entropy for the classifier logits (reference GM/engine.py:53, :73-74;
 // SURVEY.md K13 + K16): one pass produces the per-row loss, d(loss)/d(logits) for the mean
-// reduction, and the argmax==label count used for the accuracy metric, so the engine does not
+// reduction, and the argmax==label flag per row for the accuracy metric, so the engine does not
 // need a separate softmax/argmax/eq/sum chain or a host sync per batch.
 #include "common.h"
 
@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(256) xent_kernel(const float* __restrict__ log
   const bool valid = y >= 0 && y < C;  // out-of-range labels (e.g. ignore_index) contribute nothing
   if (tid == 0) {
     loss_rows[b] = valid ? lse - x[y] : 0.f;
-    if (correct && mi == (int)y) atomicAdd(correct, 1);
+    if (correct) correct[b] = mi == (int)y ? 1 : 0;  // per-row flag: no zeroed counter needed
   }
   if (dlogits) {
     const float inv = 1.f / s;

@@ -12,7 +12,8 @@ MI355X-oriented differences (no behaviour change):
   * per-batch loss/accuracy accumulate on the device; the host syncs once per epoch instead of
     twice per batch (the reference's ``.item()`` calls, GM/engine.py:54,74,121,125);
   * with :class:`~..optim.FusedAdam` the clip runs inside the optimizer (device-side coefficient,
-    no sync) and ``nn.CrossEntropyLoss()`` is executed by the fused softmax-xent kernel;
+    no sync) and ``nn.CrossEntropyLoss()`` is executed by the fused softmax-xent kernel, whose
+    per-row argmax == label flags also give the accuracy (no separate argmax / eq / sum);
   * under ``torch.distributed`` metrics are all-reduced across ranks and only rank 0 prints.
 """
 from __future__ import annotations
@@ -28,6 +29,7 @@ except Exception:  # pragma: no cover
     def tqdm(x, **_):
         return x
 
+from .ops import fused_vit
 from .ops.fused_vit import cross_entropy
 from .utils.profiling import range_push
 
@@ -48,15 +50,32 @@ def _fused_loss(loss_fn):
     return loss_fn
 
 
-def _clip_and_step(model, optimizer, max_norm: Optional[float]):
+def _accumulate(sums: torch.Tensor, loss: torch.Tensor, logits: torch.Tensor, y: torch.Tensor, lf) -> None:
+    """sums += [batch loss, batch accuracy] on the device. With the fused cross-entropy the kernel's
+    per-row argmax == label flags are summed by one small HIP kernel; otherwise argmax / eq / sum."""
+    with torch.no_grad():
+        corr = fused_vit.last_correct if lf is cross_entropy else None
+        if corr is not None and sums.is_cuda and corr.numel() == logits.shape[0]:
+            from . import _ext
+
+            _ext.ext().metrics_accum(sums, loss.detach().float().reshape(1), corr)
+            return
+        acc = (logits.argmax(dim=1) == y).sum().float() / logits.shape[0]
+        sums += torch.stack([loss.detach().float(), acc])
+
+
+def _clip_and_step(model, optimizer, max_norm: Optional[float]) -> Optional[torch.Tensor]:
+    """Clip + optimizer step; returns the pre-clip global gradient norm (a device tensor) or None."""
     from .optim.adam import FusedAdam
 
     if isinstance(optimizer, FusedAdam):
         optimizer.step(clip_norm=max_norm)
-        return
+        return optimizer.last_grad_norm
+    norm = None
     if max_norm is not None:
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
+        norm = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=max_norm)
     optimizer.step()
+    return norm
 
 
 def _reduce_means(sums: torch.Tensor, count: int, device) -> Tuple[float, ...]:
@@ -80,29 +99,36 @@ def _set_sampler_epoch(dataloader, epoch: Optional[int]) -> None:
 
 def train_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, optimizer: torch.optim.Optimizer,
                lr_scheduler, device, *, max_grad_norm: Optional[float] = 1.0,
-               epoch: Optional[int] = None) -> Tuple[float, float]:
+               epoch: Optional[int] = None, step_logger=None) -> Tuple[float, float]:
     """One training epoch (reference GM/engine.py:9-79). Returns (train_loss, train_acc).
 
-    ``epoch`` (optional) seeds a ``DistributedSampler``'s shuffle for this epoch."""
+    ``epoch`` (optional) seeds a ``DistributedSampler``'s shuffle for this epoch. ``step_logger``
+    (optional :class:`~.utils.metrics.StepLogger`) gets one record per batch: step time, img/s, lr,
+    loss, gradient norm and, under this package's DDP built with ``timing=True``, per-bucket
+    all-reduce times — without a host synchronisation per step."""
     _set_sampler_epoch(dataloader, epoch)
     model.train()
     lf = _fused_loss(loss_fn)
     sums = torch.zeros(2, dtype=torch.float32, device=device)
     nb = 0
     for X, y in dataloader:
+        if step_logger is not None:
+            step_logger.begin()
         X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
         with range_push("forward"):  # ROCTX ranges (PVR_ROCTX=1, rocprofv3 --marker-trace)
             y_pred = model(X)
             loss = lf(y_pred, y)
         optimizer.zero_grad()
         with range_push("backward"):
-            loss.backward()
+            fused_vit.backward(loss)
         with range_push("optimizer"):
-            _clip_and_step(model, optimizer, max_grad_norm)
+            norm = _clip_and_step(model, optimizer, max_grad_norm)
+        lr = optimizer.param_groups[0]["lr"]
         lr_scheduler.step()
-        with torch.no_grad():
-            acc = (y_pred.argmax(dim=1) == y).sum().float() / y_pred.shape[0]
-            sums += torch.stack([loss.detach().float(), acc])
+        _accumulate(sums, loss, y_pred, y, lf)
+        if step_logger is not None:
+            step_logger.end(batch=X.shape[0], loss=loss, grad_norm=norm, lr=lr, epoch=epoch,
+                            ddp=model if hasattr(model, "pop_timing") else None)
         nb += 1
     loss_m, acc_m = _reduce_means(sums, nb, device)
     return loss_m, acc_m
@@ -119,8 +145,7 @@ def test_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, devi
             X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
             logits = model(X)
             loss = lf(logits, y)
-            acc = (logits.argmax(dim=1) == y).sum().float() / logits.shape[0]
-            sums += torch.stack([loss.float(), acc])
+            _accumulate(sums, loss, logits, y, lf)
             nb += 1
     loss_m, acc_m = _reduce_means(sums, nb, device)
     return loss_m, acc_m
@@ -129,8 +154,12 @@ def test_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, devi
 def train(model: torch.nn.Module, train_dataloader, test_dataloader, optimizer: torch.optim.Optimizer,
           loss_fn: torch.nn.Module, lr_scheduler, epochs: int, device, *, max_grad_norm: Optional[float] = 1.0,
           checkpoint_dir: Optional[str] = None, metrics_path: Optional[str] = None, start_epoch: int = 0,
-          results: Optional[Dict[str, List]] = None) -> Dict[str, List]:
+          results: Optional[Dict[str, List]] = None, step_metrics_path: Optional[str] = None,
+          log_every: int = 50) -> Dict[str, List]:
     """Train and test for ``epochs`` epochs (reference GM/engine.py:132-211).
+
+    ``metrics_path``: one JSONL record per epoch. ``step_metrics_path``: one JSONL record per training
+    step (:class:`~.utils.metrics.StepLogger`, flushed every ``log_every`` steps; rank 0 writes).
 
     Resume (new, optional): ``start_epoch`` epochs are already done (``load_checkpoint(...)["epoch"]``)
     and ``results`` holds their metrics; only epochs ``start_epoch + 1 .. epochs`` run, numbered as
@@ -140,10 +169,20 @@ def train(model: torch.nn.Module, train_dataloader, test_dataloader, optimizer: 
     model.to(device)
     epochs_left = range(start_epoch, epochs)
     it = tqdm(epochs_left) if _rank0() else epochs_left
+    step_logger = None
+    if step_metrics_path:
+        from .utils.metrics import StepLogger
+
+        world = torch.distributed.get_world_size() if _is_dist() else 1
+        rank = torch.distributed.get_rank() if _is_dist() else 0
+        step_logger = StepLogger(step_metrics_path, flush_every=log_every, rank=rank, world=world,
+                                 device=torch.device(device))
     for epoch in it:
         train_loss, train_acc = train_step(model=model, dataloader=train_dataloader, loss_fn=loss_fn,
                                            optimizer=optimizer, lr_scheduler=lr_scheduler, device=device,
-                                           max_grad_norm=max_grad_norm, epoch=epoch)
+                                           max_grad_norm=max_grad_norm, epoch=epoch, step_logger=step_logger)
+        if step_logger is not None:
+            step_logger.flush()
         test_loss, test_acc = test_step(model=model, dataloader=test_dataloader, loss_fn=loss_fn, device=device)
         if _rank0():
             print(f"Epoch: {epoch + 1} | "

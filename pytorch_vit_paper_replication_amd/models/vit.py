@@ -110,7 +110,9 @@ class SelfAttention(nn.Module):
         else:
             o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask, dropout_p=p)
         o = o.transpose(1, 2).reshape(B, Nq, D)
-        o = self.out_proj(o)
+        # a functional call on out_proj's parameters, as in nn.MultiheadAttention (so module hooks and
+        # torchinfo-style accounting see this layer exactly as they see the reference's MHA)
+        o = F.linear(o, self.out_proj.weight, self.out_proj.bias)
         if not self.batch_first:
             o = o.transpose(0, 1)
         return o, weights
@@ -227,8 +229,8 @@ class ViT(nn.Module):
                 rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
                 rng = torch.tensor([base * 2654435761 + rank * 40503], dtype=torch.int64, device=device)
             object.__setattr__(self, "_pvr_rng", rng)
-        seed = rng.clone()
-        rng.add_(1)
+        seed = torch.empty_like(rng)
+        _ext.ext().rng_next(rng, seed)  # seed = rng; rng += 1 (one device kernel, graph-replay safe)
         return seed
 
     def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:

@@ -454,64 +454,81 @@ class EncoderBlockFn(torch.autograd.Function):
 
 
 class HeadFn(torch.autograd.Function):
-    """Final LayerNorm (token 0 only) + classifier Linear in fp32."""
+    """Final LayerNorm (token 0 only) + classifier Linear in fp32 (csrc/head.hip: one forward launch;
+    backward: dW / db / dgamma / dbeta and d(LN input) in two launches that also zero the other token
+    rows of the returned gradient)."""
 
     @staticmethod
     def forward(ctx, tokens, B, N, eps, store, ln_w, ln_b, head_w, head_b):
         ext = _ext.ext()
-        T, D = tokens.shape
-        xc, mean, rstd = ext.layernorm_fwd(tokens, ln_w, ln_b, eps, B, N * D)
-        xcf = xc.float()
-        logits = F.linear(xcf, head_w, head_b)
-        ctx.save_for_backward(tokens, xcf, mean, rstd)
+        logits, xhat, rstd = ext.head_fwd(tokens, B, N, ln_w, ln_b, eps, head_w, head_b)
+        ctx.save_for_backward(xhat, rstd)
         ctx.meta = (B, N, store, ln_w, ln_b, head_w, head_b)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         ext = _ext.ext()
-        tokens, xcf, mean, rstd = ctx.saved_tensors
+        xhat, rstd = ctx.saved_tensors
         B, N, store, ln_w, ln_b, head_w, head_b = ctx.meta
-        D = tokens.shape[1]
+        g = store.grad_dest
         dlogits = dlogits.float().contiguous()
-        gw = store.grad_dest(head_w)
-        if gw is not None:
-            gw.addmm_(dlogits.t(), xcf)
-        gb = store.grad_dest(head_b)
-        if gb is not None:
-            gb.add_(dlogits.sum(0))
-        dxc = (dlogits @ head_w).to(torch.bfloat16).contiguous()
-        dtokens = torch.zeros_like(tokens)
-        ext.layernorm_bwd(dxc, D, tokens, N * D, mean, rstd, ln_w, None, 0, dtokens, N * D,
-                          store.grad_dest(ln_w), store.grad_dest(ln_b), B)
+        dtokens = ext.head_bwd(dlogits, xhat, rstd, ln_w, ln_b, head_w, B, N, g(head_w), g(head_b), g(ln_w), g(ln_b))
         store.grad_ready([head_w, head_b, ln_w, ln_b])
         return (dtokens,) + (None,) * 8
 
 
 class CrossEntropyFn(torch.autograd.Function):
-    """Mean softmax cross-entropy with the gradient produced in the same kernel pass."""
+    """Mean softmax cross-entropy with the gradient produced in the same kernel pass (and the per-row
+    argmax == label flags the engine's accuracy metric reads: ``last_correct``)."""
 
     @staticmethod
-    def forward(ctx, logits, target):
+    def forward(ctx, logits, target, correct):
         ext = _ext.ext()
         lf = logits.float().contiguous()
         B = lf.shape[0]
         dl = torch.empty_like(lf) if logits.requires_grad else None
-        rows = ext.xent(lf, target.long().contiguous(), dl, None, 1.0 / B)
+        mean = torch.empty((), dtype=torch.float32, device=lf.device)
+        ext.xent(lf, target.long().contiguous(), dl, correct, 1.0 / B, mean.view(1))
         ctx.save_for_backward(dl) if dl is not None else None
         ctx.in_dtype = logits.dtype
-        return rows.mean()
+        return mean
 
     @staticmethod
     def backward(ctx, g):
         (dl,) = ctx.saved_tensors
-        return (dl * g).to(ctx.in_dtype), None
+        return _ext.ext().scale_by(dl, g.float().reshape(1).contiguous()).to(ctx.in_dtype), None, None
+
+
+# int32 [B] argmax == label flags of the last fused cross_entropy call (device; read by the engine)
+last_correct: Optional[torch.Tensor] = None
 
 
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    global last_correct
     if _ext.use_fused(logits) and logits.dim() == 2 and target.dim() == 1:
-        return CrossEntropyFn.apply(logits, target)
+        correct = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
+        loss = CrossEntropyFn.apply(logits, target, correct)
+        last_correct = correct
+        return loss
+    last_correct = None
     return F.cross_entropy(logits, target)
+
+
+_UNIT: dict = {}
+
+
+def backward(loss: torch.Tensor) -> None:
+    """``loss.backward()`` seeded from a persistent device 1.0 of the loss's shape: autograd's own
+    seed is a fresh ``ones_like`` (an ATen fill kernel) on every step."""
+    if not loss.is_cuda:
+        loss.backward()
+        return
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    u = _UNIT.get(key)
+    if u is None:
+        u = _UNIT[key] = torch.ones_like(loss)
+    loss.backward(u)
 
 
 class TokenLayerNormFn(torch.autograd.Function):

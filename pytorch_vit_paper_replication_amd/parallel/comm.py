@@ -43,6 +43,10 @@ class NativeCommunicator:
             return self._c.all_reduce_mesh_async(t, average)
         return self._c.all_reduce_async(t, average)
 
+    def reserve_mesh(self, max_numel: int) -> None:
+        """Size the mesh all-reduce's scratch for messages up to ``max_numel`` fp32 (at setup)."""
+        self._c.reserve_mesh(int(max_numel))
+
     def reduce_scatter(self, inp: torch.Tensor, out: torch.Tensor, average: bool = True) -> int:
         return self._c.reduce_scatter_async(inp, out, average)
 

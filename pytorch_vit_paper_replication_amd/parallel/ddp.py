@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 import warnings
 from typing import Dict, List, Optional
 
@@ -36,12 +37,13 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
-from ..runtime.param_store import ParamStore, get_store
+from ..runtime.param_store import ParamStore, get_store, unique_params
 
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 28.0,
-                 broadcast_parameters: bool = True, comm_dtype: Optional[torch.dtype] = None, comm: str = "auto"):
+                 broadcast_parameters: bool = True, comm_dtype: Optional[torch.dtype] = None, comm: str = "auto",
+                 timing: bool = False, pad_buckets: bool = True):
         super().__init__()
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("DistributedDataParallel needs an initialised torch.distributed process group")
@@ -51,6 +53,7 @@ class DistributedDataParallel(nn.Module):
         self.bucket_cap = int(bucket_cap_mb * (1 << 20))
         self.broadcast_parameters = broadcast_parameters
         self.comm_dtype = comm_dtype
+        self.pad_buckets = pad_buckets
         self.require_backward_grad_sync = True
         self._store: Optional[ParamStore] = None
         self._buckets: List[tuple] = []          # (start, end, [param indices])
@@ -68,6 +71,12 @@ class DistributedDataParallel(nn.Module):
         # native transport's all-reduce schedule: "rccl" (RCCL's algorithm) or "mesh" (PVR_COMM_ALGO=mesh:
         # csrc/comm_core.h grouped point-to-point reduce-scatter + all-gather over every xGMI link)
         self._algo = os.environ.get("PVR_COMM_ALGO", "rccl")
+        # per-bucket all-reduce timing (utils.metrics.StepLogger): (bytes, start, end) per launched
+        # bucket, start = bucket ready on the compute stream, end = collective complete (HIP events
+        # on GPU, host clock with gloo)
+        self.timing = timing
+        self._timings: List[tuple] = []
+        self._timing_stream: Optional[torch.cuda.Stream] = None
 
     def _pick_transport(self, device):
         mode = os.environ.get("PVR_COMM", self._comm_mode)
@@ -84,8 +93,54 @@ class DistributedDataParallel(nn.Module):
             return None
 
     # ------------------------------------------------------------------ setup
+    def _plan(self, params) -> List[List[int]]:
+        """Bucket membership (parameter indices in launch order) from the parameters' order and sizes.
+
+        The parameters registered first (ViT: class token, position embedding, patch conv) receive
+        their gradients LAST, after the whole encoder backward: they get a small bucket of their own
+        (<= 4 MB), so the bucket before it (the first encoder block) is all-reduced while the
+        embedding backward still runs and only a few MB of collective remain after backward. The
+        rest: reverse parameter order, contiguous flat ranges of about bucket_cap bytes."""
+        tail_cap = min(self.bucket_cap, 4 << 20)
+        tail: List[int] = []
+        tail_bytes = 0
+        for i in range(len(params)):
+            nb = params[i].numel() * 4
+            if tail and tail_bytes + nb > tail_cap:
+                break
+            tail.append(i)
+            tail_bytes += nb
+        buckets = []
+        cur: List[int] = []
+        cur_bytes = 0
+        for i in reversed(range(len(tail), len(params))):
+            cur.append(i)
+            cur_bytes += params[i].numel() * 4
+            if cur_bytes >= self.bucket_cap:
+                buckets.append(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            buckets.append(cur)
+        if tail:
+            buckets.append(list(reversed(tail)))
+        return buckets
+
+    def pad_elems(self) -> int:
+        """Bucket granularity in fp32 elements: world x 7 x 4 KiB, so a ring or mesh
+        reduce-scatter splits every bucket into equal per-rank chunks of whole 4 KiB pages per xGMI
+        link (7 links per MI355X). 0 = unpadded (``pad_buckets=False``)."""
+        return self.world * 7 * 1024 if self.pad_buckets else 0
+
+    # ------------------------------------------------------------------ setup
     def _setup(self, device):
-        store = get_store(self.module, device)
+        st = getattr(self.module, "_pvr_store", None)
+        if st is not None and st is self._store and st.covers(self.module):
+            return st
+        _, params = unique_params(self.module)
+        plan = self._plan(params)
+        pad = self.pad_elems()
+        layout = (tuple(sorted(min(idxs) for idxs in plan)), pad) if pad else None
+        store = get_store(self.module, device, layout=layout)
         if store is self._store:
             return store
         for h in self._hooks:
@@ -111,42 +166,17 @@ class DistributedDataParallel(nn.Module):
             store.refresh_shadow(force=True)
         if self.comm_dtype is not None and self.comm_dtype != store.grad_flat.dtype:
             self._comm_buf = torch.empty(store.numel, dtype=self.comm_dtype, device=store.grad_flat.device)
-        # The parameters registered first (ViT: class token, position embedding, patch conv) receive
-        # their gradients LAST, after the whole encoder backward: they get a small bucket of their own
-        # (<= 4 MB), so the bucket before it (the first encoder block) is all-reduced while the
-        # embedding backward still runs and only a few MB of collective remain after backward.
-        tail_cap = min(self.bucket_cap, 4 << 20)
-        tail: List[int] = []
-        tail_bytes = 0
-        for i in range(len(store.params)):
-            nb = store.params[i].numel() * 4
-            if tail and tail_bytes + nb > tail_cap:
-                break
-            tail.append(i)
-            tail_bytes += nb
-        # the rest: reverse parameter order, contiguous flat ranges of about bucket_cap bytes
-        buckets = []
-        cur: List[int] = []
-        cur_bytes = 0
-        for i in reversed(range(len(tail), len(store.params))):
-            cur.append(i)
-            cur_bytes += store.params[i].numel() * 4
-            if cur_bytes >= self.bucket_cap:
-                buckets.append(cur)
-                cur, cur_bytes = [], 0
-        if cur:
-            buckets.append(cur)
-        if tail:
-            buckets.append(list(reversed(tail)))
         self._buckets = []
         self._bucket_of = {}
-        for bi, idxs in enumerate(buckets):
+        for bi, idxs in enumerate(plan):
             lo = min(store.offsets[i] for i in idxs)
             hi_i = max(idxs)
             hi = store.offsets[hi_i + 1] if hi_i + 1 < len(store.params) else store.numel
             self._buckets.append((lo, hi, idxs))
             for i in idxs:
                 self._bucket_of[id(store.params[i])] = bi
+        if self._native is not None and self._algo == "mesh" and self._buckets:
+            self._native.reserve_mesh(max(hi - lo for lo, hi, _ in self._buckets))
         store.add_listener(self._on_ready)
         for p in store.params:
             if p.requires_grad:
@@ -159,6 +189,7 @@ class DistributedDataParallel(nn.Module):
         self._ready_ids = set()
         self._next_launch = 0
         self._works = []
+        self._timings = []  # one step's bucket timings (a step nobody popped is dropped here)
         self._callback_queued = False
 
     # ------------------------------------------------------------------ forward
@@ -205,23 +236,50 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, b: int):
         lo, hi, _ = self._buckets[b]
         buf = self._store.grad_flat[lo:hi]
+        t0 = self._timing_start() if self.timing else None
+        tmp = None
+        if self._comm_buf is not None:  # low-precision wire format, persistent mirror: no allocator traffic
+            tmp = self._comm_buf[lo:hi]
+            tmp.copy_(buf)
+        wire = buf if tmp is None else tmp
         if self._native is not None:
-            if self._comm_buf is not None:  # low-precision wire format, persistent mirror: no allocator traffic
-                tmp = self._comm_buf[lo:hi]
-                tmp.copy_(buf)
-                self._works.append((self._native.all_reduce(tmp), buf, tmp))
-            else:
-                self._works.append((self._native.all_reduce(buf, algo=self._algo), buf, None))
-            return
-        if self.comm_dtype is not None and self.comm_dtype != buf.dtype:
-            tmp = buf.to(self.comm_dtype)
-            op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
-            w = dist.all_reduce(tmp, op=op, group=self.process_group, async_op=True)
-            self._works.append((w, buf, tmp))
+            w = self._native.all_reduce(wire, algo=self._algo if tmp is None else "rccl")
         else:
             op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
-            w = dist.all_reduce(buf, op=op, group=self.process_group, async_op=True)
-            self._works.append((w, buf, None))
+            w = dist.all_reduce(wire, op=op, group=self.process_group, async_op=True)
+        self._works.append((w, buf, tmp))
+        if t0 is not None:
+            self._timing_end(w, t0, wire.numel() * wire.element_size())
+
+    # ------------------------------------------------------------------ timing (opt-in)
+    def _timing_start(self):
+        if self._store.grad_flat.is_cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def _timing_end(self, w, t0, nbytes: int):
+        if isinstance(t0, float):
+            self._timings.append([nbytes, t0, w])  # resolved (host clock) when _finalize waits
+            return
+        if self._timing_stream is None:
+            self._timing_stream = torch.cuda.Stream(device=self._store.grad_flat.device)
+        ts = self._timing_stream
+        e = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(ts):  # ts waits for the collective (no host sync), then stamps it
+            if self._native is not None:
+                self._native.wait(w)
+            else:
+                w.wait()
+            e.record(ts)
+        self._timings.append((nbytes, t0, e))
+
+    def pop_timing(self) -> List[tuple]:
+        """This step's (bytes, start, end) per bucket, in launch order, and reset the list."""
+        out = [tuple(t) for t in self._timings]
+        self._timings = []
+        return out
 
     def _finalize(self):
         while self._next_launch < len(self._buckets):
@@ -236,6 +294,9 @@ class DistributedDataParallel(nn.Module):
             return
         for w, buf, tmp in self._works:
             w.wait()
+            for t in self._timings:  # gloo: completion stamped on the host clock when its wait returns
+                if isinstance(t, list) and t[2] is w:
+                    t[2] = time.perf_counter()
             if tmp is not None:
                 buf.copy_(tmp)
             if not self._avg:

@@ -53,7 +53,9 @@ class GraphedTrainStep:
         self.model.train()
         loss = self.loss_fn(self.model(self.static_x), self.static_y)
         self.optimizer.zero_grad()
-        loss.backward()
+        from ..ops.fused_vit import backward
+
+        backward(loss)
         self.optimizer.step(clip_norm=self.clip_norm)
         return loss.detach()
 

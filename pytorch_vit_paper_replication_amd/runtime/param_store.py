@@ -34,28 +34,46 @@ def _norm_device(device) -> torch.device:
     return d
 
 
+def unique_params(module: torch.nn.Module):
+    """(names, parameters) in registration order, shared parameters once: the store's layout order."""
+    seen = set()
+    params: List[torch.nn.Parameter] = []
+    names: List[str] = []
+    for n, p in module.named_parameters():
+        if id(p) in seen:
+            continue
+        seen.add(id(p))
+        params.append(p)
+        names.append(n)
+    return names, params
+
+
 class ParamStore:
-    def __init__(self, module: torch.nn.Module, device: torch.device):
-        seen = set()
-        params: List[torch.nn.Parameter] = []
-        names: List[str] = []
-        for n, p in module.named_parameters():
-            if id(p) in seen:
-                continue
-            seen.add(id(p))
-            params.append(p)
-            names.append(n)
+    """``layout = (starts, align)`` (optional): the parameters with these indices begin at a multiple
+    of ``align`` elements and the buffers end at one — the data-parallel bucketer passes its buckets'
+    first parameters, so every bucket is a whole number of ``align``-element blocks (zero padding
+    between buckets; it stays zero through backward, the all-reduce and the optimizer)."""
+
+    def __init__(self, module: torch.nn.Module, device: torch.device, layout=None):
+        names, params = unique_params(module)
         self.device = _norm_device(device)
+        self.layout = layout
         # grad mode at the model call, set by the model's fused forward: the autograd Functions' own
         # forward always runs with grad mode off, so an inference call is told here (no saved tensors)
         self.grad_enabled = True
         self.params = params
         self.names = names
         self.offsets: List[int] = []
+        starts, big = (layout if layout is not None else ((), ALIGN))
+        starts = set(starts)
         off = 0
-        for p in params:
+        for i, p in enumerate(params):
+            if i in starts:
+                off = (off + big - 1) // big * big
             self.offsets.append(off)
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        if starts:
+            off = (off + big - 1) // big * big
         self.numel = max(off, ALIGN)
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(params)}
         with torch.inference_mode(False), torch.no_grad():
@@ -295,7 +313,11 @@ class ParamStore:
 
     def zero_grad(self) -> None:
         self.join_side()
-        self.grad_flat.zero_()
+        g = self.grad_flat
+        if g.is_cuda and _ext.available() and g.numel() % 4 == 0:
+            _ext.ext().zero_f32(g)  # one 16-B-store kernel over the whole flat buffer
+        else:
+            g.zero_()
         for i, p in enumerate(self.params):
             if p.requires_grad:
                 p.grad = self._gviews[i]
@@ -352,11 +374,16 @@ def lookup_store(p: torch.nn.Parameter) -> Optional[ParamStore]:
     return st
 
 
-def get_store(module: torch.nn.Module, device: torch.device) -> ParamStore:
-    """Return the module's store for ``device``, (re)building it if parameters moved."""
+def get_store(module: torch.nn.Module, device: torch.device, layout=None) -> ParamStore:
+    """Return the module's store for ``device``, (re)building it if parameters moved or (when
+    ``layout`` is given) if its bucket layout differs. A rebuilt store copies values and gradients
+    from the old one (the parameters still point into it); FusedAdam re-keys its state on it."""
     st: Optional[ParamStore] = getattr(module, "_pvr_store", None)
-    if st is not None and st.device == _norm_device(device) and st.covers(module):
+    if st is not None and st.device == _norm_device(device) and st.covers(module) and \
+            (layout is None or st.layout == layout):
         return st
-    st = ParamStore(module, device)
+    if st is not None:
+        st.join_side()
+    st = ParamStore(module, device, layout)
     object.__setattr__(module, "_pvr_store", st)
     return st

@@ -640,14 +640,37 @@ def check_xent(B, C):
     logits = rnd(B, C) * 3
     y = torch.randint(0, C, (B,), device=DEV)
     dl = torch.empty_like(logits)
-    corr = torch.zeros(1, dtype=torch.int32, device=DEV)
-    rows = ext.xent(logits, y, dl, corr, 1.0 / B)
+    corr = torch.empty(B, dtype=torch.int32, device=DEV)
+    mean = torch.empty(1, device=DEV)
+    rows = ext.xent(logits, y, dl, corr, 1.0 / B, mean)
     lr = logits.clone().requires_grad_(True)
     ref = F.cross_entropy(lr, y)
     ref.backward()
-    e = max(rel_err(rows.mean(), ref), rel_err(dl, lr.grad) * 10)
-    ok_acc = corr.item() == (logits.argmax(1) == y).sum().item()
+    e = max(rel_err(rows.mean(), ref), rel_err(mean[0], ref), rel_err(dl, lr.grad) * 10)
+    ok_acc = torch.equal(corr.bool(), logits.argmax(1) == y)
     return (f"xent B{B} C{C}", e + (0 if ok_acc else 1), 1e-4)
+
+
+def check_head(B=37, N=5, D=192, C=1000):
+    """Classifier head kernels (final LayerNorm of the CLS rows + fp32 Linear, csrc/head.hip) vs
+    PyTorch fp32 autograd: logits, dW, db, dgamma, dbeta, d(tokens) (CLS rows; all other rows 0)."""
+    ext = _ext.ext()
+    tok = bf(rnd(B * N, D))
+    gam, bet = 1 + 0.1 * rnd(D), 0.1 * rnd(D)
+    W, b = rnd(C, D, scale=0.05), rnd(C)
+    logits, xhat, rstd = ext.head_fwd(tok, B, N, gam, bet, 1e-5, W, b)
+    t = tok.float().view(B, N, D).requires_grad_(True)
+    gr, br, Wr, bbr = (x.clone().requires_grad_(True) for x in (gam, bet, W, b))
+    ref = F.linear(F.layer_norm(t[:, 0], (D,), gr, br, 1e-5), Wr, bbr)
+    dl = rnd(B, C)
+    ref.backward(dl)
+    dW, db, dg, dbt = (torch.zeros_like(x) for x in (W, b, gam, bet))
+    dtok = ext.head_bwd(dl.contiguous(), xhat, rstd, gam, bet, W, B, N, dW, db, dg, dbt)
+    dt = dtok.float().view(B, N, D)
+    errs = [rel_err(logits, ref), rel_err(dW, Wr.grad), rel_err(db, bbr.grad), rel_err(dg, gr.grad), rel_err(dbt, br.grad),
+            rel_err(dt[:, 0], t.grad[:, 0])]
+    zeros_ok = bool((dt[:, 1:] == 0).all().item())
+    return (f"head fwd/bwd B{B} N{N} D{D} C{C} (errs {', '.join(f'{e:.1e}' for e in errs)})", max(errs) + (0 if zeros_ok else 1), 1e-2)
 
 
 def check_adam():
@@ -972,6 +995,9 @@ def all_checks() -> List[Callable]:
         lambda: check_fp8_nonfinite_recovery(),
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
+        lambda: check_head(),
+        lambda: check_head(256, 197, 768, 1000),
+        lambda: check_head(5, 3, 1280, 10),
         lambda: check_adam(),
         check_adam_transposed,
         lambda: check_vit_fused_vs_reference(4, False),

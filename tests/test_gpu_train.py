@@ -433,3 +433,19 @@ def test_ddp_two_ranks_fused_path_matches_single_process(tmp_path):
         a, b = r[0]["grads"][n].float(), p.grad.detach().cpu().float()
         err = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
         assert err < 2e-2, f"{n}: DDP(2 ranks) vs single-process gradient rel err {err:.3e}"
+
+
+def test_summary_on_gpu_model_matches_notebook():
+    # torchinfo-style summary of a cuda model: the per-module path runs inside the summary (the fused
+    # encoder would bypass the hooks), the fused path is back afterwards
+    from pytorch_vit_paper_replication_amd import _ext
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.utils.summary import summary
+
+    m = ViT(num_classes=3).cuda()
+    s = summary(m, input_size=(32, 3, 224, 224), print_out=False)
+    assert s.total_params == 85_800_963 and f"{s.total_mult_adds / 1e9:.2f}" == "5.52"
+    assert (s.input_mb, s.fwd_bwd_mb, s.params_mb, s.total_mb) == (19.27, 3330.74, 229.20, 3579.21)
+    x = torch.randn(2, 3, 224, 224, device="cuda")
+    assert _ext.use_fused(x)
+    assert m(x).shape == (2, 3)

@@ -4,6 +4,7 @@
 MAIN.ipynb:81), JSONL metrics and ROCTX ranges."""
 import json
 import os
+import re
 
 import numpy as np
 import pytest
@@ -144,3 +145,42 @@ def test_range_push_is_transparent(monkeypatch):
         with range_push("fwd"):
             x = 1 + 1
         assert x == 2
+
+
+def test_summary_matches_notebook_torchinfo_figures():
+    # MAIN.ipynb cell 80 / EX.ipynb cell 17: torchinfo.summary(ViT(num_classes=3), (32, 3, 224, 224))
+    torch.manual_seed(0)
+    s = summary(ViT(num_classes=3), input_size=(32, 3, 224, 224), print_out=False)
+    assert s.total_params == 85_800_963 and s.trainable_params == 85_800_963
+    assert f"{s.total_mult_adds / 1e9:.2f}" == "5.52"
+    assert (s.input_mb, s.fwd_bwd_mb, s.params_mb, s.total_mb) == (19.27, 3330.74, 229.20, 3579.21)
+    text = str(s)
+    for row in ("PatchEmbedding (patch_embedding_block)", "MultiHeadSelfAttentionBlock (msa_block)",
+                "Conv2d (0)", "Linear (0)"):
+        assert row in text
+    lines = {re.split(r"\s{2,}", ln.lstrip("│ └├─"))[0]: ln for ln in text.splitlines()}
+    assert "152,064" in lines["PatchEmbedding (patch_embedding_block)"]
+    assert "590,592" in lines["Conv2d (0)"]
+    assert "2,363,904" in lines["MultiHeadSelfAttentionBlock (msa_block)"]
+    assert "4,723,968" in lines["MLPBlock (mlp_block)"]
+    assert "2,307" in lines["Linear (0)"] and "[32, 3]" in lines["Linear (0)"]
+
+
+def test_summary_encoder_block_and_frozen_rows():
+    # MAIN.ipynb cell 71: the encoder block alone, batch 1 -> 7,087,872 params, 4.73 M mult-adds,
+    # 0.61 / 8.47 / 18.90 / 27.98 MB; the attention row carries nn.MultiheadAttention's 2,362,368
+    from pytorch_vit_paper_replication_amd.models.vit import TransformerEncoderBlock
+    blk = TransformerEncoderBlock()
+    s = summary(blk, input_size=(1, 197, 768), print_out=False)
+    assert s.total_params == 7_087_872
+    assert f"{s.total_mult_adds / 1e6:.2f}" == "4.73"
+    assert (s.input_mb, s.fwd_bwd_mb, s.params_mb, s.total_mb) == (0.61, 8.47, 18.90, 27.98)
+    att = [ln for ln in str(s).splitlines() if "(multi_head_attention)" in ln][0]
+    assert "2,362,368" in att and "--" in att  # keyword-called: no input shape, like torchinfo
+    for p in blk.mlp_block.parameters():
+        p.requires_grad_(False)
+    s2 = str(summary(blk, input_size=(1, 197, 768), print_out=False))
+    mlp = [ln for ln in s2.splitlines() if "Linear (0)" in ln][0]
+    assert "(2,362,368)" in mlp and "False" in mlp
+    top = s2.splitlines()[3]
+    assert "Partial" in top
