@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
     p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
     p.add_argument("--pg-only", action="store_true", help="initialise a world-1 RCCL process group but do not wrap in DDP (A/B)")
-    p.add_argument("--comm", choices=["auto", "native", "torch"], default="auto", help="DDP gradient transport")
+    p.add_argument("--comm", choices=["auto", "native", "native-mesh", "torch"], default="auto", help="DDP gradient transport")
     p.add_argument("--bucket-mb", type=float, default=28.0)
     p.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                    help="gradient wire format of the DDP all-reduce (bf16: persistent bf16 mirror of the buckets)")
@@ -50,7 +50,9 @@ def parse():
     p.add_argument("--graph", action="store_true", help="replay the whole training step as one captured hipGraph")
     p.add_argument("--infer", action="store_true",
                    help="serving throughput instead: eval-mode forward under inference_mode (no backward / optimizer)")
-    p.add_argument("--main-prio", type=int, default=int(os.environ.get("PVR_MAIN_PRIO", "-1")),
+    p.add_argument("--serial-wgrad", action="store_true",
+                   help="weight-gradient GEMMs on the main stream (no side stream): clean per-kernel times for profiles")
+    p.add_argument("--main-prio", type=int, default=-1,
                    help="run the step on a stream of this priority: -1 (default) puts the dgrad chain above the weight-gradient side stream; 0 = default stream")
     return p.parse_args()
 
@@ -84,6 +86,10 @@ def main():
     from pytorch_vit_paper_replication_amd.ops.fused_vit import backward, cross_entropy
     from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
 
+    if args.serial_wgrad:
+        from pytorch_vit_paper_replication_amd.runtime import param_store
+
+        param_store.SIDE_WGRAD = False
     rank, world, device = init_distributed()
     if args.gpus > 1 and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU (torch.distributed.run)")

@@ -55,8 +55,12 @@ def _run(cmd):
     return r.stdout
 
 
-def build_extension(verbose: bool = False, force: bool = False, jobs: int | None = None, debug: bool = False) -> Path:
+def build_extension(verbose: bool = False, force: bool = False, jobs: int | None = None, debug: bool = False,
+                    extra_flags: tuple = ()) -> Path:
     """Compile every HIP kernel for gfx950 and link the torch extension. Returns the .so path.
+
+    ``extra_flags``: additional hipcc flags for experiment builds (CLI: ``--hipcc-flag=-DFOO``); pass
+    ``force=True`` with them, since the incremental check compares timestamps only.
 
     ``debug=True`` builds ``_C_debug`` (separate objects) with ``-DPVR_DEBUG``: device-side
     ``PVR_ASSERT`` invariant checks in the kernels; load it with ``PVR_DEBUG_KERNELS=1``."""
@@ -73,7 +77,7 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
     hip_flags = [
         f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
         "-munsafe-fp-atomics", "-Wno-unused-result",
-    ] + os.environ.get("PVR_HIPCC_EXTRA", "").split()  # experiment builds (e.g. -DPVR_EXP=1)
+    ] + list(extra_flags)
     for src in hip_srcs:
         obj = build_dir / (src.stem + ".o")
         objs.append(obj)
@@ -115,5 +119,6 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
 
 if __name__ == "__main__":
     force = "--force" in sys.argv
-    p = build_extension(verbose=True, force=force, debug="--debug" in sys.argv)
+    extra = tuple(a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--hipcc-flag="))
+    p = build_extension(verbose=True, force=force or bool(extra), debug="--debug" in sys.argv, extra_flags=extra)
     print(p)

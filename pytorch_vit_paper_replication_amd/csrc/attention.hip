@@ -23,10 +23,6 @@
 #include "common.h"
 #include <type_traits>
 
-#ifndef PVR_ATTN_FWD_KT64
-#define PVR_ATTN_FWD_KT64 0
-#endif
-
 namespace pvr {
 namespace {
 
@@ -127,8 +123,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
                                                         int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale) {
   using C = Hd<DH>;
   // keys per tile: 64, or 32 for two-image head rows (dh > 64), so that the two K/V stages stay at
-  // 32 KiB and four workgroups share a CU (PVR_ATTN_FWD_KT64=1 build: 64 keys throughout)
-  constexpr int KT = C::NH == 1 || PVR_ATTN_FWD_KT64 ? 64 : 32;
+  // 32 KiB and four workgroups share a CU
+  constexpr int KT = C::NH == 1 ? 64 : 32;
   constexpr int NFR = KT / 16;                   // 16-key S fragments per tile
   constexpr int TILE_BYTES = KT * 128 * C::NH;   // one K or V tile image (8 or 16 KiB)
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [stage][K|V]
@@ -757,336 +753,6 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   }
 }
 
-// ------------------------------------------------------- backward, whole head (N <= 256, dh 64)
-// Two persistent kernels over (batch, head) pairs, each with the pair's operands double-buffered in
-// LDS exactly like the whole-head forward, and no barrier inside a pair:
-//   dq:  one wave per 16 queries (query on the MFMA lane). P^T is recomputed key chunk by key chunk
-//        straight from the saved log-sum-exp (no running max), dS^T = P^T (dP^T - delta) feeds
-//        dQ^T += K^T dS^T from registers. It also forms delta = rowsum(dO * O) and writes it for:
-//   dkv: one wave per 32 keys (key on the lane) with its K/V fragments in registers, sweeping every
-//        query block of the pair: dV^T += dO^T P, dK^T += Q^T dS.
-// S and dP are computed twice (once per kernel) in exchange for no dS exchange through LDS, no
-// per-query-block barriers and no idle key waves.
-template <int NF>
-__global__ void __launch_bounds__(NF * 64) attn_bwd_dq_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
-                                                                    const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                                    const uint16_t* __restrict__ o, int64_t ld_o,
-                                                                    const float* __restrict__ lse, float* __restrict__ delta,
-                                                                    uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H,
-                                                                    int D, int npairs, float scale) {
-  constexpr int DH = 64;
-  constexpr int NP = 32 * ((NF + 1) / 2);
-  constexpr int BUF = 2 * NP * 128;  // K | V images
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, li = lane & 15;
-  PVR_ASSERT((N + 15) / 16 == NF && blockDim.x == NF * 64 && (int)gridDim.x <= npairs);
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
-  const int p0 = L * per + min(L, rem);
-  const int p1 = p0 + per + (L < rem ? 1 : 0);
-  const int q = wave * 16 + li;
-  const int qrow = min(q, N - 1);
-  const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
-  const float c = scale * LOG2E;
-
-  auto issue = [&](int pr, char* buf) {
-    const uint16_t* base = qkv + (int64_t)(pr / H) * N * ld + (pr % H) * DH;
-    dma_rows<1>(make_rsrc(base + D, extent), buf, NP, ld, 0, wave, NF, lane);
-    dma_rows<1>(make_rsrc(base + 2 * D, extent), buf + NP * 128, NP, ld, 0, wave, NF, lane);
-  };
-  // per-lane query operands: Q, dO, O fragments (lane holds X[q][32ks + 8g + j]) and lse
-  struct QOps {
-    v8s qf[2], df[2], of[2];
-    float l2;
-  };
-  auto load_q = [&](int pr, QOps& t) {
-    const int64_t row = (int64_t)(pr / H) * N + qrow;
-    const int col = (pr % H) * DH + 8 * g;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      t.qf[ks] = *(const v8s*)(qkv + row * ld + col + 32 * ks);
-      t.df[ks] = *(const v8s*)(dout + row * ld_do + col + 32 * ks);
-      t.of[ks] = *(const v8s*)(o + row * ld_o + col + 32 * ks);
-    }
-    t.l2 = lse[(int64_t)pr * N + qrow];  // scaled at use: any math here would wait for the load now
-  };
-  auto settle = [&](QOps& t) {  // the compiler's wait for these loads sits here, not at first use
-    asm volatile("" : "+v"(t.qf[0]), "+v"(t.qf[1]), "+v"(t.df[0]), "+v"(t.df[1]));
-    asm volatile("" : "+v"(t.of[0]), "+v"(t.of[1]), "+v"(t.l2));
-  };
-  constexpr int STORES = 5;  // dQ row (4 x 8 B) + delta, per wave per pair (see the counted wait)
-  const uint32_t dq_extent = clamp_bytes(((int64_t)(N - 1) * ld_dq + DH) * 2);
-
-  if (p0 >= p1) return;
-  QOps cur, nxt;
-  issue(p0, smem);
-  load_q(p0, cur);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  settle(cur);
-  for (int pr = p0; pr < p1; ++pr) {
-    const int it = pr - p0;
-    const char* kimg = smem + (it & 1) * BUF;
-    const char* vimg = kimg + NP * 128;
-    if (pr + 1 < p1) {
-      issue(pr + 1, smem + ((it + 1) & 1) * BUF);
-      load_q(pr + 1, nxt);
-    }
-    const float l2 = cur.l2 * LOG2E;
-    // delta[q] = dO[q] . O[q]: 16 dims per lane, then across the 4 lane groups
-    float dl = dot8_bf16(cur.df[1], cur.of[1], dot8_bf16(cur.df[0], cur.of[0], 0.f));
-    dl += __shfl_xor(dl, 16, 64);
-    dl += __shfl_xor(dl, 32, 64);
-    v4f dq[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) dq[e] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < (NF + 1) / 2; ++kk) {
-      // S^T, dP^T for keys 32kk .. 32kk+31 (two 16-key fragments)
-      v4f sv[2], dp[2];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int f = 2 * kk + h2;
-        sv[h2] = dp[h2] = v4f{0.f, 0.f, 0.f, 0.f};
-        if (f < NF) {
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            sv[h2] = mfma16(frag_rows(kimg, NP, 16 * f, ks, lane), cur.qf[ks], sv[h2]);
-            dp[h2] = mfma16(frag_rows(vimg, NP, 16 * f, ks, lane), cur.df[ks], dp[h2]);
-          }
-        }
-      }
-      // K^T fragments for dQ^T (asm transpose reads: the next pair's DMA stays in flight)
-      v4s klo[4], khi[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) frag_tr_async(kimg, NP, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, klo[e], khi[e]);
-      // dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse2); keys past N contribute nothing.
-      // NF = ceil(N / 16), so keys below 16 (NF - 1) are always < N: only the chunks reaching
-      // past that need the mask (one of seven at N = 197; cmp + cndmask per element otherwise).
-      const bool tail = 32 * kk + 32 > 16 * (NF - 1);  // folds per unrolled kk
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = 32 * kk + 16 * h2 + 4 * g + r;
-          const float e = __builtin_amdgcn_exp2f(fmaf(sv[h2][r], c, -l2));
-          const float pv = (!tail || key < N) ? e : 0.f;
-          sv[h2][r] = pv * (dp[h2][r] - dl);
-        }
-      const v8s dsf = pack_p(sv[0], sv[1]);
-      lds_wait();
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dq[e] = mfma16(cat44(klo[e], khi[e]), dsf, dq[e]);
-    }
-    // dQ row q (lane: dims 16e + 4g .. +3) and delta[q]: buffer stores, dropped past N / off group 0
-    {
-      typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-      const bool ok = q < N;
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc(dqkv + (int64_t)(pr / H) * N * ld_dq + (pr % H) * DH, dq_extent);
-      const uint32_t vo = ok ? (uint32_t)((q * ld_dq + 4 * g) * 2) : 0x80000000u;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const v2u w = {pack2bf(dq[e][0] * scale, dq[e][1] * scale), pack2bf(dq[e][2] * scale, dq[e][3] * scale)};
-        __builtin_amdgcn_raw_buffer_store_b64(w, rs, vo + 32 * e, 0, 0);
-      }
-      const __amdgpu_buffer_rsrc_t dsr = make_rsrc(delta + (int64_t)pr * N, (uint32_t)N * 4);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dl), dsr, ok && g == 0 ? (uint32_t)q * 4 : 0x80000000u, 0, 0);
-    }
-    static_assert(STORES == 5, "the vmcnt below counts the dQ / delta store instructions");
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    __syncthreads();
-    cur = nxt;
-    settle(cur);
-  }
-}
-
-// KF = key fragments (of 16) per wave: KF = 2 is 32 keys per wave (NK = ceil(N / 32) waves); KF = 1
-// is 16 keys per wave with twice the waves (half the accumulators per wave, more waves to hide latency).
-template <int NK, int KF>
-__global__ void __launch_bounds__(NK * 64) attn_bwd_dkv_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
-                                                                     const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                                     const float* __restrict__ lse, const float* __restrict__ delta,
-                                                                     uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H,
-                                                                     int D, int npairs, float scale) {
-  constexpr int DH = 64;
-  constexpr int NQB = (NK * KF + 1) / 2;      // 32-query blocks
-  constexpr int NP = 32 * NQB;                // query rows staged (and keys covered)
-  constexpr int BUF = 2 * NP * 128 + 2048;    // Q | dO images | lse | delta (1 KiB DMA slots)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, li = lane & 15;
-  PVR_ASSERT((N + 16 * KF - 1) / (16 * KF) == NK && blockDim.x == NK * 64 && (int)gridDim.x <= npairs);
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
-  const int p0 = L * per + min(L, rem);
-  const int p1 = p0 + per + (L < rem ? 1 : 0);
-  const int kw0 = wave * 16 * KF;
-  const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
-  const uint32_t do_extent = clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2);
-  const float c = scale * LOG2E;
-
-  auto issue = [&](int pr, char* buf) {
-    const int b = pr / H, h = pr % H;
-    dma_rows<1>(make_rsrc(qkv + (int64_t)b * N * ld + h * DH, extent), buf, NP, ld, 0, wave, NK, lane);
-    dma_rows<1>(make_rsrc(dout + (int64_t)b * N * ld_do + h * DH, do_extent), buf + NP * 128, NP, ld_do, 0, wave, NK, lane);
-    if (wave == NK - 1) {  // lse and delta rows of the pair (queries past N read as 0)
-      dma16(make_rsrc(lse + (int64_t)pr * N, (uint32_t)N * 4), to_lds(buf + 2 * NP * 128), (uint32_t)lane * 16);
-      dma16(make_rsrc(delta + (int64_t)pr * N, (uint32_t)N * 4), to_lds(buf + 2 * NP * 128 + 1024), (uint32_t)lane * 16);
-    }
-  };
-  // this wave's 32 keys: K and V fragments as B operands (lane holds X[kw0 + 16f + li][32ks + 8g + j])
-  struct KOps {
-    v8s kf[KF][2], vf[KF][2];
-  };
-  auto load_k = [&](int pr, KOps& t) {
-    const uint16_t* base = qkv + (int64_t)(pr / H) * N * ld + (pr % H) * DH + 8 * g;
-#pragma unroll
-    for (int f = 0; f < KF; ++f) {
-      const int key = min(kw0 + 16 * f + li, N - 1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        t.kf[f][ks] = *(const v8s*)(base + (int64_t)key * ld + D + 32 * ks);
-        t.vf[f][ks] = *(const v8s*)(base + (int64_t)key * ld + 2 * D + 32 * ks);
-      }
-    }
-  };
-  auto settle = [&](KOps& t) {
-#pragma unroll
-    for (int f = 0; f < KF; ++f) {
-      asm volatile("" : "+v"(t.kf[f][0]), "+v"(t.kf[f][1]));
-      asm volatile("" : "+v"(t.vf[f][0]), "+v"(t.vf[f][1]));
-    }
-  };
-  constexpr int STORES = 8 * KF;  // dK and dV rows: KF key fragments x 4 dim fragments x 2
-  const uint32_t dkv_extent = clamp_bytes(((int64_t)(N - 1) * ld_dq + 2 * D + DH) * 2);
-
-  if (p0 >= p1) return;
-  KOps cur, nxt;
-  issue(p0, smem);
-  load_k(p0, cur);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  settle(cur);
-  for (int pr = p0; pr < p1; ++pr) {
-    const int it = pr - p0;
-    const char* qimg = smem + (it & 1) * BUF;
-    const char* doimg = qimg + NP * 128;
-    const float* s_l2 = (const float*)(qimg + 2 * NP * 128);
-    const float* s_dl = s_l2 + 256;
-    if (pr + 1 < p1) {
-      issue(pr + 1, smem + ((it + 1) & 1) * BUF);
-      if constexpr (KF == 2) load_k(pr + 1, nxt);  // KF = 1: after the sweep (keeps 16 VGPRs free in it)
-    }
-    v4f dk[4][KF], dv[4][KF];
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int f = 0; f < KF; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
-    if (kw0 < N) {  // uniform: waves past N only stage
-#pragma unroll 1
-      for (int qb = 0; qb < NQB; ++qb) {
-        // S[q][key], dP[q][key]: lane holds [q = 32qb + 16a + 4g + r][key = kw0 + 16f + li]
-        v4f sv[2][KF], dp[2][KF];
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int f = 0; f < KF; ++f) sv[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int a = 0; a < 2; ++a) {
-            const v8s qa = frag_rows(qimg, NP, 32 * qb + 16 * a, ks, lane);
-            const v8s da = frag_rows(doimg, NP, 32 * qb + 16 * a, ks, lane);
-#pragma unroll
-            for (int f = 0; f < KF; ++f) {
-              sv[a][f] = mfma16(qa, cur.kf[f][ks], sv[a][f]);
-              dp[a][f] = mfma16(da, cur.vf[f][ks], dp[a][f]);
-            }
-          }
-        // dO^T / Q^T fragments for the dV / dK products (asm transpose reads). KF = 1 reads Q^T only
-        // after the dV products, so both sets are never live together (fits 128 VGPRs, no spills).
-        v4s dlo[4], dhi[4], qlo[4], qhi[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          frag_tr_async(doimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, dlo[e], dhi[e]);
-          if constexpr (KF == 2) frag_tr_async(qimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, qlo[e], qhi[e]);
-        }
-        // P = exp2(S c - lse2[q]), dS = P (dP - delta[q]); queries past N have zero Q / dO rows
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const v4f l4 = *(const v4f*)(s_l2 + 32 * qb + 16 * a + 4 * g);
-          const v4f d4 = *(const v4f*)(s_dl + 32 * qb + 16 * a + 4 * g);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int f = 0; f < KF; ++f) {
-              const float pv = __builtin_amdgcn_exp2f(fmaf(sv[a][f][r], c, -l4[r] * LOG2E));
-              sv[a][f][r] = pv;
-              dp[a][f][r] = pv * (dp[a][f][r] - d4[r]);
-            }
-        }
-        v8s pf[KF], sf[KF];
-#pragma unroll
-        for (int f = 0; f < KF; ++f) {
-          pf[f] = pack_p(sv[0][f], sv[1][f]);
-          sf[f] = pack_p(dp[0][f], dp[1][f]);
-        }
-        lds_wait();
-        if constexpr (KF == 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const v8s dot = cat44(dlo[e], dhi[e]), qt = cat44(qlo[e], qhi[e]);
-#pragma unroll
-            for (int f = 0; f < KF; ++f) {
-              dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
-              dk[e][f] = mfma16(qt, sf[f], dk[e][f]);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            dv[e][0] = mfma16(cat44(dlo[e], dhi[e]), pf[0], dv[e][0]);
-            frag_tr_async(qimg, NP, 32 * qb + 4 * g, 32 * qb + 16 + 4 * g, 16 * e, lane, qlo[e], qhi[e]);
-          }
-          lds_wait();
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dk[e][0] = mfma16(cat44(qlo[e], qhi[e]), sf[0], dk[e][0]);
-        }
-      }
-    }
-    if constexpr (KF == 1) {
-      if (pr + 1 < p1) load_k(pr + 1, nxt);
-    }
-    // dK (x scale), dV rows: lane holds X^T[d = 16e + 4g + r][key = kw0 + 16f + li]; buffer stores
-    // (keys past N dropped), exactly STORES per wave
-    {
-      typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-      const __amdgpu_buffer_rsrc_t rs = make_rsrc(dqkv + (int64_t)(pr / H) * N * ld_dq + (pr % H) * DH, dkv_extent);
-#pragma unroll
-      for (int f = 0; f < KF; ++f) {
-        const int key = kw0 + 16 * f + li;
-        const uint32_t vo = key < N ? (uint32_t)((key * ld_dq + 4 * g) * 2) : 0x80000000u;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const v2u wk = {pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale), pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale)};
-          const v2u wv = {pack2bf(dv[e][f][0], dv[e][f][1]), pack2bf(dv[e][f][2], dv[e][f][3])};
-          __builtin_amdgcn_raw_buffer_store_b64(wk, rs, vo + (uint32_t)(D + 16 * e) * 2, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(wv, rs, vo + (uint32_t)(2 * D + 16 * e) * 2, 0, 0);
-        }
-      }
-    }
-    static_assert(STORES == 16 || STORES == 8, "the vmcnt below counts the dK / dV store instructions");
-    if constexpr (STORES == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    __syncthreads();
-    cur = nxt;
-    settle(cur);
-  }
-}
-
 // Backward contribution of ONE key (index kt = N - 1) of every (batch, head) pair, after the main
 // kernel has covered keys [0, N - 1) and written dQ directly (bf16). For ViT's N = 256 + 1 (the CLS
 // token of 224/14) the main kernel's key blocks are then exactly full: a 512-thread workgroup per
@@ -1190,10 +856,9 @@ __global__ void __launch_bounds__(256) attn_bwd_lastkey_kernel(const uint16_t* _
   }
 }
 
-// ------------------------------------------- backward, whole head, one pipelined kernel (dh 64)
-// 192 < N <= 256 (ViT-B/16 and ViT-L/16 at 224 px: N = 197). One persistent 4-wave workgroup per CU
-// (one wave per SIMD, 512 registers each: every operand and accumulator stays in registers) walks its
-// (batch, head) pairs; each pair is NQ = ceil(N / 32) blocks of 32 queries, and the blocks of
+// ------------------------------------------- backward, whole head, pipelined (dh 64, 192 < N <= 224)
+// ViT-B/16 and ViT-L/16 at 224 px (N = 197). The algorithm (stated for a 4-wave form; the kernel
+// below is its 8-wave version): one persistent workgroup per CU walks its (batch, head) pairs; each pair is NQ = ceil(N / 32) blocks of 32 queries, and the blocks of
 // consecutive pairs form one stream. Wave w owns keys [64w, 64w + 64): their K / V fragments sit in
 // registers for the pair and dK^T / dV^T accumulate in registers over the pair's blocks (key
 // fragments entirely past N are skipped). Block t:
@@ -1209,433 +874,9 @@ __global__ void __launch_bounds__(256) attn_bwd_lastkey_kernel(const uint16_t* _
 // key fragments. LDS-DMA streams block t+3's Q / dO / O / lse rows (4-slot ring) and slices of the
 // NEXT pair's K / V images under block t: exactly 7 DMAs per wave per block, issued after the
 // block's stores, so one counted wait (vmcnt 7: only the newest group in flight) serves every block.
-template <int N>
-PVR_DEV void wait_barrier_lds0() { wait_barrier_lds<0>(); }
-#ifdef PVR_PIPE_SAFE
-#define PIPE_WAIT wait_barrier_lds0
-#else
-#define PIPE_WAIT wait_barrier_lds
-#endif
-#ifdef PVR_PRO_SAFE
-#define PRO_WAIT wait_barrier_lds0
-#else
-#define PRO_WAIT wait_barrier_lds
-#endif
-template <int NQ>
-__global__ void __launch_bounds__(256, 1) attn_bwd_pipe_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
-                                                                const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                                const uint16_t* __restrict__ o, int64_t ld_o,
-                                                                const float* __restrict__ lse, uint16_t* __restrict__ dqkv,
-                                                                int64_t ld_dq, float* __restrict__ dbp, int N, int H, int D,
-                                                                int npairs, float scale) {
-  static_assert(NQ == 7 || NQ == 8, "192 < N <= 256");
-  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-  constexpr int DH = 64;
-  constexpr int NP = 32 * NQ;               // staged rows (queries / keys) per pair
-  constexpr int KR = 256;                   // key rows of the images: 4 waves x 64 keys
-  constexpr int IMG = KR * 128;             // K or V image: [256][128 B], swizzled (lds_off)
-  constexpr int SLOT = 3 * 4096 + 1024;     // ring slot: Q | dO | O rows of one block, lse DMA slot
-  constexpr int RING = 4;
-  constexpr int DSB = KR * 64;              // dS^T image [key][32 queries]
-  constexpr int NKV = NP / 4;               // 1 KiB pieces of one pair's K + V images
-  constexpr int NDMA = 7;                   // DMA instructions per wave per block
-  constexpr int NSTAGE = 13;                // 1 KiB pieces of one block: 4 Q + 4 dO + 4 O + lse
-  constexpr int KV_PER_IT = 4 * NDMA - 16;  // next-pair K/V pieces per block (slots 16 .. 27)
-  static_assert((NQ - 2) * KV_PER_IT >= NKV, "the next pair's K/V images must land two blocks before it starts");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* kimg = smem;
-  char* vimg = smem + IMG;
-  char* ring = smem + 2 * IMG;
-  char* dsb = ring + RING * SLOT;
-  float* s_tab = (float*)(dsb + 2 * DSB);   // [2][64]: lse * log2e [32] | delta [32] of a block
-  float* vsb = s_tab + 128;                  // [64]: dV-bias partial of the last block (wave 0 only)
-  char* sink = (char*)(vsb + 64);           // 1 KiB target of the null DMAs that keep vmcnt uniform
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, li = lane & 15;
-  PVR_ASSERT(blockDim.x == 256 && (N + 31) / 32 == NQ && (int)gridDim.x <= npairs);
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
-  const int p0 = L * per + min(L, rem);
-  const int p1 = p0 + per + (L < rem ? 1 : 0);
-  if (p0 >= p1) return;
-  const int kw0 = wave * 64;
-  const int nf = min(4, max(0, (N - kw0 + 15) / 16));  // this wave's key fragments holding a key < N
-  const float c = scale * LOG2E;
-  const int64_t rows_all = (int64_t)(npairs / H) * N;
-  // one buffer resource per tensor (host check: every byte offset fits in 31 bits); rows past N and
-  // dropped stores use offset 0x80000000, outside every resource (zero-filled / dropped)
-  const __amdgpu_buffer_rsrc_t rq = make_rsrc(qkv, clamp_bytes(((rows_all - 1) * ld + 3 * D) * 2));
-  const __amdgpu_buffer_rsrc_t rdo = make_rsrc(dout, clamp_bytes(((rows_all - 1) * ld_do + D) * 2));
-  const __amdgpu_buffer_rsrc_t ro = make_rsrc(o, clamp_bytes(((rows_all - 1) * ld_o + D) * 2));
-  const __amdgpu_buffer_rsrc_t rl = make_rsrc(lse, clamp_bytes((int64_t)npairs * N * 4));
-  const __amdgpu_buffer_rsrc_t rdq = make_rsrc(dqkv, clamp_bytes(((rows_all - 1) * ld_dq + 3 * D) * 2));
-  constexpr uint32_t OOR = 0x80000000u;
-  const uint32_t ldq = (uint32_t)ld * 2, lddo = (uint32_t)ld_do * 2, ldoo = (uint32_t)ld_o * 2, lddq = (uint32_t)ld_dq * 2;
-
-  // ---- lane-dependent offsets, computed once
-  const int l3 = lane >> 3, l7 = lane & 7;
-  const int q4 = (lane >> 2) & 3, p4 = lane & 3;
-  // staging pieces: image row srl = 8 wave + l3 of a 32-row block (Q, dO, O: one piece each per wave)
-  const int srl = 8 * wave + l3;
-  const uint32_t sch = (uint32_t)((l7 ^ swz_a(srl)) << 4);
-  const uint32_t stq = (uint32_t)srl * ldq + sch, std_ = (uint32_t)srl * lddo + sch, sto = (uint32_t)srl * ldoo + sch;
-  // K/V piece rows rr + l3 (rr a multiple of 8): the swizzle term depends on rr's bit 3 only
-  const uint32_t kvo0 = (uint32_t)l3 * ldq + (uint32_t)((l7 ^ swz_a(l3)) << 4);
-  const uint32_t kvo1 = (uint32_t)l3 * ldq + (uint32_t)((l7 ^ swz_a(8 + l3)) << 4);
-  // A-operand rows (query 16a + li, dims 32ks + 8g ..): a adds 2048
-  const int fr0 = li * 128 + ((g ^ swz_a(li)) << 4);
-  const int fr1 = li * 128 + (((4 + g) ^ swz_a(li)) << 4);
-  // Q^T / dO^T transposed reads (rows 4g + q4, +16 -> +2048), dims 16e + 4p4
-  int trq[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) trq[e] = (4 * g + q4) * 128 + (((2 * e + (p4 >> 1)) ^ swz_a(4 * g + q4)) << 4) + 8 * (p4 & 1);
-  // dS^T image [key][query]: 8-B unit u = query / 4 XOR-swizzled by (key >> 1) & 7 (conflict-free for
-  // the ds_write_b64 of a 16-key column and for the transposed reads); keys kw0 + 16f + li
-  auto ds_off = [](int key, int u) { return key * 64 + ((u ^ ((key >> 1) & 7)) << 3); };
-  const int dsw0 = ds_off(li, g) + kw0 * 64, dsw1 = ds_off(li, 4 + g) + kw0 * 64;  // a = 0 / 1; f adds 1024
-  // phase 2: dS^T rows 32ks + 8g + q4 (+4), queries 16a + 4p4 (a: unit + 4)
-  const int p2lo0 = ds_off(8 * g + q4, p4), p2hi0 = ds_off(8 * g + q4 + 4, p4);
-  const int p2lo1 = ds_off(8 * g + q4, 4 + p4), p2hi1 = ds_off(8 * g + q4 + 4, 4 + p4);
-  // next-block table: queries 8 wave + l3, dims 8 l7 .. 8 l7 + 7 (one 16-B chunk)
-  const int tq = 8 * wave + l3;
-  const int tbo = tq * 128 + ((l7 ^ swz_a(tq)) << 4);
-
-  struct PairOff {
-    uint32_t row, col;  // b * N, h * DH * 2 (bytes)
-  };
-  auto pair_off = [&](int pr) { return PairOff{(uint32_t)((pr / H) * N), (uint32_t)((pr % H) * DH * 2)}; };
-  auto dma = [&](__amdgpu_buffer_rsrc_t rs, char* img, uint32_t voff) { dma16(rs, to_lds(img), voff); };
-  // The counted vmcnt waits assume this wave's DMAs and stores issue in program order around each
-  // DMA group: keep the compiler from moving memory ops (or anything) across these points.
-  auto order_fence = []() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // the NDMA DMAs of this wave: slots 4i + wave. Slots 0..12 stage block sqb of pair `so` into ring
-  // slot `sl` (i = 0 / 1 / 2: Q / dO / O rows 8 wave ..; i = 3: lse for wave 0), slots 16.. carry K/V
-  // pieces [kvc * KV_PER_IT, ...) of pair `ko` if kvon; the rest load nothing into `sink`
-  // No DMA here ever reads out of range: a fully out-of-range load may complete ahead of older
-  // loads, and then a counted vmcnt wait passes with an older DMA still in flight. Rows past N are
-  // clamped to row N-1 (their queries get lse = +inf -> P = 0, their keys P = 0 by mask), and DMA
-  // slots without work reload a valid piece into `sink`.
-  auto issue_group = [&](bool stv, PairOff so, int sqb, int sl, bool kvon, int kvc, PairOff ko) {
-    const int r0 = 32 * sqb;
-    char* slot = ring + sl * SLOT;
-    const int row = min(r0 + srl, N - 1) - srl;  // block row r0 (clamped so that r0 + srl < N)
-    const uint32_t rb = so.row + (uint32_t)row;
-    dma(rq, slot + 8 * wave * 128, rb * ldq + so.col + stq);
-    dma(rdo, slot + 4096 + 8 * wave * 128, rb * lddo + so.col + std_);
-    dma(ro, slot + 8192 + 8 * wave * 128, rb * ldoo + so.col + sto);
-    if (wave == 0) {  // lse[(b*H + h)*N + r0 ..] with so.row = b*N, so.col = h*128 (lanes 8.. repeat lane 7)
-      const uint32_t lo = (so.row * (uint32_t)H + (so.col >> 7) * (uint32_t)N + (uint32_t)r0) * 4 + (uint32_t)min(lane, 7) * 16;
-      dma(rl, slot + 12288, lo);
-    } else {
-      dma(rq, sink, (uint32_t)lane * 16 + 3 * 1024);
-    }
-    // (the sink reloads use distinct addresses: identical DMA calls would be merged by the compiler,
-    // and a group one instruction short breaks the counted waits)
-#pragma unroll
-    for (int i = 4; i < NDMA; ++i) {
-      const int k = kvc * KV_PER_IT + 4 * (i - 4) + wave;
-      const bool live = kvon && k < NKV;
-      const int which = k >= NP / 8, rr = (k - which * (NP / 8)) * 8;
-      const int kr = min(rr + l3, N - 1) - l3;  // clamped key rows
-      const uint32_t base = (ko.row + kr) * ldq + (uint32_t)(which + 1) * D * 2 + ko.col;
-      dma(rq, live ? (which ? vimg : kimg) + rr * 128 : sink, live ? base + ((rr & 8) ? kvo1 : kvo0) : (uint32_t)lane * 16 + i * 1024);
-    }
-  };
-  // lse*log2e and delta of the block in ring slot `sl` (local block qb) into table buffer `tb`
-  auto block_table = [&](int sl, int qb, int tb) {
-    const char* sb = ring + sl * SLOT;
-    const v8s dw = ds_read_b128(sb + 4096 + tbo);
-    const v8s ow = ds_read_b128(sb + 8192 + tbo);
-    const float d = oct_sum(dot8_bf16(dw, ow, 0.f));
-    if (l7 == 0) {
-      const float l = ((const float*)(sb + 12288))[tq];
-      // queries past N (rows clamped to N-1): lse = +inf makes their P exactly 0
-      s_tab[tb * 64 + tq] = 32 * qb + tq < N ? l * LOG2E : __builtin_huge_valf();
-      s_tab[tb * 64 + 32 + tq] = d;
-    }
-  };
-  // dQ^T fragments (dims 16 wave + 4g + r, queries 16a + li) of a block (local pqb of pair index ppair)
-  // from dS^T buffer `db`; with dbp, the block's in_proj bias-gradient partials (all stores of a
-  // block precede its DMA group)
-  auto phase2 = [&](int db, int pqb, PairOff po, int ppair, const v8s (&ktf)[NQ]) {
-    const char* img = dsb + db * DSB;
-    v4f acc0 = v4f{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    constexpr int H1 = (NQ + 1) / 2;  // two batches of key slices: fewer registers in flight
-    static_for<0, 2>([&](auto hc) {
-      constexpr int k0 = decltype(hc)::value ? H1 : 0, k1 = decltype(hc)::value ? NQ : H1;
-      v4s lo0[H1], hi0[H1], lo1[H1], hi1[H1];
-      static_for<k0, k1>([&](auto kc) {
-        constexpr int ks = decltype(kc)::value;
-        lo0[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2lo0);
-        hi0[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2hi0);
-        lo1[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2lo1);
-        hi1[ks - k0] = ds_read_tr_async_at<2048 * ks>(img + p2hi1);
-      });
-      lds_wait();
-#pragma unroll
-      for (int ks = k0; ks < k1; ++ks) {
-        acc0 = mfma16(ktf[ks], cat44(lo0[ks - k0], hi0[ks - k0]), acc0);
-        acc1 = mfma16(ktf[ks], cat44(lo1[ks - k0], hi1[ks - k0]), acc1);
-      }
-    });
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const v4f& acc = a ? acc1 : acc0;
-      const int q = pqb * 32 + 16 * a + li;
-      const uint32_t vo = q < N ? (po.row + q) * lddq + po.col + (uint32_t)(16 * wave + 4 * g) * 2 : OOR;
-      const v2u w = {pack2bf(acc[0] * scale, acc[1] * scale), pack2bf(acc[2] * scale, acc[3] * scale)};
-      __builtin_amdgcn_raw_buffer_store_b64(w, rdq, vo, 0, 0);
-    }
-    if (dbp) {
-      // q: column sums of this block's dQ (queries past N have dS = 0, so dQ = 0 exactly);
-      // v: wave 0's column sums of dO over the block's valid queries (vsb, from its phase 1b)
-      float* dst = dbp + ((int64_t)ppair * NQ + pqb) * 192;  // q | 0 (the second query half) | v
-      float cs[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[r] = row16_sum(acc0[r] + acc1[r]) * scale;
-      if (li == 0) *(float4*)(dst + 16 * wave + 4 * g) = make_float4(cs[0], cs[1], cs[2], cs[3]);
-      if (wave == 0) {
-        dst[64 + lane] = 0.f;
-        dst[128 + lane] = vsb[lane];
-      }
-    }
-  };
-
-  v8s kf[4][2], vf[4][2], ktf[NQ];
-  v4f dk[4][4], dv[4][4];  // [dims e][key fragment f]
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int f = 0; f < 4; ++f) dk[e][f] = dv[e][f] = v4f{0.f, 0.f, 0.f, 0.f};
-  };
-  // 32 stores per wave (dropped past N)
-  auto store_dkv = [&](PairOff po) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int key = kw0 + 16 * f + li;
-      const uint32_t vo = key < N ? (po.row + key) * lddq + po.col + (uint32_t)(4 * g) * 2 : OOR;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const v2u wk = {pack2bf(dk[e][f][0] * scale, dk[e][f][1] * scale), pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale)};
-        const v2u wv = {pack2bf(dv[e][f][0], dv[e][f][1]), pack2bf(dv[e][f][2], dv[e][f][3])};
-        __builtin_amdgcn_raw_buffer_store_b64(wk, rdq, vo + (uint32_t)(D + 16 * e) * 2, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(wv, rdq, vo + (uint32_t)(2 * D + 16 * e) * 2, 0, 0);
-      }
-    }
-  };
-  // this pair's K / V (S, dP B operands) and K^T (dQ A operand, dims 16 wave + li) fragments
-  auto load_kfrags = [&]() {
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        kf[f][ks] = frag_rows(kimg, KR, kw0 + 16 * f, ks, lane);
-        vf[f][ks] = frag_rows(vimg, KR, kw0 + 16 * f, ks, lane);
-      }
-    // K^T rows 32ks + 8g + q4 (+4), dims 16 wave + 4p4: the swizzle depends on 8g + q4 -> offsets 4096 ks
-    const int chunk = 2 * wave + (p4 >> 1);
-    const char* alo = kimg + lds_off(KR, 8 * g + q4, chunk) + 8 * (p4 & 1);
-    const char* ahi = kimg + lds_off(KR, 8 * g + q4 + 4, chunk) + 8 * (p4 & 1);
-    v4s klo[NQ], khi[NQ];
-    static_for<0, NQ>([&](auto kc) {
-      constexpr int ks = decltype(kc)::value;
-      klo[ks] = ds_read_tr_async_at<4096 * ks>(alo);
-      khi[ks] = ds_read_tr_async_at<4096 * ks>(ahi);
-    });
-    lds_wait();
-#pragma unroll
-    for (int ks = 0; ks < NQ; ++ks) ktf[ks] = cat44(klo[ks], khi[ks]);
-  };
-
-  // ---- prologue: image rows NP .. 255 (never staged) zeroed once, so key fragments past N compute
-  // on finite zeros; pair p0's K/V images; blocks 0, 1, 2; table of block 0
-  if constexpr (NP < KR) {
-    for (int i = threadIdx.x; i < 2 * (KR - NP) * 8; i += 256) {
-      const int r = NP + (i >> 3) % (KR - NP);
-      char* img = i < 8 * (KR - NP) ? kimg : vimg;
-      *(uint4*)(img + r * 128 + (i & 7) * 16) = make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
-  const PairOff none{0u, 0u};
-  PairOff cur = pair_off(p0);
-  for (int k = wave; k < NKV; k += 4) {
-    const int which = k >= NP / 8, rr = (k - which * (NP / 8)) * 8;
-    const int kr = min(rr + l3, N - 1) - l3;
-    const uint32_t base = (cur.row + kr) * ldq + (uint32_t)(which + 1) * D * 2 + cur.col;
-    dma(rq, (which ? vimg : kimg) + rr * 128, base + ((rr & 8) ? kvo1 : kvo0));
-  }
-  issue_group(true, cur, 0, 0, false, 0, none);
-  issue_group(true, cur, 1, 1, false, 0, none);
-  issue_group(true, cur, 2, 2, false, 0, none);
-  zero_acc();
-  PRO_WAIT<2 * NDMA>();  // K/V images and block 0 landed (blocks 1, 2 in flight)
-  block_table(0, 0, 0);
-  PRO_WAIT<NDMA>();      // block 1 landed; block 0's table visible
-
-  const int npr = p1 - p0;
-  PairOff prv = cur;
-  for (int pi = 0; pi < npr; ++pi) {
-    cur = pair_off(p0 + pi);
-    const bool has_next = pi + 1 < npr;
-    const PairOff nxt = has_next ? pair_off(p0 + pi + 1) : none;
-    const int t0 = pi * NQ;
-#pragma unroll 1
-    for (int qb = 0; qb < NQ; ++qb) {
-      const int t = t0 + qb;
-      // Blocks t, t+1 landed: the DMA groups up to t-2 are complete (group j stages block j+3) and
-      // only group t-1 may be in flight. Stores are always issued BEFORE a group, so the NDMA
-      // youngest vector-memory ops are that group's loads: loads complete in order, stores need not
-      // (gfx9 counts both in vmcnt), so a count that covered younger stores could pass early. Also:
-      // dS^T and table of block t visible; every wave past its reads of the reused buffers.
-      if (t > 0) PIPE_WAIT<NDMA>();
-      const int sl = t & (RING - 1);
-      const char* qimg = ring + sl * SLOT;
-      const char* doimg = qimg + 4096;
-      if (qb == 0) {
-        // phase 2 of the previous pair's last block BEFORE its K^T fragments are replaced (dropped
-        // stores at t = 0 keep the store count uniform)
-        if (pi > 0) phase2((t - 1) & 1, NQ - 1, prv, p0 + pi - 1, ktf);
-        order_fence();
-        load_kfrags();
-      }
-      // ---- phase 1a: Q / dO A fragments (query 16a + li, dims 32ks + 8g ..), reused by all four key
-      // fragments; this block's Q^T / dO^T transposed fragments for the dV / dK products
-      v8s qa[2][2], dA[2][2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const int fo = (ks ? fr1 : fr0) + 2048 * a;
-          qa[ks][a] = ds_read_b128(qimg + fo);
-          dA[ks][a] = ds_read_b128(doimg + fo);
-        }
-      // S[q][key], dP[q][key] of key fragments 0, 1 (lane holds [q = 16a + 4g + r][key = kw0 + 16f + li])
-      v4f s[2][2], dp[2][2];
-      auto sdp = [&](int f0) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int f = 0; f < 2; ++f) s[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int f = 0; f < 2; ++f) {
-              s[a][f] = mfma16(qa[ks][a], kf[f0 + f][ks], s[a][f]);
-              dp[a][f] = mfma16(dA[ks][a], vf[f0 + f][ks], dp[a][f]);
-            }
-      };
-      sdp(0);
-      // ---- pair end: the previous pair's dK / dV (its last block's products ran in iteration t-1)
-      order_fence();
-      if (qb == 0 && pi > 0) {
-        store_dkv(prv);
-        zero_acc();
-      }
-      // ---- phase 2 of block t-1 (same pair): its stores precede this iteration's DMA group
-      if (qb != 0) phase2((t - 1) & 1, qb - 1, cur, p0 + pi, ktf);
-      // ---- DMA: block t+3 and, in local blocks 1 .. NQ-2, slices of the next pair's K/V images
-      order_fence();
-      const bool kvon = qb >= 1 && qb <= NQ - 2 && has_next;
-      if (qb + 3 < NQ)
-        issue_group(true, cur, qb + 3, (t + 3) & (RING - 1), kvon, qb - 1, nxt);
-      else
-        issue_group(has_next, nxt, qb + 3 - NQ, (t + 3) & (RING - 1), kvon, qb - 1, nxt);
-      order_fence();
-      // ---- table of block t+1 (landed at this iteration's wait)
-      if (qb + 1 < NQ)
-        block_table((t + 1) & (RING - 1), qb + 1, (t + 1) & 1);
-      else if (has_next)
-        block_table((t + 1) & (RING - 1), 0, (t + 1) & 1);
-      // ---- phase 1b: P, dS; dS^T -> LDS; dV^T += dO^T P, dK^T += Q^T dS (key fragments in pairs)
-      const float* tl = s_tab + (t & 1) * 64 + 4 * g;
-      const v4f l40 = *(const v4f*)(tl), l41 = *(const v4f*)(tl + 16);
-      const v4f d40 = *(const v4f*)(tl + 32), d41 = *(const v4f*)(tl + 48);
-      char* img = dsb + (t & 1) * DSB;
-      v4s dlo[4], dhi[4], qlo[4], qhi[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        dlo[e] = ds_read_tr_async(doimg + trq[e]);
-        dhi[e] = ds_read_tr_async(doimg + trq[e] + 2048);
-        qlo[e] = ds_read_tr_async(qimg + trq[e]);
-        qhi[e] = ds_read_tr_async(qimg + trq[e] + 2048);
-      }
-      lds_wait();
-      auto softmax_grad = [&](int f0) {
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          const int fk = f0 + f;
-          const bool kin = kw0 + 16 * fk + li < N;
-#pragma unroll
-          for (int a = 0; a < 2; ++a) {
-            const v4f l4 = a ? l41 : l40, d4 = a ? d41 : d40;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float pv = kin ? __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l4[r])) : 0.f;
-              s[a][f][r] = pv;
-              dp[a][f][r] = pv * (dp[a][f][r] - d4[r]);
-            }
-            const v2u w = {pack2bf(dp[a][f][0], dp[a][f][1]), pack2bf(dp[a][f][2], dp[a][f][3])};
-            *(v2u*)(img + (a ? dsw1 : dsw0) + 1024 * fk) = w;
-          }
-          const v8s pf = pack_p(s[0][f], s[1][f]);
-          const v8s sf = pack_p(dp[0][f], dp[1][f]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            dv[e][fk] = mfma16(cat44(dlo[e], dhi[e]), pf, dv[e][fk]);
-            dk[e][fk] = mfma16(cat44(qlo[e], qhi[e]), sf, dk[e][fk]);
-          }
-        }
-      };
-      softmax_grad(0);
-      if (nf > 2) {  // key fragments 2, 3 (wave 3 at N = 197 holds no key there: zero dS^T rows instead)
-        sdp(2);
-        softmax_grad(2);
-      } else {
-#pragma unroll
-        for (int f = 2; f < 4; ++f)
-#pragma unroll
-          for (int a = 0; a < 2; ++a) *(v2u*)(img + (a ? dsw1 : dsw0) + 1024 * f) = v2u{0u, 0u};
-      }
-      if (dbp && wave == 0) {
-        // v-bias partial: dO^T . 1 over the block's queries < N (the dV^T product with P -> a 0/1 mask;
-        // the in_proj k bias gets no gradient: softmax rows are shift-invariant, so sum_k dS = 0)
-        v4f m0, m1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          m0[r] = 32 * qb + 4 * g + r < N ? 1.f : 0.f;
-          m1[r] = 32 * qb + 16 + 4 * g + r < N ? 1.f : 0.f;
-        }
-        const v8s ones = pack_p(m0, m1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const v4f cs = mfma16(cat44(dlo[e], dhi[e]), ones, v4f{0.f, 0.f, 0.f, 0.f});
-          if (li == 0) *(v4f*)(vsb + 16 * e + 4 * g) = cs;
-        }
-      }
-    }
-    prv = cur;
-  }
-  // last block's dQ and the last pair's dK / dV
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  phase2((npr * NQ - 1) & 1, NQ - 1, prv, p1 - 1, ktf);
-  store_dkv(prv);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-}
-
-// ------------------------------------------- backward, whole head, pipelined, two waves per SIMD
-// attn_bwd_pipe_kernel's algorithm (192 < N <= 224: NQ = 7 blocks) with 8 waves, two per SIMD: the
-// second wave on each SIMD hides the latency chains (exp -> pack -> MFMA, LDS reads, per-block waits)
-// that leave the one-wave-per-SIMD kernel's MFMA and VALU pipes idle. That needs <= 256 registers
+// The kernel: that algorithm (NQ = 7 blocks) with 8 waves, two per SIMD: the second wave on each
+// SIMD hides the latency chains (exp -> pack -> MFMA, LDS reads, per-block waits) that leave a
+// one-wave-per-SIMD form's MFMA and VALU pipes idle (measured faster in round 2). That needs <= 256 registers
 // per wave, so the persistent state shrinks: wave w owns keys [32w, 32w + 32) (two key fragments:
 // 64 accumulator registers), and the K image is double-buffered by pair so the K (S operand) and
 // K^T (dQ operand) fragments are read from LDS each block instead of being held; only V (dP
@@ -2068,15 +1309,6 @@ static int device_cus() {
   return n;
 }
 
-// PVR_ATTN_FWD_TILED=1 forces the tiled (online-softmax) forward everywhere (A/B switch)
-static bool fwd_tiled_forced() {
-  static const bool f = [] {
-    const char* e = getenv("PVR_ATTN_FWD_TILED");
-    return e && e[0] == '1';
-  }();
-  return f;
-}
-
 // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take up to
 // 128 KiB of LDS), ceil(N/16) waves
 template <int NF>
@@ -2100,7 +1332,7 @@ template <int DH>
 static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
                                   int D, float scale, hipStream_t s) {
   using namespace pvr;
-  if (DH == 64 && N <= 256 && !fwd_tiled_forced()) {
+  if (DH == 64 && N <= 256) {
     // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take
     // up to 128 KiB of LDS), ceil(N/16) waves
     switch ((N + 15) / 16) {
@@ -2144,19 +1376,10 @@ extern "C" int pvr_attn_bwd_waves(int N) {
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
 }
 
-// PVR_ATTN_BWD_TAIL=0: one launch over every key block (A/B of the body / tail launches below)
-static bool attn_bwd_tail_split() {
-  static const bool on = [] {
-    const char* e = getenv("PVR_ATTN_BWD_TAIL");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // N = (full key blocks) + 1 key: main kernel + last-key kernel, dQ written directly (no dq_acc)
 static bool attn_bwd_lastkey_path(int N, bool dbias) {
   const int KB = 32 * pvr_attn_bwd_waves(N);
-  return attn_bwd_tail_split() && (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && N <= 512;
+  return (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && N <= 512;
 }
 
 // 1 if pvr_attn_bwd needs the zero-initialised f32 dQ workspace for this shape
@@ -2164,132 +1387,6 @@ extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias) {
   if (dh == 64 && N <= 256) return 0;
   if (pvr_attn_bwd_key_blocks(N) <= 1) return 0;
   return attn_bwd_lastkey_path(N, dbias != 0) ? 0 : 1;
-}
-
-// PVR_ATTN_BWD_FUSED=1 forces the single-kernel (dS through LDS) backward everywhere (A/B switch)
-static bool bwd_fused_forced() {
-  static const bool f = [] {
-    const char* e = getenv("PVR_ATTN_BWD_FUSED");
-    return e && e[0] == '1';
-  }();
-  return f;
-}
-
-// Backward grids: one persistent workgroup per CU, like the forward. (PVR_ATTN_BWD_PPW=n deals
-// n pairs per workgroup instead; measured in-step at ViT-B/16 b256, beside the side-stream weight
-// GEMMs: 1 per CU 6996 img/s, n = 6 / 3 / 2 / 1: 6986 / 6954 / 6918 / 6851.)
-static int bwd_grid(int npairs) {
-  static const int ppw = [] {
-    const char* e = getenv("PVR_ATTN_BWD_PPW");
-    return e ? atoi(e) : 0;
-  }();
-  if (ppw > 0) return (npairs + ppw - 1) / ppw;
-  return npairs < device_cus() ? npairs : device_cus();
-}
-
-template <int NF>
-static hipError_t attn_bwd_dq_head_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                          int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, int npairs,
-                                          int N, int H, int D, float scale, hipStream_t s) {
-  using namespace pvr;
-  constexpr int SMEM = 2 * 2 * 32 * ((NF + 1) / 2) * 128;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_dq_head_kernel<NF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  const int grid = bwd_grid(npairs);
-  hipLaunchKernelGGL(attn_bwd_dq_head_kernel<NF>, dim3(grid), dim3(NF * 64), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, delta,
-                     dqkv, ld_dq, N, H, D, npairs, scale);
-  return hipGetLastError();
-}
-
-template <int NK, int KF>
-static hipError_t attn_bwd_dkv_head_launch(const uint16_t* qkv, int64_t ld, const uint16_t* dout, int64_t ld_do, const float* lse,
-                                           const float* delta, uint16_t* dqkv, int64_t ld_dq, int npairs, int N, int H, int D,
-                                           float scale, hipStream_t s) {
-  using namespace pvr;
-  constexpr int SMEM = 2 * (2 * 32 * ((NK * KF + 1) / 2) * 128 + 2048);
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_dkv_head_kernel<NK, KF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  const int grid = bwd_grid(npairs);
-  hipLaunchKernelGGL((attn_bwd_dkv_head_kernel<NK, KF>), dim3(grid), dim3(NK * 64), SMEM, s, qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq,
-                     N, H, D, npairs, scale);
-  return hipGetLastError();
-}
-
-// whole-head backward (dh 64, N <= 256): dQ + delta, then dK / dV
-static hipError_t attn_bwd_head(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout, int64_t ld_do,
-                                const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, int B, int N, int H, int D, float scale,
-                                hipStream_t s) {
-  const int npairs = B * H;
-  hipError_t e = hipErrorInvalidValue;
-  switch ((N + 15) / 16) {
-#define PVR_BWD_DQ(NF) \
-  case NF: e = attn_bwd_dq_head_launch<NF>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s); break;
-    PVR_BWD_DQ(1) PVR_BWD_DQ(2) PVR_BWD_DQ(3) PVR_BWD_DQ(4) PVR_BWD_DQ(5) PVR_BWD_DQ(6) PVR_BWD_DQ(7) PVR_BWD_DQ(8)
-    PVR_BWD_DQ(9) PVR_BWD_DQ(10) PVR_BWD_DQ(11) PVR_BWD_DQ(12) PVR_BWD_DQ(13) PVR_BWD_DQ(14) PVR_BWD_DQ(15) PVR_BWD_DQ(16)
-#undef PVR_BWD_DQ
-    default: break;
-  }
-  if (e != hipSuccess) return e;
-  static const int kf = [] {  // PVR_DKV_KF: 16-key fragments per dK/dV wave (2: 32 keys, 1: 16 keys)
-    const char* e = getenv("PVR_DKV_KF");
-    return e && atoi(e) == 1 ? 1 : 2;
-  }();
-  if (kf == 1) {
-    switch ((N + 15) / 16) {
-#define PVR_BWD_DKV1(NK) \
-  case NK: return attn_bwd_dkv_head_launch<NK, 1>(qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s);
-      PVR_BWD_DKV1(1) PVR_BWD_DKV1(2) PVR_BWD_DKV1(3) PVR_BWD_DKV1(4) PVR_BWD_DKV1(5) PVR_BWD_DKV1(6) PVR_BWD_DKV1(7)
-      PVR_BWD_DKV1(8) PVR_BWD_DKV1(9) PVR_BWD_DKV1(10) PVR_BWD_DKV1(11) PVR_BWD_DKV1(12) PVR_BWD_DKV1(13) PVR_BWD_DKV1(14)
-      PVR_BWD_DKV1(15) PVR_BWD_DKV1(16)
-#undef PVR_BWD_DKV1
-      default: break;
-    }
-    return hipErrorInvalidValue;
-  }
-  switch ((N + 31) / 32) {
-#define PVR_BWD_DKV(NK) \
-  case NK: return attn_bwd_dkv_head_launch<NK, 2>(qkv, ld, dout, ld_do, lse, delta, dqkv, ld_dq, npairs, N, H, D, scale, s);
-    PVR_BWD_DKV(1) PVR_BWD_DKV(2) PVR_BWD_DKV(3) PVR_BWD_DKV(4) PVR_BWD_DKV(5) PVR_BWD_DKV(6) PVR_BWD_DKV(7) PVR_BWD_DKV(8)
-#undef PVR_BWD_DKV
-    default: break;
-  }
-  return hipErrorInvalidValue;
-}
-
-// PVR_ATTN_BWD_PIPE=0: the two-kernel whole-head backward instead of the pipelined one (A/B switch)
-static bool bwd_pipe_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("PVR_ATTN_BWD_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-template <int NQ>
-static hipError_t attn_bwd_pipe_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                       int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dbp, int B, int N, int H,
-                                       int D, float scale, hipStream_t s) {
-  using namespace pvr;
-  constexpr int SMEM = 2 * 256 * 128 + 4 * (3 * 4096 + 1024) + 2 * 256 * 64 + 512 + 256 + 1024;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_pipe_kernel<NQ>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  const int npairs = B * H;
-  const int grid = npairs < device_cus() ? npairs : device_cus();
-  hipLaunchKernelGGL(attn_bwd_pipe_kernel<NQ>, dim3(grid), dim3(256), SMEM, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq, dbp, N,
-                     H, D, npairs, scale);
-  return hipGetLastError();
 }
 
 template <int NQ>
@@ -2311,45 +1408,22 @@ static hipError_t attn_bwd_pipe8_launch(const uint16_t* qkv, int64_t ld, const u
   return hipGetLastError();
 }
 
-// PVR_ATTN_BWD_WAVES=4: the one-wave-per-SIMD pipelined backward instead of the 8-wave one (A/B)
-static int bwd_pipe_waves() {
-  static const int w = [] {
-    const char* e = getenv("PVR_ATTN_BWD_WAVES");
-    return e && e[0] == '4' ? 4 : 8;
-  }();
-  return w;
-}
-
-// pipelined whole-head backward: dh 64, 192 < N <= 256
-static hipError_t attn_bwd_pipe(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout, int64_t ld_do,
-                                const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dbp, int B, int N, int H, int D, float scale,
-                                hipStream_t s) {
-  if (bwd_pipe_waves() == 8 && (N + 31) / 32 == 7)  // 192 < N <= 224 (the K double buffer fits LDS)
-    return attn_bwd_pipe8_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
-  switch ((N + 31) / 32) {
-    case 7: return attn_bwd_pipe_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
-    case 8: return attn_bwd_pipe_launch<8>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbp, B, N, H, D, scale, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// the pipelined backward serves this shape / these layouts (dh 64, 192 < N <= 256, 31-bit offsets)
+// the pipelined backward serves this shape / these layouts (dh 64, 192 < N <= 224: the K double
+// buffer fits LDS; 31-bit offsets)
 static bool attn_bwd_pipe_ok(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq) {
   const int64_t rows_all = (int64_t)B * N;
   const bool off31 = ((rows_all - 1) * std::max(std::max(ld, ld_do), std::max(ld_o, ld_dq)) + 3 * D) * 2 < (1ll << 31) &&
                      (int64_t)B * H * N * 4 < (1ll << 31);
-  return H > 0 && D == 64 * H && N > 192 && N <= 256 && off31 && !bwd_fused_forced() && bwd_pipe_enabled();
+  return H > 0 && D == 64 * H && N > 192 && N <= 224 && off31;
 }
 
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                  int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                  int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
   if (DH == 64 && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][128] partials
-    return attn_bwd_pipe(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
-  if (DH == 64 && N <= 256 && !dbias && delta && !bwd_fused_forced())
-    return attn_bwd_head(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, B, N, H, D, scale, s);
+    return attn_bwd_pipe8_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
@@ -2370,7 +1444,6 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
     hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout, ld_do, out,
                        ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1, dq_mode);
   };
-  const bool tail_split = attn_bwd_tail_split();
   const int rem = N % KB;
   if (attn_bwd_lastkey_path(N, dbias != nullptr)) {
     // one key past a full key block: the main kernel over keys [0, N - 1) writes dQ directly, the
@@ -2383,7 +1456,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
                        N, H, D, scale);
     return hipGetLastError();
   }
-  if (tail_split && nkb > 1 && rem >= 16 && rem <= 128 && !dbias) {
+  if (nkb > 1 && rem >= 16 && rem <= 128 && !dbias) {
     // N = a multiple of KB plus a short tail (ViT-L/16@384: 577 = 2 x 256 + 65): the KB-aligned body
     // in full-size workgroups, the tail in workgroups sized for it, instead of 8-wave workgroups with
     // 3 live waves holding a CU each (818 vs 862 us at B64 H16). A 1-key tail (257 = 256 + 1, the
@@ -2420,15 +1493,13 @@ extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, in
 // dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
 // every element is written), whose row sum is the in_proj bias gradient; on the pipelined path
 // (pvr_attn_bwd_uses_pipe) the per-block partials described there.
-// delta: optional f32 [B*H][N] workspace; with it, dh 64 and N <= 256 take the two-kernel
-// whole-head backward (which does not fuse the bias gradient: dbias forces the single kernel).
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                   int64_t ld_do, const float* lse, float* delta, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                   int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                    int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
   switch (D / H) {
 #define PVR_BWD_DH(DH) \
-  case DH: return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, delta, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale, s);
+  case DH: return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale, s);
     PVR_BWD_DH(64) PVR_BWD_DH(80) PVR_BWD_DH(96) PVR_BWD_DH(128)
 #undef PVR_BWD_DH
     default: return hipErrorInvalidValue;

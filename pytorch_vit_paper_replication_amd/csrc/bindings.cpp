@@ -62,7 +62,7 @@ int pvr_attn_dbias_splits(int, int);
 hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float*, const uint16_t*, int64_t, int, uint16_t*, int64_t,
                                hipStream_t);
 hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, int, hipStream_t);
-hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float, hipStream_t);
 }
 
 namespace {
@@ -628,16 +628,10 @@ void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor d
 // Persistent f32 dQ accumulator of the multi-key-block attention backward, one per (device, stream),
 // zero-initialised once: the backward converts the accumulated dQ and zeroes it again, so no
 // per-call zero fill (a 151 MB memset per layer at ViT-L/16 384 px). Deliberately never freed (a
-// static tensor's destructor would run after the HIP runtime's teardown). PVR_ATTN_DQ_WS=0: a fresh
-// zeroed tensor per call instead (A/B).
+// static tensor's destructor would run after the HIP runtime's teardown).
 // drop = true: forget the cached accumulator of this (device, stream) (after a failed backward, whose
 // partial sums it may still hold); the next call re-creates it with torch::zeros.
 torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts, bool drop = false) {
-  static const bool on = [] {
-    const char* e = getenv("PVR_ATTN_DQ_WS");
-    return !(e && e[0] == '0');
-  }();
-  if (!on) return torch::Tensor();
   static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
   const auto key = std::make_pair((int)opts.device().index(), stream());
   torch::Tensor*& t = cache[key];
@@ -665,7 +659,6 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
                        double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
-  auto delta = torch::empty_like(lse);  // rowsum(dO * O) workspace of the two-kernel backward
   torch::Tensor dq_acc;
   int dq_rezero = 0;
   const bool has_db = dbias.has_value() && dbias->defined();
@@ -696,7 +689,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
       dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
   const hipError_t err = pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"),
-                                      ld_of(dout, "dout"), f32(lse, "lse"), f32_mut(delta, "delta"), bf_mut(dqkv, "dqkv"),
+                                      ld_of(dout, "dout"), f32(lse, "lse"), bf_mut(dqkv, "dqkv"),
                                       ld_of(dqkv, "dqkv"), dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
                                       dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
                                       (float)scale, stream());
@@ -716,16 +709,6 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 }
 
 }  // namespace
-
-// A HIP stream restricted to the CUs whose bits are set in `words` (32 CUs per word): the
-// weight-gradient side stream can be confined to a CU partition (PVR_SIDE_CU_MASK, A/B knob).
-int64_t cu_mask_stream(std::vector<int64_t> words) {
-  std::vector<uint32_t> m(words.size());
-  for (size_t i = 0; i < words.size(); ++i) m[i] = (uint32_t)words[i];
-  hipStream_t st = nullptr;
-  check(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()), "hipExtStreamCreateWithCUMask");
-  return (int64_t)(intptr_t)st;
-}
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pvr_comm::register_comm(m);
@@ -752,7 +735,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("im2col", &im2col);
   m.def("cls_rows", &cls_rows);
   m.def("patch_bwd", &patch_bwd);
-  m.def("cu_mask_stream", &cu_mask_stream);
   m.def("xent", &xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"), py::arg("correct"), py::arg("grad_scale"),
         py::arg("mean") = py::none());
   m.def("grad_norm", &grad_norm);

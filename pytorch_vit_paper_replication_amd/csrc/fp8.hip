@@ -243,14 +243,10 @@ extern "C" hipError_t pvr_fp8_quant(const uint16_t* x, int64_t ldx, uint8_t* y, 
   using namespace pvr;
   if (rows <= 0 || cols <= 0) return hipSuccess;
   if (cols % 16) return hipErrorInvalidValue;
-  // PVR_FP8_QBLOCKS: grid cap. 512 (two blocks per CU) keeps enough loads in flight: 4.1 -> 5.0 TB/s
-  // at ViT-H/14 activation shapes, H/14 fp8 step 925 -> 938 img/s (profiles/fp8_quant_blocks_ab.log);
-  // more blocks add same-address amax atomics without more bandwidth
-  static const int cap = [] {
-    const char* e = getenv("PVR_FP8_QBLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 512;
-  }();
+  // grid cap 512 (two blocks per CU) keeps enough loads in flight: 4.1 -> 5.0 TB/s at ViT-H/14
+  // activation shapes, H/14 fp8 step 925 -> 938 img/s (profiles/fp8_quant_blocks_ab.log); more
+  // blocks add same-address amax atomics without more bandwidth
+  constexpr int cap = 512;
   int64_t blocks = (rows * (cols / 16) + 255) / 256;
   if (blocks > cap) blocks = cap;  // grid-stride over the tensor
   if (fmt == 0)

@@ -294,23 +294,13 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
-  static const int cap_env = [] {  // PVR_LN_BWD_BLOCKS: grid cap (A/B of row pipelining vs atomics per column)
-    const char* e = getenv("PVR_LN_BWD_BLOCKS");
-    return e ? atoi(e) : 0;
-  }();
-  // PVR_LN_BWD_W4 (A/B): 0 = 16-B chunks always; 1 = 4-column chunks where they tile the row exactly.
-  // ViT-B/16 b256 (profiles/r2s/ln_bwd_w4_ab.log): 79 -> 64 us per call (91 -> 79 with the linked
-  // dropout backward), step neutral-to-+0.3 %; forcing 4 waves/SIMD (<= 128 VGPRs) spilled 18 VGPRs and
-  // took 114 us.
-  static const int w4 = [] {
-    const char* e = getenv("PVR_LN_BWD_W4");
-    return e ? atoi(e) : 1;
-  }();
+  // 4-column chunks (D = 768, profiles/r2s/ln_bwd_w4_ab.log): 79 -> 64 us per call (91 -> 79 with the
+  // linked dropout backward); forcing 4 waves/SIMD (<= 128 VGPRs) spilled 18 VGPRs and took 114 us.
   // 4-column chunks when they tile the row over the 64 lanes exactly and 8-column ones do not
-  const bool use_w4 = w4 && (D / 4) % 64 == 0 && (D / 8) % 64 != 0 && D / 4 <= 64 * 5;
+  const bool use_w4 = (D / 4) % 64 == 0 && (D / 8) % 64 != 0 && D / 4 <= 64 * 5;
   // D = 768 on 4-column chunks (146 VGPRs, 3 blocks per CU): one grid of exactly the resident blocks,
   // so no block starts late; otherwise 1024
-  const int cap = cap_env > 0 ? cap_env : (use_w4 && D == 768 ? device_cus() * 3 : 1024);
+  const int cap = use_w4 && D == 768 ? device_cus() * 3 : 1024;
   int nblk = (rows + 3) / 4;
   // 1024 blocks (4 per CU, ~12 pipelined rows per wave): in-step 0.2 % ahead of 512 and 768
   // (profiles/ln_bwd_grid_step_ab_r2.log); 2048 was 22 % slower in isolation, its 2048 x 3 x D column

@@ -15,7 +15,6 @@ Reference semantics (models/vit.py):
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional
 
 import torch
@@ -25,18 +24,6 @@ from .. import _ext
 from . import gemm
 
 SITE_SHIFT = 32
-# in_proj bias gradient inside the attention backward: correct, but A/B-measured 0.35 ms/step slower than
-# the separate column-sum kernel on ViT-B/16 b256, so opt-in
-_FUSE_QKV_DBIAS = os.environ.get("PVR_ATTN_DBIAS", "0") == "1"
-# in_proj bias gradient from the pipelined attention backward's partial sums (PVR_PIPE_QKV_DB=0: column-sum pass, A/B)
-_PIPE_QKV_DB = os.environ.get("PVR_PIPE_QKV_DB", "1") == "1"
-# in_proj bias gradient on the weight-gradient side stream (PVR_SIDE_QKV_DB=0: on the dgrad chain, A/B)
-_SIDE_QKV_DB = os.environ.get("PVR_SIDE_QKV_DB", "1") == "1"
-# fc1 bias gradient as a side-stream column sum instead of inside the dGELU GEMM epilogue (A/B)
-_SIDE_B1_DB = os.environ.get("PVR_SIDE_B1_DB", "0") == "1"
-# queue each weight gradient on the side stream as soon as its operands exist (W2 before the fc2
-# dgrad, Wo before the attention backward) instead of in two batches behind later dgrad kernels
-EARLY_WGRAD = os.environ.get("PVR_EARLY_WGRAD", "0") == "1"  # A/B: slower (profiles/early_wgrad_ab.log)
 
 
 # Test hook: called as DGRAD_TAP(which, output) after every encoder-block dgrad GEMM (which = 0 fc2,
@@ -113,48 +100,10 @@ class BlockLink:
         self.drop2, self.b2, self.dz2, self.done = drop2, b2, None, False
 
 
-# PVR_BLOCK_LINK=0: every block computes its own fc2 dropout backward / bias gradient (A/B switch)
-BLOCK_LINK = os.environ.get("PVR_BLOCK_LINK", "1") == "1"
-
-
 def block_links(blocks, drops2):
     """(own link, previous block's link) per block, for EncoderBlockFn's ``links`` argument."""
-    if not BLOCK_LINK:
-        return [None] * len(blocks)
     own = [BlockLink(d, blk.mlp_block.mlp[3].bias) for blk, d in zip(blocks, drops2)]
     return [(own[i], own[i - 1] if i else None) for i in range(len(own))]
-
-
-# Two-stream micro-batching of the encoder blocks (opt-in, PVR_MICRO=2): each block's batch is split
-# into two halves whose kernel chains run on two compute streams, so one half's memory-bound kernels
-# (LayerNorm, attention, column sums) and last-wave GEMM tiles can overlap the other half's GEMMs.
-# Every kernel of the block is row-parallel (or per (image, head)), so a half is a contiguous row range
-# of the same [B*N, D] buffers; weight gradients of both halves accumulate on the one side stream.
-# Measured on one MI355X (scripts/gpu_micro.sh): ViT-B/16 b256 6730 img/s split vs 7060 unsplit (two
-# concurrent half-size GEMM chains interfere more than they fill each other's idle CUs), b512 7409 vs
-# ~7400 — so it stays off by default. Numerics: identical logits, gradients within summation order.
-MICRO = int(os.environ.get("PVR_MICRO", "1"))
-MICRO_MIN_IMAGES = int(os.environ.get("PVR_MICRO_MIN", "32"))  # per half
-_HALF_SEED_SHIFT = 48  # half h > 0 draws its dropout masks from seed offset + (h << 48)
-
-
-def _half_drop(drop, h: int):
-    if drop is None or h == 0:
-        return drop
-    return (drop[0], drop[1] + (h << _HALF_SEED_SHIFT), drop[2])
-
-
-def _use_micro(x: torch.Tensor, B: int, f8) -> bool:
-    return MICRO > 1 and f8 is None and x.is_cuda and B >= 2 * MICRO_MIN_IMAGES
-
-
-def _micro_stream(store, main: torch.cuda.Stream) -> torch.cuda.Stream:
-    """Second compute stream, created once per store at the caller's stream priority."""
-    s = getattr(store, "_micro_stream", None)
-    if s is None or s.priority != main.priority or s.device != main.device:
-        s = torch.cuda.Stream(device=main.device, priority=main.priority)
-        store._micro_stream = s
-    return s
 
 
 class EncoderBlockFn(torch.autograd.Function):
@@ -166,9 +115,6 @@ class EncoderBlockFn(torch.autograd.Function):
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
         T, D = x.shape
         ctx.links = links if links is not None else (None, None)
-        if _use_micro(x, B, f8):
-            return EncoderBlockFn._forward_micro(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, params)
-        ctx.halves = None
         # fp8 dgrad GEMMs (e5m2 gradients x e4m3 W^T) only if the model asked for them:
         # ViT.enable_fp8(dgrad=True), the default (+5 % ViT-H/14, profiles/fp8_dgrad_ab.log)
         ctx.f8d = f8 if f8 is not None and f8[0].dgrad else None
@@ -213,45 +159,7 @@ class EncoderBlockFn(torch.autograd.Function):
         return x2
 
     @staticmethod
-    def _forward_micro(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, params):
-        ext = _ext.ext()
-        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
-        T, D = x.shape
-        M = w1.shape[0]
-        scale = 1.0 / math.sqrt(D // H)
-        main = torch.cuda.current_stream(x.device)
-        side = _micro_stream(store, main)
-        side.wait_stream(main)
-        x2 = torch.empty_like(x)
-        b_half = (B + 1) // 2
-        halves = []
-        for hi, (b0, nb) in enumerate(((0, b_half), (b_half, B - b_half))):
-            r0, r1 = b0 * N, (b0 + nb) * N
-            Th = r1 - r0
-            d1, d2 = _half_drop(drop1, hi), _half_drop(drop2, hi)
-            with torch.cuda.stream(main if hi == 0 else side):
-                xh = x[r0:r1]
-                u = torch.empty(Th, M, dtype=torch.bfloat16, device=x.device)
-                xn1, mean1, rstd1 = ext.layernorm_fwd(xh, ln1w, ln1b, eps1, Th, D)
-                qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
-                o, lse = ext.attn_fwd(qkv, nb, N, H, scale)
-                x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=xh)
-                xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, Th, D)
-                h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, drop=d1)
-                gemm.linear_fwd(h, store.bf16(w2), b2, resid=x1, drop=d2, out=x2[r0:r1])
-            halves.append((r0, r1, nb, d2, (xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)))
-        x.record_stream(side)
-        x2.record_stream(side)
-        main.wait_stream(side)
-        ctx.save_for_backward(x)
-        ctx.halves = halves
-        ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
-        return x2
-
-    @staticmethod
     def backward(ctx, dx2):
-        if ctx.halves is not None:
-            return EncoderBlockFn._backward_micro(ctx, dx2)
         ext = _ext.ext()
         x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = ctx.saved_tensors
         B, N, H, scale, store, drop1, drop2, params = ctx.meta
@@ -298,17 +206,11 @@ class EncoderBlockFn(torch.autograd.Function):
                 gemm.bias_grad(dx2, g(b2))
         # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
         gb1 = g(b1)
-        side_b1 = _SIDE_B1_DB and gb1 is not None
         gw2, gw1 = g(w2), g(w1)
-        early = EARLY_WGRAD
-        if early and gw2 is not None:  # dW2 = dz2^T h needs nothing from this block's dgrads
-            store.on_side(lambda: wgrad(dz2, h, gw2, 0, 3), dz2, h)
-        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=None if side_b1 else gb1)
+        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=gb1)
 
         def mlp_wgrads():
-            if side_b1:
-                gemm.bias_grad(du, gb1)
-            if gw2 is not None and not early:
+            if gw2 is not None:
                 wgrad(dz2, h, gw2, 0, 3)
             if gw1 is not None:
                 wgrad(du, xn2, gw1, 1, 2)
@@ -321,26 +223,20 @@ class EncoderBlockFn(torch.autograd.Function):
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
         gwo, gwqkv = g(wo), g(wqkv)
-        if early and gwo is not None:  # dWo = dx1^T o: ready as soon as dx1 is
-            store.on_side(lambda: wgrad(dx1, o, gwo, 2, 1), dx1, o)
         do = dgrad(dx1, wo, 2)
-        # in_proj bias gradient (column sums of dQ | dK | dV) reduced inside the attention backward
         gbqkv = g(bqkv)
         side_db = False
         db_part = None
-        if gbqkv is not None and _PIPE_QKV_DB and ext.attn_bwd_pipe_path(B, N, H, D):
+        if gbqkv is not None and ext.attn_bwd_pipe_path(B, N, H, D):
             # the pipelined attention backward emits per-(image, head, query block) column sums of dQ and
             # dO (= the v-bias gradient; the k bias has none); only their small reduction remains (side
             # stream), no pass over dQKV
             db_part = torch.empty(B * H, (N + 31) // 32, 192, dtype=torch.float32, device=do.device)
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part)
-        elif _FUSE_QKV_DBIAS:
-            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None if gbqkv is None else gbqkv.view(-1))
         else:
+            # other shapes: the in_proj bias gradient is a column sum of dQKV on the side stream
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
-            side_db = gbqkv is not None and _SIDE_QKV_DB
-            if gbqkv is not None and not _SIDE_QKV_DB:
-                gemm.bias_grad(dqkv, gbqkv)
+            side_db = gbqkv is not None
 
         def attn_wgrads():
             # the in_proj bias gradient (a memory-bound column sum, consumed only by the optimizer)
@@ -349,7 +245,7 @@ class EncoderBlockFn(torch.autograd.Function):
                 ext.attn_dbias_reduce(db_part, B, H, gbqkv.view(-1))
             if side_db:
                 gemm.bias_grad(dqkv, gbqkv)
-            if gwo is not None and not early:
+            if gwo is not None:
                 wgrad(dx1, o, gwo, 2, 1)
             if gwqkv is not None:
                 wgrad(dqkv, xn1, gwqkv, 3, 0)
@@ -367,89 +263,6 @@ class EncoderBlockFn(torch.autograd.Function):
         else:
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])
-        return (dx,) + (None,) * (10 + len(params))
-
-    @staticmethod
-    def _backward_micro(ctx, dx2):
-        ext = _ext.ext()
-        (x,) = ctx.saved_tensors
-        B, N, H, scale, store, drop1, drop2, params = ctx.meta
-        ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
-        g = store.grad_dest
-        dx2 = dx2.contiguous()
-        T, D = dx2.shape
-        own, prev = ctx.links
-        main = torch.cuda.current_stream(dx2.device)
-        side = _micro_stream(store, main)
-        # gradient destinations resolved once, before either stream touches them
-        gb2, gb1, gw2, gw1 = g(b2), g(b1), g(w2), g(w1)
-        gln2w, gln2b, gbo, gwo, gbqkv, gwqkv = g(ln2w), g(ln2b), g(bo), g(wo), g(bqkv), g(wqkv)
-        gln1w, gln1b = g(ln1w), g(ln1b)
-        gprev_b2 = g(prev.b2) if prev is not None else None
-        linked = own is not None and own.done
-        if linked:
-            dz2_full = own.dz2 if own.dz2 is not None else dx2
-            own.dz2 = None
-        elif drop2 is not None:
-            dz2_full = torch.empty_like(dx2)
-        else:
-            dz2_full = dx2
-        dx1 = torch.empty_like(dx2)
-        dx = torch.empty_like(dx2)
-        prev_drop = prev.drop2 if prev is not None else None
-        dzp = torch.empty_like(dx2) if prev_drop is not None else None
-        side.wait_stream(main)
-        w2b, w2t, w1b, w1t = store.bf16(w2), store.bf16_t(w2), store.bf16(w1), store.bf16_t(w1)
-        wob, wot, wqb, wqt = store.bf16(wo), store.bf16_t(wo), store.bf16(wqkv), store.bf16_t(wqkv)
-        for hi, (r0, r1, nb, d2, saved) in enumerate(ctx.halves):
-            xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = saved
-            Th = r1 - r0
-            with torch.cuda.stream(main if hi == 0 else side):
-                dx2h, dz2 = dx2[r0:r1], dz2_full[r0:r1]
-                if not linked:
-                    if drop2 is not None:
-                        gemm.bias_grad(dx2h, gb2, drop=d2, dz=dz2)
-                    elif gb2 is not None:
-                        gemm.bias_grad(dx2h, gb2)
-                du = gemm.linear_dgrad(dz2, w2b, dgelu_aux=u, wt=w2t, colsum=gb1)
-
-                def mlp_wgrads(dz2=dz2, h=h, du=du, xn2=xn2):
-                    if gw2 is not None:
-                        gemm.linear_wgrad(dz2, h, gw2)
-                    if gw1 is not None:
-                        gemm.linear_wgrad(du, xn2, gw1)
-
-                store.on_side(mlp_wgrads, dz2, h, du, xn2)
-                dxn2 = gemm.linear_dgrad(du, w1b, wt=w1t)
-                dx1h = dx1[r0:r1]
-                ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2h, D, dx1h, D, gln2w, gln2b, Th, dsum=gbo)
-                do = gemm.linear_dgrad(dx1h, wob, wt=wot)
-                dqkv = ext.attn_bwd(do, qkv, o, lse, nb, N, H, scale)
-                if gbqkv is not None:
-                    gemm.bias_grad(dqkv, gbqkv)
-
-                def attn_wgrads(dx1h=dx1h, o=o, dqkv=dqkv, xn1=xn1):
-                    if gwo is not None:
-                        gemm.linear_wgrad(dx1h, o, gwo)
-                    if gwqkv is not None:
-                        gemm.linear_wgrad(dqkv, xn1, gwqkv)
-
-                store.on_side(attn_wgrads, dx1h, o, dqkv, xn1)
-                dxn1 = gemm.linear_dgrad(dqkv, wqb, wt=wqt)
-                if prev is not None:
-                    seed, soff, p = gemm._drop_args(_half_drop(prev_drop, hi))
-                    ext.layernorm_bwd(dxn1, D, x[r0:r1], D, mean1, rstd1, ln1w, dx1h, D, dx[r0:r1], D, gln1w, gln1b, Th,
-                                      dsum=gprev_b2, dz=None if dzp is None else dzp[r0:r1], seed=seed,
-                                      seed_offset=soff, drop_p=p)
-                else:
-                    ext.layernorm_bwd(dxn1, D, x[r0:r1], D, mean1, rstd1, ln1w, dx1h, D, dx[r0:r1], D, gln1w, gln1b, Th)
-        for t in (dx2, dz2_full, dx1, dx, x) + ((dzp,) if dzp is not None else ()):
-            t.record_stream(side)
-        main.wait_stream(side)
-        if prev is not None:
-            prev.dz2, prev.done = dzp, True
-        ctx.halves = None
-        store.grad_ready([w2, b2, w1, b1, ln2w, ln2b, bo, wo, bqkv, wqkv, ln1w, ln1b])
         return (dx,) + (None,) * (10 + len(params))
 
 

@@ -8,7 +8,6 @@ copies of activations or weights anywhere.
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -17,9 +16,8 @@ from .. import _ext
 
 EPI_BF16, EPI_GELU, EPI_DGELU, EPI_F32_ATOMIC, EPI_F32_STORE = range(5)
 
-# tile configs: 0 = 128x128 (4 waves), 1 = 256x128 (8 waves), 2 = 128x256 (8 waves)
-_FORCE_TILE = os.environ.get("PVR_GEMM_TILE")
-_PERSISTENT = os.environ.get("PVR_PERSISTENT_GEMM", "0") == "1"  # persistent ping-pong for every fwd / dgrad GEMM
+# tile configs (csrc/gemm.hip): 0 = 128x128 (4 waves), 6 = 256x256 BK=32 ring, 12 = 256x256 8-wave
+# ping-pong, 13 = its persistent form, 14 = ping-pong with split-K f32 partial stores
 
 
 def _n_cus() -> int:
@@ -30,8 +28,8 @@ def _n_cus() -> int:
 
 
 _N_CUS = None
-# A/B: bf16 epilogues of the ping-pong GEMM staged through LDS (1) instead of register-direct (0)
-_EPI_STAGED = int(os.environ.get("PVR_EPI_STAGED", "0"))
+# test hook (tests/kernel_checks.py): force one tile config for every GEMM while set
+FORCE_TILE: Optional[int] = None
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
@@ -42,8 +40,8 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
     are at least four output tiles per CU, one tile per workgroup (12) otherwise (K % 64 != 0: the
     4-stage BK=32 ring, 6); token-reduced wgrad (both operands mn-contiguous, split-K) -> the same
     ping-pong with transposed LDS reads when the token count is large, 128x128 (0) otherwise."""
-    if _FORCE_TILE is not None:
-        return int(_FORCE_TILE)
+    if FORCE_TILE is not None:
+        return int(FORCE_TILE)
     if kind in ("fwd", "dgrad_t") and M >= 2048 and N >= 256:
         if K % 64:
             return 6
@@ -56,7 +54,7 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
         # the next tile's first K-tile (qkv fwd 0.171-0.179 vs 0.183-0.185 ms, fc1 GELU fwd 0.347-0.352
         # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log). The dGELU
         # dgrad (column-sum exchange at every tile end) stays on 12: 0.300 vs 0.325 ms (profiles/r3/gemm_ab.log)
-        if K >= 128 and not dgelu and (_PERSISTENT or math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus()):
+        if K >= 128 and not dgelu and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
             return 13
         return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
@@ -64,17 +62,12 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
     return 0
 
 
-# Small-M forward GEMMs (serving-size batches) split K when the 256x256 output tiles cannot fill the
-# chip: PVR_SMALL_SPLITK=0 keeps them on one tile per workgroup (A/B)
-_SMALL_SPLITK = os.environ.get("PVR_SMALL_SPLITK", "1") == "1"
-
-
 def _small_splitk(T: int, N: int, K: int) -> int:
     """K splits for a forward GEMM on 256x256 tiles (T >= 2048) with fewer than 128 output tiles
     (0: do not split). Each split keeps at least two 64-deep K-tiles; the splits aim at ~256
     workgroups. Measured (profiles/r2s/small_splitk_ab.log): eval forward at batch 32 +5 %; below
     2048 rows the 128x128 one-pass tiles are faster (batch 1: 1.32 ms unsplit vs 1.89 split)."""
-    if not _SMALL_SPLITK or K % 128 or N % 4 or T < 2048:
+    if K % 128 or N % 4 or T < 2048:
         return 0
     tiles = math.ceil(T / 256) * math.ceil(N / 256)
     if tiles >= 128:
@@ -84,7 +77,7 @@ def _small_splitk(T: int, N: int, K: int) -> int:
 
 
 def _gemm(*args, tile: int, colsum=None):
-    _ext.ext().gemm(*args, tile, colsum=colsum, epi_staged=_EPI_STAGED)
+    _ext.ext().gemm(*args, tile, colsum=colsum)
 
 
 def _drop_args(drop: Drop):
@@ -148,9 +141,9 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
     return out
 
 
-# workgroups a 256x256 weight-gradient GEMM is split into (one resident workgroup per CU): the
-# side stream's share of the 256 CUs while the dgrad chain runs beside it (PVR_WGRAD_WGS)
-_WGRAD_WGS = int(os.environ.get("PVR_WGRAD_WGS", "256"))
+# workgroups a 256x256 weight-gradient GEMM is split into: one resident workgroup per CU (measured
+# best beside the dgrad chain, scripts/gpu_wgs_ab.sh in round 2)
+_WGRAD_WGS = 256
 
 
 def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
@@ -167,7 +160,6 @@ def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
     return s
 
 
-_SPLITK_REDUCE = os.environ.get("PVR_WGRAD_REDUCE", "1") == "1"
 _workspaces = {}  # (device index, stream id) -> flat f32 split-K workspace
 
 
@@ -197,7 +189,7 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.
     ksplit = math.ceil(math.ceil(T / splits) / 64) * 64
     ext = _ext.ext()
     nsplit = math.ceil(T / ksplit)
-    if tile == 12 and _SPLITK_REDUCE and nsplit > 1 and out.is_contiguous() and N % 4 == 0:
+    if tile == 12 and nsplit > 1 and out.is_contiguous() and N % 4 == 0:
         ws = _workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
         ext.gemm(dy, False, x, False, ws, N, K, T, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0,
                  None, 0, 0.0, ksplit, 14)

@@ -21,8 +21,6 @@ import torch
 
 from .. import _ext
 
-# Adam writes the transposed bf16 weight shadow itself (PVR_FUSED_WT=0: separate transpose pass, A/B)
-_FUSED_WT = __import__("os").environ.get("PVR_FUSED_WT", "1") == "1"
 
 
 def _store_of(params):
@@ -249,7 +247,7 @@ class FusedAdam(torch.optim.Optimizer):
                 _ext.ext().grad_norm(store.grad_flat, 0.0, ws, clip)  # max_norm 0 -> coef 1, flag only
                 use_clip = True
             table = self._group_table(step, store.device)
-            tt = self._transposed_tables(store) if _FUSED_WT else None
+            tt = self._transposed_tables(store)  # Adam also writes the bf16 W^T shadow when it can
             if tt is not None and tt[3] > 0:
                 # master, m, v, bf16 shadow and the dgrad GEMMs' W^T shadow in one pass
                 store.ensure_transposed()  # only if something else changed the weights since

@@ -18,17 +18,31 @@ Design, MI355X-first rather than a copy of torch 
 
 Transport (``comm``): ``"torch"`` (the default, ``"auto"``) all-reduces each bucket with
 ``torch.distributed`` (ProcessGroupNCCL = RCCL on ROCm, its own HIP stream, ``ReduceOp.AVG``), joined
-into the compute stream by ``work.wait()`` — no host synchronisation. ``"native"`` (or
-``PVR_COMM=native``) uses the framework's C++ RCCL communicator (``parallel/comm.py`` ->
-``csrc/comm.cpp``) on its own high-priority stream, event-gated the same way. Measured at ViT-B/16
-b512 on one MI355X (world 1, scripts/gpu_ddp_ab2.sh): torch 7410 img/s, native 6934-6970, no DDP
-7444 — the native transport slows the whole step by ~6 %, so it is opt-in. gloo/CPU always uses
-``torch.distributed``.
+into the compute stream by ``work.wait()`` — no host synchronisation. ``"native"`` uses the
+framework's C++ RCCL communicator (``parallel/comm.py`` -> ``csrc/comm.cpp``) on its own stream,
+event-gated the same way; ``"native-mesh"`` runs that communicator's own reduce-scatter + all-gather
+schedule (``csrc/comm_core.h``: grouped point-to-point transfers to every peer at once, fp32). gloo /
+CPU always uses ``torch.distributed``. World-1 A/B at ViT-B/16 b512 (profiles/r3/ddp_transport_world1_b512.log):
+no DDP 8082 / 8075 img/s, torch 8053, torch with the bf16 wire 8034 — RCCL's one-rank kernel
+(``oneRankReduce``, ~0.2 ms per bucket) hides under the backward. The native transport's stream was
+high-priority there (7411 img/s): RCCL's kernels then pre-empted the overlapped GEMMs; it now runs
+at normal priority.
+
+Wire format (``comm_dtype``): fp32 by default. ``torch.bfloat16`` keeps a persistent bf16 mirror of
+the gradient buffer (no per-step allocation): each bucket is cast into its slice, all-reduced in
+bf16 (half the bytes on xGMI) and cast back. At 8 GPUs the fp32 gradients of ViT-B/16 (330 MB per
+step) need ~2 ms of ring time against a ~60 ms backward at 512 images per GPU, fully hidden, so the
+bf16 wire buys no step time there and costs two cast passes plus bf16 rounding of every gradient
+(rel-L2 < 1e-2, tests/test_ddp_cpu.py): it is opt-in, for bandwidth-bound (multi-node, small-batch)
+runs.
+
+Bucket padding (``pad_buckets``, default on): every bucket is a whole number of world x 7 x 4 KiB
+blocks — the flat store lays the buckets out on those boundaries with zero padding,
+so a reduce-scatter splits each bucket into equal per-rank chunks of whole 4 KiB pages per xGMI link.
 """
 from __future__ import annotations
 
 import contextlib
-import os
 import time
 import warnings
 from typing import Dict, List, Optional
@@ -68,9 +82,9 @@ class DistributedDataParallel(nn.Module):
         self._comm_mode = comm
         self._native = None          # parallel.comm.NativeCommunicator when the native transport is used
         self._comm_buf: Optional[torch.Tensor] = None  # persistent low-precision gradient mirror
-        # native transport's all-reduce schedule: "rccl" (RCCL's algorithm) or "mesh" (PVR_COMM_ALGO=mesh:
+        # native transport's all-reduce schedule: "rccl" (RCCL's algorithm) or "mesh" (comm="native-mesh":
         # csrc/comm_core.h grouped point-to-point reduce-scatter + all-gather over every xGMI link)
-        self._algo = os.environ.get("PVR_COMM_ALGO", "rccl")
+        self._algo = "mesh" if comm == "native-mesh" else "rccl"
         # per-bucket all-reduce timing (utils.metrics.StepLogger): (bytes, start, end) per launched
         # bucket, start = bucket ready on the compute stream, end = collective complete (HIP events
         # on GPU, host clock with gloo)
@@ -79,15 +93,15 @@ class DistributedDataParallel(nn.Module):
         self._timing_stream: Optional[torch.cuda.Stream] = None
 
     def _pick_transport(self, device):
-        mode = os.environ.get("PVR_COMM", self._comm_mode)
-        if mode != "native" or device.type != "cuda" or not self._avg:
+        mode = self._comm_mode
+        if mode not in ("native", "native-mesh") or device.type != "cuda" or not self._avg:
             return None
         from .comm import NativeCommunicator
 
         try:
             return NativeCommunicator.create(device, self.process_group)
         except Exception as e:  # pragma: no cover - only on GPU boxes
-            if mode == "native":
+            if mode.startswith("native"):
                 raise
             warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed collectives")
             return None

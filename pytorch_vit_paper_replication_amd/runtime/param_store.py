@@ -16,7 +16,6 @@ bucketer) as soon as a group of parameters has its final gradient.
 """
 from __future__ import annotations
 
-import os
 import weakref
 from typing import Callable, Dict, Iterable, List, Optional
 
@@ -25,6 +24,9 @@ import torch
 from .. import _ext
 
 ALIGN = 64  # elements; keeps every parameter 256-B aligned and 4-element vectorisable
+# weight-gradient GEMMs on a second stream (module attribute, not an env knob: the side-stream
+# ordering test switches it off to compare against the serial schedule)
+SIDE_WGRAD = True
 
 
 def _norm_device(device) -> torch.device:
@@ -268,15 +270,10 @@ class ParamStore:
     # stream after it has caught up with main; an end-of-backward autograd callback joins the side
     # stream back into the caller's stream, so anything after backward() sees complete gradients.
     def side_stream(self) -> Optional[torch.cuda.Stream]:
-        if self.device.type != "cuda" or os.environ.get("PVR_SIDE_WGRAD", "1") == "0":
+        if self.device.type != "cuda" or not SIDE_WGRAD:
             return None
         if self._side is None:
-            spec = os.environ.get("PVR_SIDE_CU_MASK")
-            if spec:
-                handle = _ext.ext().cu_mask_stream(cu_mask_words(spec, torch.cuda.get_device_properties(self.device).multi_processor_count))
-                self._side = torch.cuda.ExternalStream(handle, device=self.device)
-            else:
-                self._side = torch.cuda.Stream(device=self.device)
+            self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
     def on_side(self, fn: Callable[[], None], *tensors: torch.Tensor) -> None:
@@ -343,26 +340,6 @@ class ParamStore:
                 return
             for fn in self._listeners:
                 fn(ps)
-
-
-def cu_mask_words(spec: str, n_cu: int) -> List[int]:
-    """CU-mask words for a spec: comma-separated ``lo-hi`` CU ranges, or ``mod:M:r1+r2`` (CUs whose
-    index mod M is one of the r's)."""
-    sel = set()
-    for part in spec.split(","):
-        part = part.strip()
-        if part.startswith("mod:"):
-            _, m, rs = part.split(":")
-            keep = {int(r) for r in rs.split("+")}
-            sel |= {c for c in range(n_cu) if c % int(m) in keep}
-        elif part:
-            lo, _, hi = part.partition("-")
-            sel |= set(range(int(lo), int(hi or lo) + 1))
-    words = [0] * ((n_cu + 31) // 32)
-    for c in sel:
-        if 0 <= c < n_cu:
-            words[c // 32] |= 1 << (c % 32)
-    return words
 
 
 def lookup_store(p: torch.nn.Parameter) -> Optional[ParamStore]:

@@ -34,5 +34,5 @@ def timed(fn, reps=10):
 f = 4.0 * B * H * N * N * dh
 tf = timed(lambda: ext.attn_fwd(qkv, B, N, H, scale))
 tb = timed(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, scale))
-print(f"B{B} N{N} H{H} dh{dh} [{os.environ.get('PVR_ATTN_BWD_TAIL', '1')}]: fwd {tf:7.1f} us ({f / tf / 1e6:5.1f} TF)  "
+print(f"B{B} N{N} H{H} dh{dh}: fwd {tf:7.1f} us ({f / tf / 1e6:5.1f} TF)  "
       f"bwd {tb:7.1f} us ({2.5 * f / tb / 1e6:5.1f} TF)", flush=True)

@@ -59,14 +59,14 @@ def main():
             t_lib = timeit(lambda: torch.matmul(x, w.t()))
             print(f"fwd   {name:4s} T{T} N{n} K{k}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
             for t in tiles:
-                G._FORCE_TILE = str(t)
+                G.FORCE_TILE = t
                 tt = timeit(lambda: G.linear_fwd(x, w, b))
                 print(f"fwd   {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
             t_lib = timeit(lambda: torch.matmul(dy, w))
             print(f"dgrad {name:4s} T{T} N{k} K{n}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
             wt = w.t().contiguous()
             for t in tiles:
-                G._FORCE_TILE = str(t)
+                G.FORCE_TILE = t
                 tt = timeit(lambda: G.linear_dgrad(dy, w, wt=wt))
                 print(f"dgrad {name:4s} tile{t}   ours(wT) {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
                 tt = timeit(lambda: G.linear_dgrad(dy, w, tile=t))
@@ -75,10 +75,10 @@ def main():
             t_lib = timeit(lambda: torch.matmul(dy.t(), x))
             print(f"wgrad {name:4s} N{n} K{k} T{T}  hipblaslt {t_lib:7.3f} ms {fl / t_lib / 1e9:7.1f} TF", flush=True)
             for t in [t for t in tiles if t in (0, 6, 12)]:
-                G._FORCE_TILE = str(t)
+                G.FORCE_TILE = t
                 tt = timeit(lambda: G.linear_wgrad(dy, x, out))
                 print(f"wgrad {name:4s} tile{t}      ours {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF  x{t_lib / tt:5.2f}", flush=True)
-            G._FORCE_TILE = None
+            G.FORCE_TILE = None
     if "epi" in a.only:
         # the fused epilogues exactly as the training step runs them (ViT-B/16 b256 shapes)
         seed = torch.tensor([1234], dtype=torch.int64, device=dev)
@@ -109,7 +109,7 @@ def main():
         dq3, wqkvt = torch.randn(T, M3, device=dev, dtype=torch.bfloat16), wqkv.t().contiguous()
         for _round in range(a.rounds):
           for t in [int(v) for v in a.epi_tiles.split(",")]:  # one tile per workgroup / persistent / stream-K
-            G._FORCE_TILE = str(t)
+            G.FORCE_TILE = t
             for name, fl, fn in [
                 ("qkv fwd  bias            ", 2.0 * T * M3 * D, lambda: G.linear_fwd(x, wqkv, bqkv)),
                 ("out fwd  bias+resid      ", 2.0 * T * D * D, lambda: G.linear_fwd(x, wo, b2, resid=r)),
@@ -122,11 +122,11 @@ def main():
             ]:
                 tt = timeit(fn)
                 print(f"epi   {name} tile{t} {tt:7.3f} ms {fl / tt / 1e9:7.1f} TF", flush=True)
-            G._FORCE_TILE = None
+            G.FORCE_TILE = None
         for t in [int(v) for v in a.gelu_tiles.split(",") if v]:  # other structures for the GELU epilogue
-            G._FORCE_TILE = str(t)
+            G.FORCE_TILE = t
             tt = timeit(lambda: G.linear_fwd(x, w1, b1, gelu_aux=u, drop=(seed, 3 << 32, 0.1)))
-            G._FORCE_TILE = None
+            G.FORCE_TILE = None
             print(f"epi   fc1 fwd GELU tile{t:<3d}            {tt:7.3f} ms {2.0 * T * M * D / tt / 1e9:7.1f} TF", flush=True)
     if "fp8" in a.only:
         from pytorch_vit_paper_replication_amd.ops import fp8 as F8
@@ -141,9 +141,9 @@ def main():
             meta = F8.Fp8Meta(2, dev, history=1)
             xq, xs = meta.quantize(x, 0, current=True)
             wq, ws = meta.quantize(w, 1, current=True)
-            G._FORCE_TILE = "12"
+            G.FORCE_TILE = 12
             t16 = timeit(lambda: G.linear_fwd(x, w, b))
-            G._FORCE_TILE = None
+            G.FORCE_TILE = None
             t8 = timeit(lambda: F8.linear_fwd_fp8(xq, xs, wq, ws, b))
             tq = timeit(lambda: meta.quantize(x, 0))
             t_lib = timeit(lambda: torch.matmul(x, w.t()))

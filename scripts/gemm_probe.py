@@ -15,7 +15,7 @@ x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
 w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
 b = torch.randn(N, device="cuda")
 for t in tiles:
-    G._FORCE_TILE = str(t)
+    G.FORCE_TILE = t
     for _ in range(3):
         G.linear_fwd(x, w, b)
 for _ in range(3):

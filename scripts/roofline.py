@@ -84,7 +84,7 @@ def main():
         g["wbytes"] += write
         if gui > 0:
             g["util"].append(busy / (gui / 8.0 * 1024.0))
-    print(f"# Roofline of one ViT-B/16 b256 training step (serial: PVR_SIDE_WGRAD=0), {n} dispatches, "
+    print(f"# Roofline of one ViT-B/16 b256 training step (serial: bench.py --serial-wgrad), {n} dispatches, "
           f"{step_us / 1e3:.2f} ms of kernel time\n")
     print("Peaks: 2.5 PF bf16 dense MFMA, 8 TB/s HBM3E. FLOP from SQ_VALU_MFMA_BUSY_CYCLES x 1024; bytes = 2 x FETCH_SIZE + "
           "WRITE_SIZE (upper estimate of reads). `bound` = max(FLOP/peak, bytes/BW); `% of bound` = bound / measured.\n")

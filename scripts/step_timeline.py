@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-queue busy time and the dispatch timeline of the last full training step in a rocprofv3
-kernel trace (the step = dispatches after the second-to-last adam_kernel up to the last).
+kernel trace (the step = dispatches after the second-to-last adam_kernel / adam_t_kernel up to the last).
 
   python scripts/step_timeline.py <k_kernel_trace.csv> [first last]   # print dispatches first..last
 """
@@ -17,7 +17,7 @@ def main():
         n = re.sub(r"^void ", "", r["Kernel_Name"]).replace("pvr::(anonymous namespace)::", "")
         r["n"] = n.split("(")[0][:48]
     rows.sort(key=lambda r: r["s"])
-    ad = [i for i, r in enumerate(rows) if "adam_kernel" in r["n"]]
+    ad = [i for i, r in enumerate(rows) if "adam_kernel" in r["n"] or "adam_t_kernel" in r["n"]]
     step = rows[ad[-2] + 1: ad[-1] + 1]
     t0, t1 = step[0]["s"], step[-1]["e"]
     print(f"step {(t1 - t0) / 1e6:.3f} ms, {len(step)} dispatches")

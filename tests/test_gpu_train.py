@@ -348,8 +348,10 @@ def test_side_stream_matches_serial_weight_gradients(monkeypatch):
     from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
     from pytorch_vit_paper_replication_amd.optim import FusedAdam
 
-    def run(side: str):
-        monkeypatch.setenv("PVR_SIDE_WGRAD", side)
+    from pytorch_vit_paper_replication_amd.runtime import param_store
+
+    def run(side: bool):
+        monkeypatch.setattr(param_store, "SIDE_WGRAD", side)
         torch.manual_seed(0)
         m = ViT(**dict(CFG, mlp_dropout=0.0, embedding_dropout=0.0)).cuda()
         opt = FusedAdam(m.parameters(), lr=1e-3)
@@ -366,8 +368,8 @@ def test_side_stream_matches_serial_weight_gradients(monkeypatch):
         torch.cuda.synchronize()
         return grads, [p.detach().clone() for p in m.parameters()]
 
-    ga, pa = run("1")
-    gb, pb = run("0")
+    ga, pa = run(True)
+    gb, pb = run(False)
     for a, b in zip(ga, gb):
         assert torch.allclose(a, b, rtol=1e-3, atol=1e-6), (a - b).abs().max().item()
     for a, b in zip(pa, pb):
