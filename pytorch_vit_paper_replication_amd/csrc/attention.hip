@@ -117,10 +117,31 @@ PVR_DEV void static_for(F&& f) {
 
 PVR_DEV uint32_t clamp_bytes(int64_t b) { return b < 0 ? 0u : (b > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)b); }
 
+// Attention-probability dropout (nn.MultiheadAttention(dropout=p), reference models/vit.py:86-90):
+// element (query q, key k) of pair bh is kept iff the 16-bit half (k even: low, odd: high) of
+// rng_mix32((idx >> 1) ^ key(bh)) >= thr16, idx = q * Npad + k (Npad = N rounded up to 4, so a row's
+// 4-key groups start at a multiple of 4). The forward draws 4 consecutive keys per 2 hashes
+// (rng_keep4_32), the backward one element at a time: the same bits, no stored mask. Kept
+// probabilities scale by 65536 / (65536 - thr16); the softmax normaliser uses the undropped P.
+struct AttnDrop {
+  const uint64_t* seed;  // device seed (the step's snapshot); null: no dropout
+  uint64_t off;          // per-layer site offset
+  uint32_t thr;          // round(p * 65536)
+  float scale;           // 1 / keep probability
+};
+PVR_DEV uint32_t attn_drop_key(const AttnDrop& d, int bh) {
+  return rng_mix32(rng_key(*d.seed + d.off) ^ (0x9E3779B9u * (uint32_t)(bh + 1)));
+}
+PVR_DEV bool attn_keep1(uint32_t key, uint32_t idx, uint32_t thr) {
+  const uint32_t h = rng_mix32((idx >> 1) ^ key);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+}
+
 // ----------------------------------------------------------------------------------- forward
-template <int DH>
+template <int DH, bool DROP>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
-                                                        int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale) {
+                                                        int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale,
+                                                        AttnDrop drop) {
   using C = Hd<DH>;
   // keys per tile: 64, or 32 for two-image head rows (dh > 64), so that the two K/V stages stay at
   // 32 KiB and four workgroups share a CU
@@ -153,6 +174,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
 
   const float c = scale * LOG2E;
   float m_run = -INFINITY, l_run = 0.f;
+  uint32_t dkey = 0, drow = 0;  // dropout: the pair's hash key, this lane's query row start idx
+  if constexpr (DROP) {
+    dkey = attn_drop_key(drop, bh);
+    drow = (uint32_t)min(q0 + li, N - 1) * (uint32_t)((N + 3) & ~3);
+  }
   v4f o[C::NE];
 #pragma unroll
   for (int e = 0; e < C::NE; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -206,13 +232,17 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float psum = 0.f;
 #pragma unroll
-      for (int f = 0; f < NFR; ++f)
+      for (int f = 0; f < NFR; ++f) {
+        bool keep[4] = {true, true, true, true};
+        if constexpr (DROP) rng_keep4_32(dkey, drow + (uint32_t)(kbase + 16 * f + 4 * g), drop.thr, keep);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float pv = __builtin_amdgcn_exp2f(fmaf(s[f][r], c, -m_new));
-          s[f][r] = pv;
-          psum += pv;
+          psum += pv;  // the normaliser sums the undropped probabilities
+          if constexpr (DROP) s[f][r] = keep[r] ? pv * drop.scale : 0.f;
+          else s[f][r] = pv;
         }
+      }
       l_run = l_run * alpha + psum;
       m_run = m_new;
 #pragma unroll
@@ -410,14 +440,14 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
 // grid (nkb, B*H), block NW*64 (NW in {1,2,4,8}); workgroup keys [kb*KB, kb*KB + KB), KB = 32*NW.
 // delta = rowsum(dO * O) of each query block is formed in-kernel from the staged dO and O rows
 // (no separate pass over dO and O, no delta round trip through HBM).
-template <int DH>
+template <int DH, bool DROP>
 __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                         const uint16_t* __restrict__ dout, int64_t ld_do,
                                                         const uint16_t* __restrict__ o, int64_t ld_o,
                                                         const float* __restrict__ lse,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
                                                         float* __restrict__ dbias, int N, int H, int D, float scale,
-                                                        int key_off, int key_end, int dq_mode) {
+                                                        int key_off, int key_end, int dq_mode, AttnDrop drop) {
   using C = Hd<DH>;
   constexpr int QB = 32;
   constexpr int RB = 128 * C::NH;  // LDS bytes per staged head row
@@ -489,6 +519,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 
   const float c = scale * LOG2E;
   const int nqb = (N + QB - 1) / QB;
+  const uint32_t dkey = DROP ? attn_drop_key(drop, bh) : 0u, npad = (uint32_t)((N + 3) & ~3);
   auto stage = [&](int qb) {  // Q / dO / O rows and the lse of query block qb into slot qb & 1
     // everything by LDS-DMA: a plain load of lse here would make hipcc wait vmcnt(0) at its first
     // use, draining these DMAs right after issuing them. lse of queries past N reads as 0; their
@@ -565,8 +596,18 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const float pv = __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l2));
-          s[a][f][r] = pv;
-          dp[a][f][r] = pv * (dp[a][f][r] - dl);
+          if constexpr (DROP) {
+            // dropout: dV takes the dropped P, dP = mask * scale * (dO . V); rows past N have
+            // dO = 0 and delta = 0, so their dS stays 0 whatever the mask
+            const int key = kw0 + 16 * f + li;
+            const uint32_t qi = (uint32_t)min(q0 + ql, N - 1);
+            const float m = attn_keep1(dkey, qi * npad + (uint32_t)min(key, N - 1), drop.thr) ? drop.scale : 0.f;
+            s[a][f][r] = pv * m;
+            dp[a][f][r] = pv * (m * dp[a][f][r] - dl);
+          } else {
+            s[a][f][r] = pv;
+            dp[a][f][r] = pv * (dp[a][f][r] - dl);
+          }
         }
       }
     // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
@@ -1330,8 +1371,13 @@ static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t
 
 template <int DH>
 static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
-                                  int D, float scale, hipStream_t s) {
+                                  int D, float scale, const pvr::AttnDrop& drop, hipStream_t s) {
   using namespace pvr;
+  if (drop.seed) {  // attention dropout: the tiled kernel with the in-register keep mask
+    hipLaunchKernelGGL((attn_fwd_kernel<DH, true>), dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D,
+                       scale, drop);
+    return hipGetLastError();
+  }
   if (DH == 64 && N <= 256) {
     // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take
     // up to 128 KiB of LDS), ceil(N/16) waves
@@ -1346,19 +1392,24 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
     }
   }
   // 1-D grid of (B*H) x query blocks, XCD-remapped in-kernel
-  hipLaunchKernelGGL(attn_fwd_kernel<DH>, dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D, scale);
+  hipLaunchKernelGGL((attn_fwd_kernel<DH, false>), dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D,
+                     scale, drop);
   return hipGetLastError();
 }
 
+// seed (optional): attention-probability dropout with keep threshold thr16 (see AttnDrop); the
+// backward must get the same seed / seed_off / thr16
 extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
-                                   int H, int D, float scale, hipStream_t s) {
+                                   int H, int D, float scale, const uint64_t* seed, uint64_t seed_off, uint32_t thr16, float keep_scale,
+                                   hipStream_t s) {
   using namespace pvr;
-  if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
+  if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
+  const AttnDrop drop{seed, seed_off, thr16, keep_scale};
   switch (D / H) {
-    case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
-    case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
-    case 96: return attn_fwd_launch<96>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
-    case 128: return attn_fwd_launch<128>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
+    case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
+    case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
+    case 96: return attn_fwd_launch<96>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
+    case 128: return attn_fwd_launch<128>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1376,17 +1427,17 @@ extern "C" int pvr_attn_bwd_waves(int N) {
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
 }
 
-// N = (full key blocks) + 1 key: main kernel + last-key kernel, dQ written directly (no dq_acc)
-static bool attn_bwd_lastkey_path(int N, bool dbias) {
+// N = (full key blocks) + 1 key: main kernel + last-key kernel, dQ written directly (no dq_acc);
+// not with attention dropout (the last-key kernel has no mask)
+static bool attn_bwd_lastkey_path(int N, bool dbias, bool drop) {
   const int KB = 32 * pvr_attn_bwd_waves(N);
-  return (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && N <= 512;
+  return (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && !drop && N <= 512;
 }
 
 // 1 if pvr_attn_bwd needs the zero-initialised f32 dQ workspace for this shape
-extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias) {
-  if (dh == 64 && N <= 256) return 0;
+extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias, int drop) {
   if (pvr_attn_bwd_key_blocks(N) <= 1) return 0;
-  return attn_bwd_lastkey_path(N, dbias != 0) ? 0 : 1;
+  return attn_bwd_lastkey_path(N, dbias != 0, drop != 0) ? 0 : 1;
 }
 
 template <int NQ>
@@ -1417,22 +1468,21 @@ static bool attn_bwd_pipe_ok(int B, int N, int H, int D, int64_t ld, int64_t ld_
   return H > 0 && D == 64 * H && N > 192 && N <= 224 && off31;
 }
 
-template <int DH>
-static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
-                                  int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                  int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
+template <int DH, bool DROP>
+static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                   int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, const pvr::AttnDrop& drop,
+                                   hipStream_t s) {
   using namespace pvr;
-  if (DH == 64 && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][128] partials
-    return attn_bwd_pipe8_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
-  if (nkb > 1 && !dq_acc && !attn_bwd_lastkey_path(N, dbias != nullptr)) return hipErrorInvalidValue;
+  if (nkb > 1 && !dq_acc && !attn_bwd_lastkey_path(N, dbias != nullptr, DROP)) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   const int RB = 128 * Hd<DH>::NH;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)(8 * 32 * RB + 6 * 32 * RB + 32 * 8 * 32 * 2 + 2 * 1024));
     if (e != hipSuccess) return e;
     attr = true;
@@ -1441,17 +1491,17 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   auto launch = [&](int nw, int k0, int k1, int dq_mode) {
     const int kb = nw * 32;
     const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
-    hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout, ld_do, out,
-                       ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1, dq_mode);
+    hipLaunchKernelGGL((attn_bwd_kernel<DH, DROP>), dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout,
+                       ld_do, out, ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1, dq_mode, drop);
   };
   const int rem = N % KB;
-  if (attn_bwd_lastkey_path(N, dbias != nullptr)) {
+  if (attn_bwd_lastkey_path(N, dbias != nullptr, DROP)) {
     // one key past a full key block: the main kernel over keys [0, N - 1) writes dQ directly, the
     // last key's dK / dV and dQ contribution come from the streaming kernel above
     const int kb = NW * 32, k1 = N - 1;
     const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
-    hipLaunchKernelGGL(attn_bwd_kernel<DH>, dim3((k1 + kb - 1) / kb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do, out,
-                       ld_o, lse, dqkv, ld_dq, nullptr, nullptr, N, H, D, scale, 0, k1, 0);
+    hipLaunchKernelGGL((attn_bwd_kernel<DH, DROP>), dim3((k1 + kb - 1) / kb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do,
+                       out, ld_o, lse, dqkv, ld_dq, nullptr, nullptr, N, H, D, scale, 0, k1, 0, drop);
     hipLaunchKernelGGL(attn_bwd_lastkey_kernel<DH>, dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq,
                        N, H, D, scale);
     return hipGetLastError();
@@ -1479,13 +1529,27 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
   return hipGetLastError();
 }
 
+template <int DH>
+static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
+                                  int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
+                                  int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, const pvr::AttnDrop& drop,
+                                  hipStream_t s) {
+  if (drop.seed)  // attention dropout: the generic kernel regenerates the forward's keep mask
+    return attn_bwd_generic<DH, true>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale,
+                                      drop, s);
+  if (DH == 64 && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][128] partials
+    return attn_bwd_pipe8_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
+  return attn_bwd_generic<DH, false>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale,
+                                     drop, s);
+}
+
 // 1 if pvr_attn_bwd takes the pipelined whole-head backward for this shape and these layouts; its
 // dbias is then f32 [B*H][ceil(N/32)][192] partials instead: per (batch, head, 32-query block) the
 // column sums of dQ over its two 16-query halves (2 x 64, the head's q-bias slice; summed) and of dO
 // (64: the v-bias slice, sum_k dV = sum_q dO since softmax rows sum to 1); the k-bias gradient is
 // exactly 0 (sum_k dS = 0 per query)
-extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq) {
-  return attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq) ? 1 : 0;
+extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq, int drop) {
+  return !drop && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq) ? 1 : 0;
 }
 
 // dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head);
@@ -1495,11 +1559,14 @@ extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, in
 // (pvr_attn_bwd_uses_pipe) the per-block partials described there.
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                    int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, hipStream_t s) {
-  if (H <= 0 || D % H != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
+                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, const uint64_t* seed,
+                                   uint64_t seed_off, uint32_t thr16, float keep_scale, hipStream_t s) {
+  if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
+  const pvr::AttnDrop drop{seed, seed_off, thr16, keep_scale};
   switch (D / H) {
 #define PVR_BWD_DH(DH) \
-  case DH: return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale, s);
+  case DH:             \
+    return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale, drop, s);
     PVR_BWD_DH(64) PVR_BWD_DH(80) PVR_BWD_DH(96) PVR_BWD_DH(128)
 #undef PVR_BWD_DH
     default: return hipErrorInvalidValue;

@@ -54,15 +54,17 @@ hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const fl
 hipError_t pvr_fp8_quant_t(const uint16_t*, int64_t, uint8_t*, int64_t, int, int, const float*, int, hipStream_t);
 hipError_t pvr_fp8_quant_multi(const int64_t*, int, int64_t, const float*, unsigned*, int, int, hipStream_t);
 int pvr_attn_bwd_key_blocks(int);
-int pvr_attn_bwd_needs_dq_acc(int, int, int);
+int pvr_attn_bwd_needs_dq_acc(int, int, int, int);
 int pvr_attn_bwd_waves(int);
-int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t);
-hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, hipStream_t);
+int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
+hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, const uint64_t*, uint64_t,
+                        uint32_t, float, hipStream_t);
 int pvr_attn_dbias_splits(int, int);
 hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float*, const uint16_t*, int64_t, int, uint16_t*, int64_t,
                                hipStream_t);
 hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, int, hipStream_t);
-hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float,
+                        const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 }
 
 namespace {
@@ -600,13 +602,16 @@ void fp8_scale_update(torch::Tensor hist, torch::Tensor amax, torch::Tensor qsca
         "fp8_scale_update");
 }
 
-std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int64_t H, double scale) {
+// seed / seed_offset / drop_p: attention-probability dropout (the backward gets the same three)
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int64_t H, double scale, c10::optional<torch::Tensor> seed,
+                                    int64_t seed_offset, double drop_p) {
   const int64_t D = qkv.size(1) / 3;
   auto out = torch::empty({B * N, D}, qkv.options());
   auto lse = torch::empty({B * H, N}, qkv.options().dtype(torch::kFloat32));
   TORCH_CHECK(qkv.size(0) == B * N, "attn_fwd: qkv rows != B*N");
+  const DropArgs d = drop_args(seed, drop_p, "attn_fwd");
   check(pvr_attn_fwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf_mut(out, "out"), D, f32_mut(lse, "lse"), (int)B, (int)N, (int)H, (int)D,
-                     (float)scale, stream()),
+                     (float)scale, d.seed, (uint64_t)seed_offset, d.thr, d.scale, stream()),
         "attn_fwd");
   return {out, lse};
 }
@@ -648,21 +653,24 @@ torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts, bool
 }
 
 // pipelined backward taken for the standard layouts of this shape (qkv [T][3D], dO / O [T][D])
-bool attn_bwd_pipe_path(int64_t B, int64_t N, int64_t H, int64_t D) {
-  return pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D) != 0;
+bool attn_bwd_pipe_path(int64_t B, int64_t N, int64_t H, int64_t D, bool drop) {
+  return pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D, drop ? 1 : 0) != 0;
 }
 
 // dbias: [3D] f32 accumulated with the in_proj bias gradient. dbias_part (pipelined path only,
 // [B*H][ceil(N/32)][192] f32): receives the kernel's per-block partials instead, left unreduced (the
 // caller reduces them, e.g. on the weight-gradient side stream: attn_dbias_reduce).
 torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
-                       double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out) {
+                       double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out,
+                       c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
   torch::Tensor dq_acc;
   int dq_rezero = 0;
   const bool has_db = dbias.has_value() && dbias->defined();
-  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)(D / H), has_db ? 1 : 0)) {
+  const DropArgs drop = drop_args(seed, drop_p, "attn_bwd");
+  const int has_drop = drop.seed ? 1 : 0;
+  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)(D / H), has_db ? 1 : 0, has_drop)) {
     dq_acc = dq_workspace(B * N * D, qkv.options());
     dq_rezero = dq_acc.defined() ? 1 : 0;
     if (!dq_acc.defined()) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
@@ -671,7 +679,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   torch::Tensor dbias_part;
   const bool want_db = dbias.has_value() && dbias->defined();
   const bool pipe = pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, ld_of(qkv, "qkv"), ld_of(dout, "dout"), ld_of(out, "out"),
-                                           ld_of(dqkv, "dqkv")) != 0;
+                                           ld_of(dqkv, "dqkv"), has_drop) != 0;
   const bool part_out = dbias_part_out.has_value() && dbias_part_out->defined();
   if (part_out) {
     TORCH_CHECK(pipe && !want_db, "dbias_part: pipelined backward only, and not together with dbias");
@@ -692,7 +700,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
                                       ld_of(dout, "dout"), f32(lse, "lse"), bf_mut(dqkv, "dqkv"),
                                       ld_of(dqkv, "dqkv"), dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
                                       dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
-                                      (float)scale, stream());
+                                      (float)scale, drop.seed, (uint64_t)seed_offset, drop.thr, drop.scale, stream());
   // a persistent accumulator is re-zeroed only by a completed backward: after a failed launch it
   // may hold stale partial sums, so it is dropped (re-created zeroed by the next call)
   if (err != hipSuccess && dq_rezero) dq_workspace(0, qkv.options(), true);
@@ -727,7 +735,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("splitk_epilogue", &splitk_epilogue);
-  m.def("attn_bwd_pipe_path", &attn_bwd_pipe_path);
+  m.def("attn_bwd_pipe_path", &attn_bwd_pipe_path, py::arg("B"), py::arg("N"), py::arg("H"), py::arg("D"), py::arg("drop") = false);
   m.def("attn_dbias_reduce", &attn_dbias_reduce);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("transpose_batched", &transpose_batched);
@@ -761,8 +769,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8_wgrad", &gemm_fp8_wgrad);
   m.def("fp8_quant_multi", &fp8_quant_multi, py::arg("segs"), py::arg("nchunks"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"),
         py::arg("amax_only"));
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("B"), py::arg("N"), py::arg("H"), py::arg("scale"),
+        py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
-        py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none());
+        py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none(),
+        py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("arch", []() { return std::string("gfx950"); });
 }

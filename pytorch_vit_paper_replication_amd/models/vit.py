@@ -216,8 +216,6 @@ class ViT(nn.Module):
             return False
         if c["mlp_size"] % 64 != 0:
             return False
-        if self.training and c["attn_dropout"] > 0:
-            return False  # attention-probability dropout only on the PyTorch path
         P = c["patch_size"]
         return x.shape[2] == x.shape[3] == c["image_size"] and x.shape[2] % P == 0
 
@@ -234,7 +232,17 @@ class ViT(nn.Module):
         return seed
 
     def _forward_fused(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops.fused_vit import EncoderBlockFn, block_links, HeadFn, PatchEmbedFn, site_drop
+        from ..ops.fused_vit import HeadFn
+
+        tokens, store, B, N = self._fused_encoder(x)
+        head = self.classifier[0]
+        return HeadFn.apply(tokens, B, N, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias,
+                            head.weight, head.bias)
+
+    def _fused_encoder(self, x: torch.Tensor):
+        """Patch embedding + every encoder block on the fused path: (bf16 tokens [B*N, D], store, B, N).
+        Shared by this model's head and the classifier-free backbone (models/vit_no_classifier.py)."""
+        from ..ops.fused_vit import ATTN_SITE, EncoderBlockFn, block_links, PatchEmbedFn, site_drop
         from ..runtime.param_store import get_store
 
         c = self.config
@@ -254,7 +262,7 @@ class ViT(nn.Module):
         store.grad_enabled = grad  # the fused Functions' forward runs with grad mode off: tell them
         if grad:
             store.prepare_grads()
-        need_seed = training and (c["mlp_dropout"] > 0 or c["embedding_dropout"] > 0)
+        need_seed = training and (c["mlp_dropout"] > 0 or c["embedding_dropout"] > 0 or c["attn_dropout"] > 0)
         seed = self._dropout_seed(dev) if need_seed else None
         pe = self.patch_embedding_block
         conv = pe.patch_and_flatten[0]
@@ -271,13 +279,12 @@ class ViT(nn.Module):
         for i, blk in enumerate(blocks):
             ln1 = blk.msa_block.layer_norm
             ln2 = blk.mlp_block.layer_norm
-            p1 = blk.mlp_block.mlp[2].p
-            tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads, ln1.eps, ln2.eps,
-                                          store, site_drop(seed, 1 + 2 * i, p1, training), drops2[i],
+            mha = blk.msa_block.multi_head_attention
+            drops = (site_drop(seed, 1 + 2 * i, blk.mlp_block.mlp[2].p, training), drops2[i],
+                     site_drop(seed, ATTN_SITE + i, mha.dropout, training))
+            tokens = EncoderBlockFn.apply(tokens, B, N, mha.num_heads, ln1.eps, ln2.eps, store, drops,
                                           None if f8 is None else (f8, i), links[i], *blk.fused_params())
-        head = self.classifier[0]
-        return HeadFn.apply(tokens, B, N, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias,
-                            head.weight, head.bias)
+        return tokens, store, B, N
 
     # ------------------------------------------------------------------ fp8
     def enable_fp8(self, enabled: bool = True, history: int = 16, margin: int = 0, dgrad: bool = True,

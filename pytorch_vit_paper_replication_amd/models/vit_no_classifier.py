@@ -30,38 +30,8 @@ class ViT(_FullViT):
         return self.forward_features(x)
 
     def _forward_fused_features(self, x: torch.Tensor) -> torch.Tensor:
-        from ..ops.fused_vit import EncoderBlockFn, block_links, PatchEmbedFn, TokenLayerNormFn, site_drop
-        from ..runtime.param_store import get_store
+        from ..ops.fused_vit import TokenLayerNormFn
 
-        c = self.config
-        dev = x.device
-        store = get_store(self, dev)
-        store.refresh_shadow()
-        if not getattr(store, "_vit_t_registered", False):
-            store.register_transposed([w for blk in self.transformer_encoder for w in blk.fused_params()[2:12:2] if w.dim() == 2])
-            store._vit_t_registered = True
-        store.ensure_transposed()
-        training = self.training
-        store.grad_enabled = torch.is_grad_enabled()  # the fused Functions' forward runs with grad mode off
-        if store.grad_enabled:
-            store.prepare_grads()
-        need_seed = training and (c["mlp_dropout"] > 0 or c["embedding_dropout"] > 0)
-        seed = self._dropout_seed(dev) if need_seed else None
-        pe = self.patch_embedding_block
-        conv = pe.patch_and_flatten[0]
-        tokens = PatchEmbedFn.apply(x, c["patch_size"], store, seed, pe.dropout.p, training,
-                                    conv.weight, conv.bias, pe.class_token, pe.position_embedding)
-        B, N = x.shape[0], pe.number_of_patches + 1
-        f8 = self._fp8_state(dev, B * N)
-        if f8 is not None:
-            f8.begin_step(training)
-        blocks = list(self.transformer_encoder)
-        drops2 = [site_drop(seed, 2 + 2 * i, blk.mlp_block.mlp[4].p, training) for i, blk in enumerate(blocks)]
-        links = block_links(blocks, drops2)
-        for i, blk in enumerate(blocks):
-            tokens = EncoderBlockFn.apply(tokens, B, N, blk.msa_block.multi_head_attention.num_heads,
-                                          blk.msa_block.layer_norm.eps, blk.mlp_block.layer_norm.eps, store,
-                                          site_drop(seed, 1 + 2 * i, blk.mlp_block.mlp[2].p, training), drops2[i],
-                                          None if f8 is None else (f8, i), links[i], *blk.fused_params())
+        tokens, store, B, N = self._fused_encoder(x)  # the full ViT's fused encoder (device checks, side-stream join)
         y = TokenLayerNormFn.apply(tokens, self.layer_norm.eps, store, self.layer_norm.weight, self.layer_norm.bias)
         return y.float().view(B, N, -1)

@@ -24,6 +24,7 @@ from .. import _ext
 from . import gemm
 
 SITE_SHIFT = 32
+ATTN_SITE = 1 << 20  # dropout site of block i's attention probabilities: ATTN_SITE + i
 
 
 # Test hook: called as DGRAD_TAP(which, output) after every encoder-block dgrad GEMM (which = 0 fc2,
@@ -110,8 +111,10 @@ class EncoderBlockFn(torch.autograd.Function):
     """One pre-LN transformer encoder block, forward and hand-written backward."""
 
     @staticmethod
-    def forward(ctx, x, B, N, H, eps1, eps2, store, drop1, drop2, f8, links, *params):
+    def forward(ctx, x, B, N, H, eps1, eps2, store, drops, f8, links, *params):
         ext = _ext.ext()
+        drop1, drop2, dropa = drops  # fc1 (after GELU), fc2, attention probabilities
+        aseed, aoff, ap = gemm._drop_args(dropa)
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
         T, D = x.shape
         ctx.links = links if links is not None else (None, None)
@@ -129,7 +132,7 @@ class EncoderBlockFn(torch.autograd.Function):
         xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
         if f8 is None:
             qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
-            o, lse = ext.attn_fwd(qkv, B, N, H, scale)
+            o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
             x1 = gemm.linear_fwd(o, store.bf16(wo), bo, resid=x)
             xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
             h = gemm.linear_fwd(xn2, store.bf16(w1), b1, gelu_aux=u, gelu=True, drop=drop1)
@@ -145,7 +148,7 @@ class EncoderBlockFn(torch.autograd.Function):
             wq = [st.weight(store.bf16(w), id(w), gen, lay) for w in (wqkv, wo, w1, w2)]
             a, s_ = st.act_quant(xn1, blk, 0)
             qkv = F8.linear_fwd_fp8(a, s_, *wq[0], bqkv)
-            o, lse = ext.attn_fwd(qkv, B, N, H, scale)
+            o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
             a, s_ = st.act_quant(o, blk, 1)
             x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
             xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
@@ -155,15 +158,16 @@ class EncoderBlockFn(torch.autograd.Function):
             x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
         if need_bwd:
             ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
-        ctx.meta = (B, N, H, scale, store, drop1, drop2, params)
+        ctx.meta = (B, N, H, scale, store, drop1, drop2, dropa, params)
         return x2
 
     @staticmethod
     def backward(ctx, dx2):
         ext = _ext.ext()
         x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = ctx.saved_tensors
-        B, N, H, scale, store, drop1, drop2, params = ctx.meta
+        B, N, H, scale, store, drop1, drop2, dropa, params = ctx.meta
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
+        aseed, aoff, ap = gemm._drop_args(dropa)
         g = store.grad_dest
         dx2 = dx2.contiguous()
         T, D = dx2.shape
@@ -227,7 +231,7 @@ class EncoderBlockFn(torch.autograd.Function):
         gbqkv = g(bqkv)
         side_db = False
         db_part = None
-        if gbqkv is not None and ext.attn_bwd_pipe_path(B, N, H, D):
+        if gbqkv is not None and ext.attn_bwd_pipe_path(B, N, H, D, aseed is not None):
             # the pipelined attention backward emits per-(image, head, query block) column sums of dQ and
             # dO (= the v-bias gradient; the k bias has none); only their small reduction remains (side
             # stream), no pass over dQKV
@@ -235,7 +239,7 @@ class EncoderBlockFn(torch.autograd.Function):
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part)
         else:
             # other shapes: the in_proj bias gradient is a column sum of dQKV on the side stream
-            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale)
+            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, None, aseed, aoff, ap)
             side_db = gbqkv is not None
 
         def attn_wgrads():
@@ -263,7 +267,7 @@ class EncoderBlockFn(torch.autograd.Function):
         else:
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])
-        return (dx,) + (None,) * (10 + len(params))
+        return (dx,) + (None,) * (9 + len(params))
 
 
 class HeadFn(torch.autograd.Function):

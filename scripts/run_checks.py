@@ -16,9 +16,9 @@ for fn in KC.all_checks():
     if not any(n in label for n in names):
         continue
     torch.manual_seed(0)
-    name, err, tol = fn()
+    name, metrics, limits = fn()
     torch.cuda.synchronize()
-    ok = err <= tol
+    ok = KC.passed(metrics, limits)
     bad += not ok
-    print(f"{'ok  ' if ok else 'FAIL'} {name}: err {err:.3e} tol {tol:.1e}", flush=True)
+    print(f"{'ok  ' if ok else 'FAIL'} {name}: {KC.fmt_metrics(metrics, limits)}", flush=True)
 sys.exit(1 if bad else 0)

@@ -21,3 +21,16 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Print every numerics check's measured errors next to its limits (tests/test_gpu_kernels.py)."""
+    mod = sys.modules.get("tests.test_gpu_kernels")
+    rows = getattr(mod, "MEASURED", None) if mod is not None else None
+    if not rows:
+        return
+    from tests.kernel_checks import fmt_metrics, passed
+
+    terminalreporter.section("kernel numerics: measured / limit")
+    for name, metrics, limits in rows:
+        terminalreporter.write_line(f"{'OK  ' if passed(metrics, limits) else 'FAIL'} {name}: {fmt_metrics(metrics, limits)}")
