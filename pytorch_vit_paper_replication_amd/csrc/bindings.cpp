@@ -57,6 +57,7 @@ int pvr_attn_bwd_key_blocks(int);
 int pvr_attn_bwd_needs_dq_acc(int, int, int, int);
 int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
+int pvr_attn_bwd_part_rows(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, const uint64_t*, uint64_t,
                         uint32_t, float, hipStream_t);
 int pvr_attn_dbias_splits(int, int);
@@ -652,9 +653,10 @@ torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts, bool
   return *t;
 }
 
-// pipelined backward taken for the standard layouts of this shape (qkv [T][3D], dO / O [T][D])
-bool attn_bwd_pipe_path(int64_t B, int64_t N, int64_t H, int64_t D, bool drop) {
-  return pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D, drop ? 1 : 0) != 0;
+// R > 0: for the standard layouts of this shape (qkv [T][3D], dO / O [T][D]) the backward emits the
+// in_proj bias gradient as f32 [B*H][R][192] partials (pipelined or chunked kernel); 0: it does not
+int64_t attn_bwd_bias_rows(int64_t B, int64_t N, int64_t H, int64_t D, bool drop) {
+  return pvr_attn_bwd_part_rows((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D, drop ? 1 : 0);
 }
 
 // dbias: [3D] f32 accumulated with the in_proj bias gradient. dbias_part (pipelined path only,
@@ -678,21 +680,22 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
   torch::Tensor dbias_part;
   const bool want_db = dbias.has_value() && dbias->defined();
-  const bool pipe = pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, ld_of(qkv, "qkv"), ld_of(dout, "dout"), ld_of(out, "out"),
-                                           ld_of(dqkv, "dqkv"), has_drop) != 0;
+  const int prow = pvr_attn_bwd_part_rows((int)B, (int)N, (int)H, (int)D, ld_of(qkv, "qkv"), ld_of(dout, "dout"), ld_of(out, "out"),
+                                          ld_of(dqkv, "dqkv"), has_drop);
+  const bool pipe = prow > 0;  // the kernel writes [B*H][prow][192] partials
   const bool part_out = dbias_part_out.has_value() && dbias_part_out->defined();
   if (part_out) {
-    TORCH_CHECK(pipe && !want_db, "dbias_part: pipelined backward only, and not together with dbias");
+    TORCH_CHECK(pipe && !want_db, "dbias_part: pipelined / chunked backward only, and not together with dbias");
     TORCH_CHECK(dbias_part_out->is_cuda() && dbias_part_out->scalar_type() == torch::kFloat32 && dbias_part_out->is_contiguous() &&
-                    dbias_part_out->numel() == B * H * ((N + 31) / 32) * 192,
-                "dbias_part [B*H][ceil(N/32)][192] f32");
+                    dbias_part_out->numel() == B * H * prow * 192,
+                "dbias_part [B*H][attn_bwd_bias_rows][192] f32");
     dbias_part = *dbias_part_out;
   }
   if (want_db) {
     TORCH_CHECK(dbias->numel() == 3 * D && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous(), "dbias [3D] f32");
     const int dh = (int)(D / H);
-    if (pipe)  // per-(batch, head, query block) partials written by the pipelined backward: q 2 x 64 | v 64
-      dbias_part = torch::empty({B * H, (N + 31) / 32, 192}, qkv.options().dtype(torch::kFloat32));
+    if (pipe)  // per-(batch, head, block or chunk) partials written by the kernel: q 2 x 64 | v 64
+      dbias_part = torch::empty({B * H, (int64_t)prow, 192}, qkv.options().dtype(torch::kFloat32));
     else if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
       dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
@@ -735,7 +738,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("splitk_epilogue", &splitk_epilogue);
-  m.def("attn_bwd_pipe_path", &attn_bwd_pipe_path, py::arg("B"), py::arg("N"), py::arg("H"), py::arg("D"), py::arg("drop") = false);
+  m.def("attn_bwd_bias_rows", &attn_bwd_bias_rows, py::arg("B"), py::arg("N"), py::arg("H"), py::arg("D"), py::arg("drop") = false);
   m.def("attn_dbias_reduce", &attn_dbias_reduce);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("transpose_batched", &transpose_batched);

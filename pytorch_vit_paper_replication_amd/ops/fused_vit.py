@@ -231,11 +231,12 @@ class EncoderBlockFn(torch.autograd.Function):
         gbqkv = g(bqkv)
         side_db = False
         db_part = None
-        if gbqkv is not None and ext.attn_bwd_pipe_path(B, N, H, D, aseed is not None):
-            # the pipelined attention backward emits per-(image, head, query block) column sums of dQ and
-            # dO (= the v-bias gradient; the k bias has none); only their small reduction remains (side
-            # stream), no pass over dQKV
-            db_part = torch.empty(B * H, (N + 31) // 32, 192, dtype=torch.float32, device=do.device)
+        prow = ext.attn_bwd_bias_rows(B, N, H, D, aseed is not None) if gbqkv is not None else 0
+        if prow > 0:
+            # the pipelined / chunked attention backward emits per-(image, head, query block or key
+            # chunk) column sums of dQ and dV (the v-bias gradient; the k bias has none); only their
+            # small reduction remains (side stream), no pass over dQKV
+            db_part = torch.empty(B * H, prow, 192, dtype=torch.float32, device=do.device)
             dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part)
         else:
             # other shapes: the in_proj bias gradient is a column sum of dQKV on the side stream
@@ -247,14 +248,20 @@ class EncoderBlockFn(torch.autograd.Function):
             # rides on the side stream with the weight gradients, off the dgrad chain
             if db_part is not None:
                 ext.attn_dbias_reduce(db_part, B, H, gbqkv.view(-1))
-            if side_db:
+            if side_db and aseed is None:
+                # sum_k dK = 0 (softmax rows: sum_k dS = 0 per query) and sum_k dV = sum_q dO (rows of P
+                # sum to 1): the k slice gets nothing, the v slice the column sums of dO, so two
+                # [T, D] column sums replace one over [T, 3D]
+                gemm.bias_grad(dqkv[:, :D], gbqkv[:D])
+                gemm.bias_grad(do, gbqkv[2 * D:])
+            elif side_db:
                 gemm.bias_grad(dqkv, gbqkv)
             if gwo is not None:
                 wgrad(dx1, o, gwo, 2, 1)
             if gwqkv is not None:
                 wgrad(dqkv, xn1, gwqkv, 3, 0)
 
-        store.on_side(attn_wgrads, dx1, o, dqkv, xn1, *(() if db_part is None else (db_part,)))
+        store.on_side(attn_wgrads, dx1, o, dqkv, xn1, do, *(() if db_part is None else (db_part,)))
         dxn1 = dgrad(dqkv, wqkv, 3)
         dx = torch.empty_like(dx2)
         if prev is not None:

@@ -168,8 +168,9 @@ def main():
         dor = torch.randn_like(orf)
         t_lib = timeit(lambda: torch.autograd.grad(orf, (qr, kr, vr), dor, retain_graph=True))
         print(f"attn_bwd B{B} N{N} H{H}: ours {tt:.3f} ms {2.5 * fl / tt / 1e9:.1f} TF | sdpa {t_lib:.3f} ms x{t_lib / tt:.2f}", flush=True)
-        if ext.attn_bwd_pipe_path(B, N, H, Da):
-            part = torch.empty(B * H, (N + 31) // 32, 192, device=dev, dtype=torch.float32)
+        prow = ext.attn_bwd_bias_rows(B, N, H, Da)
+        if prow > 0:
+            part = torch.empty(B * H, prow, 192, device=dev, dtype=torch.float32)
             tb = timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, sc, None, part))
             print(f"attn_bwd+dbias B{B} N{N} H{H}: ours {tb:.3f} ms (bias partials in-kernel)", flush=True)
     if "ln" in a.only:

@@ -1018,6 +1018,12 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd(1, 64, 1, 64, True),
         lambda: check_attn_bwd(1, 257, 2, 64, True),
         lambda: check_attn_bwd(1, 577, 2),
+        # generic kernel with the fused in_proj bias gradient: 3 key blocks (577), a 1-key last block
+        # (513 = 2 x 256 + 1), more pairs than CUs, 4 key blocks (1000 keys)
+        lambda: check_attn_bwd(2, 577, 3, 64, True),
+        lambda: check_attn_bwd(3, 513, 4, 64, True),
+        lambda: check_attn_bwd(150, 300, 2, 64, True),
+        lambda: check_attn_bwd(1, 1000, 2, 64, True),
         # again: the persistent dQ accumulator must have been re-zeroed by the tail launch's
         # conversion (577 = 2 x 256 + 65) and by the separate conversion pass (400 = 256 + 144)
         lambda: check_attn_bwd(2, 577, 3),
@@ -1064,6 +1070,10 @@ def all_checks() -> List[Callable[[], Result]]:
         check_adam,
         check_adam_transposed,
         lambda: check_vit_fused_vs_reference(4, False),
+        # generic attention backward in the model (N = 257 > 224, dh 64 and dh 80): the in_proj bias
+        # gradient from the dQ and dO column sums (k slice 0)
+        lambda: check_vit_fused_vs_reference(2, False, image_size=256),
+        lambda: check_vit_fused_vs_reference(2, False, image_size=224, patch_size=14, embedding_dim=320, num_heads=4),
         check_vit_inference,
         check_gemm_patch_embed_epilogue,
         lambda: check_gemm_small_splitk(6304, 768, 3072, resid=True),   # b32: 75 tiles
