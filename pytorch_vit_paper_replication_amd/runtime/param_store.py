@@ -17,7 +17,7 @@ bucketer) as soon as a group of parameters has its final gradient.
 from __future__ import annotations
 
 import weakref
-from typing import Callable, Dict, Iterable, List, Optional
+from typing import Callable, Dict, Iterable, List, Optional, Tuple
 
 import torch
 
@@ -113,6 +113,7 @@ class ParamStore:
         self._side: Optional[torch.cuda.Stream] = None
         self._side_pending = False
         self._join_queued = False
+        self._side_refs: List[Tuple[torch.cuda.Stream, Tuple[torch.Tensor, ...]]] = []  # held until join_side
         self.refresh_shadow(force=True)
 
     # ------------------------------------------------------------------ validity
@@ -278,7 +279,13 @@ class ParamStore:
 
     def on_side(self, fn: Callable[[], None], *tensors: torch.Tensor) -> None:
         """Run ``fn`` (kernel launches) on the side stream after the work queued so far on the
-        current stream; ``tensors`` are kept alive for the side stream by the caching allocator."""
+        current stream. ``tensors`` (produced on the current stream) are held until ``join_side``
+        has made that stream wait for the side stream, and only then released: the caching allocator
+        then reuses their blocks in stream order, as in a one-stream program. (``record_stream`` would
+        instead keep each block out of reuse until the GPU has passed the side-stream work, so every
+        step the host runs ahead of the GPU would hold a whole step of activations: at ViT-L/16 384 px
+        batch 128 that exhausted the 288 GB and the allocator's free-and-retry stalled steps for
+        seconds.)"""
         side = self.side_stream()
         if side is None:
             fn()
@@ -287,8 +294,7 @@ class ParamStore:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             fn()
-        for t in tensors:
-            t.record_stream(side)
+        self._side_refs.append((main, tensors))
         self._side_pending = True
         self._queue_join()
 
@@ -302,10 +308,16 @@ class ParamStore:
             self.join_side()
 
     def join_side(self) -> None:
-        """Make the current stream wait for every side-stream launch so far."""
+        """Make the current stream (and every stream that produced a held tensor) wait for every
+        side-stream launch so far, then release the held tensors."""
         self._join_queued = False
         if self._side_pending and self._side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(self._side)
+            for s in {st for st, _ in self._side_refs}:
+                if s != cur:
+                    s.wait_stream(self._side)
+            self._side_refs.clear()
             self._side_pending = False
 
     def zero_grad(self) -> None:
