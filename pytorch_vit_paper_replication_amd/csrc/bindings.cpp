@@ -1,6 +1,7 @@
 // pybind11 / ATen bindings for the gfx950 kernels. Every entry point launches on PyTorch's current
 // HIP stream (so it composes with torch streams, events and hipGraph capture) and validates dtypes,
 // shapes and strides before touching device memory.
+#include <algorithm>
 #include <map>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
@@ -23,6 +24,8 @@ struct AdamGroup {
 extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
+hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
+                                unsigned*, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
 hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, hipStream_t);
@@ -186,6 +189,28 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor w, torch
   check(pvr_layernorm_fwd(bf(x, "x"), x_row_stride, f32(w, "w"), f32(b, "b"), bf_mut(y, "y"), D, f32_mut(mean, "mean"),
                           f32_mut(rstd, "rstd"), (int)rows, (int)D, (float)eps, stream()),
         "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+// layernorm_fwd + the output's e4m3 copy q_out [rows][D] (uint8) quantized with *q_scale, amax
+// recorded into *q_amax (int32 float bits): the fp8 forward's quantize pass folded into the LayerNorm
+std::vector<torch::Tensor> layernorm_fwd_q8(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps, int64_t rows,
+                                            int64_t x_row_stride, torch::Tensor q_out, torch::Tensor q_scale, torch::Tensor q_amax) {
+  const int64_t D = w.numel();
+  auto y = torch::empty({rows, D}, x.options());
+  auto mean = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  auto rstd = torch::empty({rows}, x.options().dtype(torch::kFloat32));
+  TORCH_CHECK(x.stride(-1) == 1, "layernorm: x last dim must be contiguous");
+  TORCH_CHECK(q_out.is_cuda() && q_out.scalar_type() == torch::kUInt8 && q_out.dim() == 2 && q_out.size(0) >= rows &&
+                  q_out.size(1) >= D && q_out.stride(1) == 1 && q_out.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(q_out.data_ptr()) % 8 == 0,
+              "layernorm_fwd_q8: q_out uint8 [rows][D], 8-byte aligned rows");
+  TORCH_CHECK(q_amax.is_cuda() && q_amax.scalar_type() == torch::kInt32, "layernorm_fwd_q8: q_amax int32");
+  check(pvr_layernorm_fwd_q8(bf(x, "x"), x_row_stride, f32(w, "w"), f32(b, "b"), bf_mut(y, "y"), D,
+                             reinterpret_cast<uint8_t*>(q_out.data_ptr()), q_out.stride(0), f32(q_scale, "q_scale"),
+                             reinterpret_cast<unsigned*>(q_amax.data_ptr<int32_t>()), f32_mut(mean, "mean"), f32_mut(rstd, "rstd"),
+                             (int)rows, (int)D, (float)eps, stream()),
+        "layernorm_fwd_q8");
   return {y, mean, rstd};
 }
 
@@ -483,7 +508,8 @@ const uint8_t* u8(const torch::Tensor& t, const char* name) {
 void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, torch::Tensor C, int64_t M, int64_t N, int64_t K,
               int64_t epi, torch::Tensor scale_a, torch::Tensor scale_b, c10::optional<torch::Tensor> bias,
               c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> seed, int64_t seed_offset,
-              double drop_p, c10::optional<torch::Tensor> colsum) {
+              double drop_p, c10::optional<torch::Tensor> colsum, c10::optional<torch::Tensor> q_out,
+              c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, int64_t q_fmt) {
   pvr::GemmParams p{};
   p.drop_scale = 1.f;
   p.M = (int)M; p.N = (int)N; p.K = (int)K;
@@ -500,6 +526,25 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
   if (aux.has_value() && aux->defined()) { p.aux = const_cast<uint16_t*>(bf(*aux, "aux")); p.ld_aux = ld_of(*aux, "aux"); }
   if (epi == 1 || epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm_fp8: GELU epilogues need aux");
   if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
+  if (q_out.has_value() && q_out->defined()) {
+    // fp8 copy of the GELU / dGELU output from the register-direct epilogue (its preconditions:
+    // 16-B column groups, 31-bit offsets of every row-major operand it touches)
+    TORCH_CHECK(epi == 1 || epi == 2, "gemm_fp8: q_out with the GELU / dGELU epilogues only");
+    TORCH_CHECK(q_out->is_cuda() && q_out->scalar_type() == torch::kUInt8 && q_out->dim() == 2 && q_out->stride(1) == 1 &&
+                    q_out->size(0) >= M && q_out->size(1) >= N && q_out->stride(0) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(q_out->data_ptr()) % 8 == 0,
+                "gemm_fp8: q_out uint8 [M][N], row stride and base 8-byte aligned");
+    TORCH_CHECK(q_scale.has_value() && q_scale->defined() && q_amax.has_value() && q_amax->defined() &&
+                    q_amax->scalar_type() == torch::kInt32 && q_amax->is_cuda() && (q_fmt == 0 || q_fmt == 1),
+                "gemm_fp8: q_out needs q_scale (f32), q_amax (int32) and q_fmt 0 / 1");
+    const int64_t ld_max = std::max(std::max(p.ldc, p.ld_aux), std::max(p.ld_resid, (int64_t)N));
+    TORCH_CHECK(M * ld_max * 2 < (1ll << 31), "gemm_fp8: q_out path needs 31-bit output offsets");
+    p.q_out = reinterpret_cast<uint8_t*>(q_out->data_ptr());
+    p.ld_q = q_out->stride(0);
+    p.q_scale = f32(*q_scale, "q_scale");
+    p.q_amax = reinterpret_cast<unsigned*>(q_amax->data_ptr<int32_t>());
+    p.q_fmt = (int)q_fmt;
+  }
   if (drop_p > 0.0) {
     TORCH_CHECK(seed.has_value() && seed->defined() && seed->scalar_type() == torch::kInt64, "dropout needs an int64 seed tensor");
     p.seed_ptr = reinterpret_cast<const uint64_t*>(seed->data_ptr());
@@ -732,6 +777,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi_staged") = 0);
   m.def("num_cus", &num_cus);
   m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_fwd_q8", &layernorm_fwd_q8);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("dy_stride"), py::arg("x"), py::arg("x_stride"),
         py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),
         py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none(),
@@ -764,7 +810,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8", &gemm_fp8, py::arg("A"), py::arg("fmt_a"), py::arg("B"), py::arg("fmt_b"), py::arg("C"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("scale_a"), py::arg("scale_b"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("aux") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0,
-        py::arg("drop_p") = 0.0, py::arg("colsum") = py::none());
+        py::arg("drop_p") = 0.0, py::arg("colsum") = py::none(), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
+        py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);

@@ -279,4 +279,25 @@ PVR_DEV int xcd_remap(int bid, int nblocks) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// Two f32 -> OCP fp8 (FMT 0 e4m3fn, 1 e5m2) into byte pair HI of `old` (v_cvt_pk_fp8 / bf8_f32):
+// finite overflow saturates; a NaN stays a NaN (fminf/fmaxf would turn it into -FMAX and hide it)
+template <int FMT, bool HI>
+PVR_DEV int pack2_fp8(float a, float b, int old) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;  // OCP e4m3fn / e5m2 largest finite
+  a = a != a ? a : fminf(fmaxf(a, -FMAX), FMAX);
+  b = b != b ? b : fminf(fmaxf(b, -FMAX), FMAX);
+  if constexpr (FMT == 0)
+    return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
+  else
+    return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
+}
+// 8 f32 -> 8 fp8 bytes (little-endian order) of format fmt
+template <int FMT>
+PVR_DEV uint2 pack8_fp8(const float (&v)[8], float qs) {
+  uint2 r;
+  r.x = (uint32_t)pack2_fp8<FMT, true>(v[2] * qs, v[3] * qs, pack2_fp8<FMT, false>(v[0] * qs, v[1] * qs, 0));
+  r.y = (uint32_t)pack2_fp8<FMT, true>(v[6] * qs, v[7] * qs, pack2_fp8<FMT, false>(v[4] * qs, v[5] * qs, 0));
+  return r;
+}
+
 }  // namespace pvr

@@ -15,18 +15,6 @@
 namespace pvr {
 namespace {
 
-template <int FMT, bool HI>
-PVR_DEV int pack2_fp8(float a, float b, int old) {
-  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;  // OCP e4m3fn / e5m2 largest finite
-  // saturate finite overflow; a NaN stays a NaN (fminf/fmaxf would turn it into -FMAX and hide it)
-  a = a != a ? a : fminf(fmaxf(a, -FMAX), FMAX);
-  b = b != b ? b : fminf(fmaxf(b, -FMAX), FMAX);
-  if constexpr (FMT == 0)
-    return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
-  else
-    return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
-}
-
 // 16 elements (two 16-B bf16 loads, one 16-B fp8 store) per thread and grid-stride step.
 template <int FMT>
 __global__ void __launch_bounds__(256) quant_kernel(const uint16_t* __restrict__ x, int64_t ldx, uint8_t* __restrict__ y, int64_t ldy,

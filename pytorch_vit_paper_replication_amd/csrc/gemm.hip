@@ -953,6 +953,7 @@ __host__ __device__ inline bool direct_ok(const GemmParams& p) {
 template <int EPI, bool RES, bool SCALED = false>
 PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, int mb, int nb, int wm, int wn, int lane) {
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  typedef uint32_t v2u_q __attribute__((ext_vector_type(2)));
   const int li = lane & 15, g = lane >> 4;
   const float deq = SCALED ? (*p.scale_a) * (*p.scale_b) : 1.f;  // fp8 operands: per-tensor dequant
   // rows [mb, min(M, mb + 128)) of C (and of the residual / aux tensors) from the wave's first row
@@ -1002,6 +1003,13 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   // of being paid per fragment row. Row offsets go into the VGPR offset: the SGPR offset of a
   // buffer access is outside its range check, so rows past M would be accessed.
   constexpr bool HAS_IN = (EPI == EPI_BF16 && RES) || EPI == EPI_DGELU;
+  // fp8 copy of the GELU / dGELU output (fp8 GEMMs only): 8 bytes per lane and fragment row
+  constexpr bool QOK = SCALED && (EPI == EPI_GELU || EPI == EPI_DGELU);
+  const bool qon = QOK && p.q_out != nullptr;
+  const __amdgpu_buffer_rsrc_t qrs = make_rsrc(qon ? p.q_out + (int64_t)mb * p.ld_q : p.q_out,
+                                               qon && rows ? (uint32_t)((int64_t)(rows - 1) * p.ld_q + p.N) : 0u);
+  const float qsc = qon ? *p.q_scale : 1.f;
+  float qam = 0.f;
   v4u xin_all[HAS_IN ? 8 : 1][2];
   if constexpr (HAS_IN) {
 #pragma unroll
@@ -1071,6 +1079,8 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
           d2 *= s2;
           out[q] = pack2bf(g2.x, g2.y);
           ax[q] = pack2bf(d2.x, d2.y);
+          v[2 * q] = g2.x;  // the output, for the fp8 copy
+          v[2 * q + 1] = g2.y;
         }
         __builtin_amdgcn_raw_buffer_store_b128(ax, xrs, vx[jp] + so_x, 0, 0);  // no aux (inference): 0-byte resource
       } else {  // EPI_DGELU
@@ -1085,6 +1095,16 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         for (int q = 0; q < 4; ++q) out[q] = pack2bf(v[2 * q], v[2 * q + 1]);
       }
       __builtin_amdgcn_raw_buffer_store_b128(out, crs, vc[jp] + so_c, 0, 0);
+      if constexpr (QOK) {
+        if (qon) {
+          // rows past M / columns past N: out-of-range offset (dropped); their values are 0 anyway
+          const uint32_t vq = c0[jp] < p.N ? (uint32_t)((int64_t)(16 * i + li) * p.ld_q + c0[jp]) : OOB;
+          const uint2 q8 = p.q_fmt ? pack8_fp8<1>(v, qsc) : pack8_fp8<0>(v, qsc);
+          __builtin_amdgcn_raw_buffer_store_b64((v2u_q){q8.x, q8.y}, qrs, vq, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) qam = nan_max(qam, fabsf(v[e]));
+        }
+      }
     }
   }
   if constexpr (EPI == EPI_DGELU) {
@@ -1118,6 +1138,25 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
           const float mine = wm == 0 ? csum[0][e] : csum[1][e];
           __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(mine + red[jp * 128 + wn * 32 + (c0[jp] - nb - 32 * jp) + e], srs, vo + 4 * e, 0, 0);
         }
+      }
+    }
+  }
+  if constexpr (QOK) {
+    if (qon) {
+      // max |out| of the workgroup's tile: waves -> LDS (past the colsum exchange area), one atomic
+      // per workgroup (same-address atomics serialise at L2)
+      qam = wave_max_nan(qam);
+      float* qred = (float*)(smem + 2048);
+      const int w = (int)(threadIdx.x >> 6);
+      if (lane == 0) qred[w] = qam;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // raw barrier: the output stores stay in flight
+      asm volatile("" ::: "memory");
+      if (threadIdx.x == 0) {
+        float b = qred[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) b = nan_max(b, qred[k]);
+        if (!(b <= 0.f)) atomicMax(p.q_amax, __float_as_uint(b));
       }
     }
   }

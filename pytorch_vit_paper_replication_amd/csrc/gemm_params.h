@@ -28,6 +28,10 @@ struct GemmParams {
   // EPI_F32_STORE with split-K (tile 14): split z writes its partial to C + z * split_stride
   int64_t split_stride;
   int epi_staged;  // A/B: ping-pong bf16 epilogues through LDS (1) instead of register-direct (0)
+  // optional fp8 copy of a GELU / dGELU output written by the fp8 GEMM's epilogue (the producer-side
+  // quantization of the delayed-scaling recipe): q_out[m][n] = fp8(out * (*q_scale)) (fmt 0 e4m3,
+  // 1 e5m2, row stride ld_q bytes), *q_amax = max(*q_amax, max |out|) (float bits, NaN-propagating)
+  uint8_t* q_out; int64_t ld_q; const float* q_scale; unsigned* q_amax; int q_fmt;
 };
 
 }  // namespace pvr

@@ -80,6 +80,94 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const uint16_t* __restrict_
   }
 }
 
+// The same forward plus the output's e4m3 copy for an fp8 GEMM (producer-side quantization of the
+// delayed-scaling recipe): yq = fp8(y * qscale), *amax = max(*amax, max|y|). Rows are grid-strided
+// over a capped grid so the workgroups' same-address amax atomics (one each) stay few.
+template <int MAXCH>
+__global__ void __launch_bounds__(256) ln_fwd_q8_kernel(const uint16_t* __restrict__ x, int64_t x_stride,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        uint16_t* __restrict__ y, int64_t y_stride, uint8_t* __restrict__ yq,
+                                                        int64_t q_stride, const float* __restrict__ qscale,
+                                                        unsigned* __restrict__ amax, float* __restrict__ mean_out,
+                                                        float* __restrict__ rstd_out, int rows, int D, float eps) {
+  __shared__ float wm[4];
+  const int lane = threadIdx.x & 63;
+  const int nch = D >> 3;
+  const float qs = *qscale;
+  float am = 0.f;
+  for (int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const uint16_t* xr = x + (int64_t)row * x_stride;
+    float v[MAXCH][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        const uint4 q = *(const uint4*)(xr + c * 8);
+        const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[i][2 * j] = bf2f(u[j] & 0xFFFF);
+          v[i][2 * j + 1] = bf2f(u[j] >> 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[i][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+      }
+    }
+    const float mean = wave_sum(s) / D;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[i][j] - mean;
+          ss += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+    uint16_t* yr = y + (int64_t)row * y_stride;
+    uint8_t* qr = yq + (int64_t)row * q_stride;
+#pragma unroll
+    for (int i = 0; i < MAXCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        const float4 w0 = *(const float4*)(w + c * 8), w1 = *(const float4*)(w + c * 8 + 4);
+        const float4 b0 = *(const float4*)(b + c * 8), b1 = *(const float4*)(b + c * 8 + 4);
+        const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = (v[i][j] - mean) * rstd * ww[j] + bb[j];
+          am = nan_max(am, fabsf(o[j]));
+        }
+        uint4 q;
+        q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
+        q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
+        *(uint4*)(yr + c * 8) = q;
+        *(uint2*)(qr + c * 8) = pack8_fp8<0>(o, qs);
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+  am = wave_max_nan(am);
+  if (lane == 0) wm[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = nan_max(nan_max(wm[0], wm[1]), nan_max(wm[2], wm[3]));
+    if (!(m <= 0.f)) atomicMax(amax, __float_as_uint(m));
+  }
+}
+
 PVR_DEV void load8(const uint16_t* p, float* o) {
   const uint4 q = *(const uint4*)p;
   const uint32_t u[4] = {q.x, q.y, q.z, q.w};
@@ -282,6 +370,26 @@ extern "C" hipError_t pvr_layernorm_fwd(const uint16_t* x, int64_t x_stride, con
     case 2: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
     case 3: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
     default: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, mean, rstd, rows, D, eps); break;
+  }
+  return hipGetLastError();
+}
+
+// pvr_layernorm_fwd plus the e4m3 copy yq (row stride q_stride bytes) with scale *qscale and the
+// amax record (see ln_fwd_q8_kernel)
+extern "C" hipError_t pvr_layernorm_fwd_q8(const uint16_t* x, int64_t x_stride, const float* w, const float* b, uint16_t* y,
+                                           int64_t y_stride, uint8_t* yq, int64_t q_stride, const float* qscale, unsigned* amax,
+                                           float* mean, float* rstd, int rows, int D, float eps, hipStream_t s) {
+  using namespace pvr;
+  if (rows <= 0) return hipSuccess;
+  if (D % 8 != 0 || D > 2048 || q_stride % 8 != 0) return hipErrorInvalidValue;
+  int nblk = (rows + 3) / 4;
+  if (nblk > 1024) nblk = 1024;
+  const dim3 grid(nblk), block(256);
+  switch ((D / 8 + 63) / 64) {
+    case 1: hipLaunchKernelGGL(ln_fwd_q8_kernel<1>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, yq, q_stride, qscale, amax, mean, rstd, rows, D, eps); break;
+    case 2: hipLaunchKernelGGL(ln_fwd_q8_kernel<2>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, yq, q_stride, qscale, amax, mean, rstd, rows, D, eps); break;
+    case 3: hipLaunchKernelGGL(ln_fwd_q8_kernel<3>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, yq, q_stride, qscale, amax, mean, rstd, rows, D, eps); break;
+    default: hipLaunchKernelGGL(ln_fwd_q8_kernel<4>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, yq, q_stride, qscale, amax, mean, rstd, rows, D, eps); break;
   }
   return hipGetLastError();
 }

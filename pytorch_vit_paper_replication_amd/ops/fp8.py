@@ -69,6 +69,12 @@ class Fp8Meta:
         ext.fp8_quant(x, y, self.qscale[slot:slot + 1], am, self.fmt)
         return y, self.dscale[slot:slot + 1]
 
+    def producer(self, slot: int) -> Optional[Tuple["Fp8Meta", int]]:
+        """(self, slot) if the slot is calibrated, so the kernel producing the tensor can write its fp8
+        copy with the slot's delayed scale and record its amax (``quant=`` of the fp8 GEMMs); None on the
+        tensor's first step, which goes through ``quantize`` (amax pass, then quantize)."""
+        return (self, slot) if self.calibrated[slot] else None
+
 
 class Fp8State:
     """Per-model fp8 state: activation slots (4 per encoder block) + weight cache."""
@@ -101,6 +107,12 @@ class Fp8State:
 
     def grad_quant(self, g: torch.Tensor, block: int, which: int) -> Tuple[torch.Tensor, torch.Tensor]:
         return self.grad.quantize(g, block * self.ACT_PER_BLOCK + which)
+
+    def act_producer(self, block: int, which: int):
+        return self.act.producer(block * self.ACT_PER_BLOCK + which)
+
+    def grad_producer(self, block: int, which: int):
+        return self.grad.producer(block * self.ACT_PER_BLOCK + which)
 
     def wgrad_ready(self, block: int, which_grad: int, which_act: int) -> bool:
         """fp8 weight gradient of (grad slot, activation slot) possible: both slots calibrated (the
@@ -181,31 +193,59 @@ class Fp8State:
         self._batch_gen = generation
 
 
+def _quant_args(quant, rows: int, cols: int, device):
+    """``quant=(meta, slot)`` of the fp8 GEMMs -> (gemm_fp8 kwargs, (fp8 copy, dequant scale))."""
+    if quant is None:
+        return {}, None
+    meta, slot = quant
+    q = torch.empty(rows, cols, dtype=torch.uint8, device=device)
+    kw = dict(q_out=q, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1], q_fmt=meta.fmt)
+    return kw, (q, meta.dscale[slot:slot + 1])
+
+
+def layernorm_fwd_q8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, quant):
+    """LayerNorm forward that also writes the output's e4m3 copy with a calibrated slot's delayed scale
+    (``quant=(meta, slot)``, ``Fp8Meta.producer``) and records its amax:
+    returns ``(y, mean, rstd, (y_fp8, dequant scale))``."""
+    meta, slot = quant
+    T, D = x.shape
+    q = torch.empty(T, D, dtype=torch.uint8, device=x.device)
+    y, mean, rstd = _ext.ext().layernorm_fwd_q8(x, w, b, eps, T, D, q, meta.qscale[slot:slot + 1], meta.amax[slot:slot + 1])
+    return y, mean, rstd, (q, meta.dscale[slot:slot + 1])
+
+
 def linear_fwd_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
                    bias: Optional[torch.Tensor] = None, *, resid: Optional[torch.Tensor] = None, drop=None,
-                   gelu_aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y = resid + dropout(dequant(xq . wq^T) + bias), or the GELU variant (see gemm.linear_fwd)."""
+                   gelu_aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, quant=None):
+    """y = resid + dropout(dequant(xq . wq^T) + bias), or the GELU variant (see gemm.linear_fwd).
+
+    ``quant=(meta, slot)`` (GELU variant, a calibrated slot: ``Fp8Meta.producer``): the epilogue also
+    writes y's fp8 copy with the slot's delayed scale and records y's amax, so the next GEMM needs no
+    quantize pass; returns ``(y, (y_fp8, dequant scale))`` then."""
     T, K = xq.shape
     N = wq.shape[0]
     if out is None:
         out = torch.empty(T, N, dtype=torch.bfloat16, device=xq.device)
     seed, soff, p = gemm._drop_args(drop)
     epi = gemm.EPI_GELU if gelu_aux is not None else gemm.EPI_BF16
-    _ext.ext().gemm_fp8(xq, E4M3, wq, E4M3, out, T, N, K, epi, xs, ws, bias, resid, gelu_aux, seed, soff, p)
-    return out
+    kw, q = _quant_args(quant, T, N, xq.device)
+    _ext.ext().gemm_fp8(xq, E4M3, wq, E4M3, out, T, N, K, epi, xs, ws, bias, resid, gelu_aux, seed, soff, p, **kw)
+    return out if quant is None else (out, q)
 
 
 def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts: torch.Tensor, *,
                      dgelu_aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
-                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dx = dequant(gq (e5m2) . wtq^T (e4m3, W^T rows)) [* dgelu_aux]."""
+                     out: Optional[torch.Tensor] = None, quant=None):
+    """dx = dequant(gq (e5m2) . wtq^T (e4m3, W^T rows)) [* dgelu_aux]; ``quant`` as in linear_fwd_fp8
+    (dGELU variant: the e5m2 copy of dx for the next dgrad GEMM)."""
     T, N = gq.shape
     K = wtq.shape[0]
     if out is None:
         out = torch.empty(T, K, dtype=torch.bfloat16, device=gq.device)
     epi = gemm.EPI_DGELU if dgelu_aux is not None else gemm.EPI_BF16
-    _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum)
-    return out
+    kw, q = _quant_args(quant, T, K, gq.device)
+    _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum, **kw)
+    return out if quant is None else (out, q)
 
 
 def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torch.Tensor, x_meta: "Fp8Meta", x_slot: int,

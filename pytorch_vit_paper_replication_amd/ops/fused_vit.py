@@ -129,7 +129,13 @@ class EncoderBlockFn(torch.autograd.Function):
         need_bwd = getattr(store, "grad_enabled", True) and any(ctx.needs_input_grad)
         u = (torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
              if need_bwd or f8 is not None else None)
-        xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
+        q1 = f8[0].act_producer(f8[1], 0) if f8 is not None else None
+        if q1 is not None:  # fp8 forward, calibrated: xn1's e4m3 copy from the LayerNorm itself
+            from . import fp8 as F8
+
+            xn1, mean1, rstd1, xq1 = F8.layernorm_fwd_q8(x, ln1w, ln1b, eps1, q1)
+        else:
+            xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
         if f8 is None:
             qkv = gemm.linear_fwd(xn1, store.bf16(wqkv), bqkv)
             o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
@@ -146,15 +152,23 @@ class EncoderBlockFn(torch.autograd.Function):
             gen = store.generation
             lay = store.layout_key()
             wq = [st.weight(store.bf16(w), id(w), gen, lay) for w in (wqkv, wo, w1, w2)]
-            a, s_ = st.act_quant(xn1, blk, 0)
+            a, s_ = xq1 if q1 is not None else st.act_quant(xn1, blk, 0)
             qkv = F8.linear_fwd_fp8(a, s_, *wq[0], bqkv)
             o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
             a, s_ = st.act_quant(o, blk, 1)
             x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
-            xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
-            a, s_ = st.act_quant(xn2, blk, 2)
-            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1)
-            a, s_ = st.act_quant(h, blk, 3)
+            q2 = st.act_producer(blk, 2)
+            if q2 is not None:
+                xn2, mean2, rstd2, (a, s_) = F8.layernorm_fwd_q8(x1, ln2w, ln2b, eps2, q2)
+            else:
+                xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
+                a, s_ = st.act_quant(xn2, blk, 2)
+            hq = st.act_producer(blk, 3)  # h's e4m3 copy from the fc1 epilogue (calibrated slot)
+            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq)
+            if hq is not None:
+                h, (a, s_) = h
+            else:
+                a, s_ = st.act_quant(h, blk, 3)
             x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
         if need_bwd:
             ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
@@ -174,15 +188,21 @@ class EncoderBlockFn(torch.autograd.Function):
         own, prev = ctx.links
         f8d = ctx.f8d
 
+        pre_q = {}  # grad slot -> (e5m2 copy, dequant scale) written by the producing dgrad epilogue
+
         def dgrad(dy, w, which, dgelu_aux=None, colsum=None):
             wt = store.bf16_t(w)
             if f8d is not None and wt is not None:
                 from . import fp8 as F8
 
                 st, blk = f8d
-                gq, gs = st.grad_quant(dy, blk, which)
+                gq, gs = pre_q.pop(which) if which in pre_q else st.grad_quant(dy, blk, which)
                 wq, ws = st.weight(wt, ~id(w), store.generation, store.layout_key())
-                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum)
+                # the dGELU dgrad (fc2) also writes dU's e5m2 copy for the fc1 dgrad (grad slot 1)
+                nq = st.grad_producer(blk, 1) if dgelu_aux is not None else None
+                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq)
+                if nq is not None:
+                    out, pre_q[1] = out
             else:
                 out = gemm.linear_dgrad(dy, store.bf16(w), dgelu_aux=dgelu_aux, wt=wt, colsum=colsum)
             if DGRAD_TAP is not None:

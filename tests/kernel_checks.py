@@ -522,6 +522,75 @@ def check_gemm_fp8(M, N, K, resid=False, gelu=False):
     return (f"gemm_fp8 e4m3 M{M} N{N} K{K} r{int(resid)} g{int(gelu)}", m, lim(3.5e-3, 6e-3, bf16_l2=6.5e-2))
 
 
+def _fp8_code_dist(q: torch.Tensor, ref: torch.Tensor) -> float:
+    """Largest distance between two fp8 byte tensors in representable steps (sign-magnitude codes:
+    adjacent magnitudes are one step apart; a sign flip counts the steps through zero)."""
+    a, b = q.to(torch.int32), ref.to(torch.int32)
+    sa = torch.where(a & 0x80 != 0, -(a & 0x7F), a & 0x7F)
+    sb = torch.where(b & 0x80 != 0, -(b & 0x7F), b & 0x7F)
+    return (sa - sb).abs().max().item()
+
+
+def check_gemm_fp8_producer(M, N, K, dgelu=False):
+    """Producer-side quantization: the fp8 GEMM's GELU (e4m3) / dGELU (e5m2) epilogue writes the
+    output's fp8 copy with a slot's scale and records its amax. Against the quantize pass over the
+    bf16 output with the same scale: decoded values (differences only where the epilogue rounds the
+    fp32 value and the pass the bf16 one: at most one fp8 step), the amax (bf16 rounding of the
+    output at most), and the bf16 output itself is bit-identical to the GEMM without the copy."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    x, w = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05))
+    xq, xs, _ = _fp8_operand(x, 1 if dgelu else 0)  # dgrad: e5m2 gradient operand
+    wq, ws, _ = _fp8_operand(w)
+    fmt = F8.E5M2 if dgelu else F8.E4M3
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=fmt)
+    meta.calibrated[0] = True
+    meta.qscale.fill_(3.0 if dgelu else 40.0)
+    meta.dscale.copy_(1.0 / meta.qscale)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    if dgelu:
+        aux.copy_(bf(torch.rand(M, N, device=DEV) * 1.1))
+        plain = F8.linear_dgrad_fp8(xq, xs, wq, ws, dgelu_aux=aux)
+        y, (q, ds) = F8.linear_dgrad_fp8(xq, xs, wq, ws, dgelu_aux=aux, quant=meta.producer(0))
+    else:
+        b = rnd(N)
+        plain = F8.linear_fwd_fp8(xq, xs, wq, ws, b, gelu_aux=aux)
+        y, (q, ds) = F8.linear_fwd_fp8(xq, xs, wq, ws, b, gelu_aux=aux, quant=meta.producer(0))
+    ref = torch.empty(M, N, dtype=torch.uint8, device=DEV)
+    scratch = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ext.fp8_quant(y, ref, meta.qscale[0:1], scratch, fmt)
+    amax = meta.amax.view(torch.float32)[0].item()
+    m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
+         "amax_rel": abs(amax - y.float().abs().max().item()) / y.float().abs().max().item(),
+         "bf16_not_identical": float(not torch.equal(y, plain))}
+    return (f"gemm_fp8 producer quant {'dgelu e5m2' if dgelu else 'gelu e4m3'} M{M} N{N} K{K}", m,
+            {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "bf16_not_identical": 0})
+
+
+def check_layernorm_fwd_q8(T=3000, D=1280):
+    """LayerNorm forward with the fused e4m3 copy: y, mean, rstd bit-identical to the plain forward;
+    the copy within one fp8 step of quantizing y (fp32 vs bf16-rounded input) and amax = max|y|."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    x = bf(rnd(T, D) * 2 + 0.5)
+    w, b = rnd(D) * 0.5 + 1.0, rnd(D) * 0.1
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+    meta.calibrated[0] = True
+    meta.qscale.fill_(60.0)
+    meta.dscale.copy_(1.0 / meta.qscale)
+    y0, m0, r0 = ext.layernorm_fwd(x, w, b, 1e-6, T, D)
+    y, m1, r1, (q, ds) = F8.layernorm_fwd_q8(x, w, b, 1e-6, meta.producer(0))
+    ref = torch.empty(T, D, dtype=torch.uint8, device=DEV)
+    ext.fp8_quant(y, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), 0)
+    amax = meta.amax.view(torch.float32)[0].item()
+    m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
+         "amax_rel": abs(amax - y.float().abs().max().item()) / y.float().abs().max().item(),
+         "ln_not_identical": float(not (torch.equal(y, y0) and torch.equal(m0, m1) and torch.equal(r0, r1)))}
+    return (f"layernorm_fwd_q8 T{T} D{D}", m, {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "ln_not_identical": 0})
+
+
 def check_wgrad_fp8(T, N, K):
     """dW = dequant(dy^T (e5m2) . x (e4m3)) from the transposed quantize passes + split-K fp8 GEMM,
     against the exact product of the same quantized operands and against bf16."""
@@ -1058,6 +1127,10 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_fp8(700, 2304, 768, True, False),
         lambda: check_gemm_fp8(520, 3072, 384, False, True),
         lambda: check_dgrad_fp8(1030, 1280, 768),
+        lambda: check_gemm_fp8_producer(1000, 1280, 512),
+        check_layernorm_fwd_q8,
+        lambda: check_layernorm_fwd_q8(50, 768),
+        lambda: check_gemm_fp8_producer(1030, 768, 1280, True),
         check_vit_fp8,
         check_vit_fp8_dgrad,
         check_vit_fp8_wgrad,
