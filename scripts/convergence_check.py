@@ -45,7 +45,9 @@ def run(path, args, init_sd, data):
                 mlp_dropout=args.dropout, embedding_dropout=args.dropout).to(dev)
     model.load_state_dict(init_sd)
     if path == "fused_fp8":
-        model.enable_fp8()  # e4m3 forward, e5m2-gradient dgrad + wgrad GEMMs, delayed scaling
+        model.enable_fp8()  # e4m3 forward, e5m2-gradient dgrad GEMMs, delayed scaling (wgrad bf16)
+    elif path == "fused_fp8w":
+        model.enable_fp8(dgrad=True, wgrad=True)  # + e5m2 x e4m3 weight-gradient GEMMs
     groups = param_groups_weight_decay(model, 0.03)
     opt = FusedAdam(groups, lr=args.lr) if fused else torch.optim.Adam(groups, lr=args.lr)
     sched = warmup_linear_decay(opt, args.steps, 0.05)
@@ -121,7 +123,12 @@ def main():
     p.add_argument("--fp8", action="store_true", help="also train the fused path with enable_fp8() (fp8 GEMMs)")
     p.add_argument("--no-reference", action="store_true",
                    help="skip the two PyTorch paths (large models: fused bf16 vs fused fp8 only)")
+    p.add_argument("--fp8-study", type=int, default=0, metavar="SEEDS",
+                   help="seed study: SEEDS inits x {fused bf16, fp8 fwd+dgrad, fp8 fwd+dgrad+wgrad}; prints the "
+                        "per-variant mean / spread of the final loss and held-out accuracy")
     args = p.parse_args()
+    if args.fp8_study:
+        return fp8_study(args)
 
     from pytorch_vit_paper_replication_amd import _ext
     from pytorch_vit_paper_replication_amd.models import vit
@@ -152,6 +159,48 @@ def main():
         summary["fused_fp8"] = {"first": f8["losses"][0], "last10pct_mean": sum(f8["losses"][-k:]) / k,
                                 "test_loss": f8["test_loss"], "test_acc": f8["test_acc"], "train_s": f8["train_s"],
                                 "max_abs_loss_diff_vs_fused_first50": max(abs(a - b) for a, b in zip(f8["losses"][:50], lf[:50]))}
+    print(json.dumps(summary), flush=True)
+
+
+def fp8_study(args):
+    """Learning-phase parity of the fp8 paths: for each seed, the same init and batch order through the
+    fused bf16 path, fp8 forward + dgrad (ViT.enable_fp8 default) and fp8 forward + dgrad + wgrad; the
+    question is whether each fp8 variant's final loss / held-out accuracy falls inside the bf16 seed
+    spread."""
+    from pytorch_vit_paper_replication_amd import _ext
+    from pytorch_vit_paper_replication_amd.models import vit
+
+    assert torch.cuda.is_available(), "GPU script"
+    _ext.ext()
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(0)
+    g = args.image_size // 16
+    templates = F.interpolate(torch.rand(args.classes, 3, g, g, generator=gen, device=dev),
+                              size=(args.image_size, args.image_size), mode="nearest")
+    tr = make_data(args.train_size, args.classes, args.image_size, gen, dev, templates)
+    te = make_data(args.test_size, args.classes, args.image_size, gen, dev, templates)
+    k = max(1, args.steps // 10)
+    res = {v: [] for v in ("fused", "fused_fp8", "fused_fp8w")}
+    for seed in range(args.fp8_study):
+        torch.manual_seed(seed)
+        init_sd = {n: t.clone() for n, t in vit(args.model, image_size=args.image_size, num_classes=args.classes,
+                                               mlp_dropout=args.dropout, embedding_dropout=args.dropout).state_dict().items()}
+        perm = torch.randperm(tr[0].shape[0], generator=torch.Generator().manual_seed(seed)).to(dev)
+        data = ((tr[0][perm], tr[1][perm]), te)
+        for v in res:
+            r = run(v, args, init_sd, data)
+            res[v].append({"final_loss": sum(r["losses"][-k:]) / k, "test_acc": r["test_acc"], "test_loss": r["test_loss"]})
+            print(f"[study] seed {seed} {v}: final loss {res[v][-1]['final_loss']:.4f} test acc {r['test_acc']:.3f} "
+                  f"test loss {r['test_loss']:.4f}", flush=True)
+
+    def stats(xs):
+        m = sum(xs) / len(xs)
+        return {"mean": round(m, 4), "min": round(min(xs), 4), "max": round(max(xs), 4),
+                "std": round((sum((x - m) ** 2 for x in xs) / max(1, len(xs) - 1)) ** 0.5, 4)}
+
+    summary = {"model": args.model, "steps": args.steps, "batch": args.batch, "lr": args.lr, "seeds": args.fp8_study}
+    for v, rs in res.items():
+        summary[v] = {key: stats([r[key] for r in rs]) for key in ("final_loss", "test_acc", "test_loss")}
     print(json.dumps(summary), flush=True)
 
 
