@@ -55,6 +55,7 @@ hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, i
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
 hipError_t pvr_fp8_quant_t(const uint16_t*, int64_t, uint8_t*, int64_t, int, int, const float*, int, hipStream_t);
+hipError_t pvr_fp8_transpose(const uint8_t*, int64_t, uint8_t*, int64_t, int, int, hipStream_t);
 hipError_t pvr_fp8_quant_multi(const int64_t*, int, int64_t, const float*, unsigned*, int, int, hipStream_t);
 int pvr_attn_bwd_key_blocks(int);
 int pvr_attn_bwd_needs_dq_acc(int, int, int, int);
@@ -571,6 +572,20 @@ void fp8_quant_t(torch::Tensor x, torch::Tensor yt, torch::Tensor qscale, int64_
         "fp8_quant_t");
 }
 
+// yT[cols][ldy] = x8^T (fp8 bytes), zero past x8's rows: the transposed wgrad operand from a row-major fp8 copy
+void fp8_transpose(torch::Tensor x8, torch::Tensor yt) {
+  TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == torch::kUInt8 && x8.dim() == 2 && x8.stride(1) == 1 && x8.stride(0) % 16 == 0 &&
+                  x8.size(1) % 16 == 0 && reinterpret_cast<uintptr_t>(x8.data_ptr()) % 16 == 0,
+              "fp8_transpose: x8 uint8 [rows][cols], cols and row stride multiples of 16, 16-byte aligned");
+  TORCH_CHECK(yt.is_cuda() && yt.scalar_type() == torch::kUInt8 && yt.dim() == 2 && yt.size(0) == x8.size(1) &&
+                  yt.size(1) >= x8.size(0) && yt.stride(1) == 1 && yt.stride(0) % 64 == 0 && yt.size(1) == yt.stride(0) &&
+                  reinterpret_cast<uintptr_t>(yt.data_ptr()) % 16 == 0,
+              "fp8_transpose: yT uint8 [cols][>= rows], row stride a multiple of 64");
+  check(pvr_fp8_transpose(x8.data_ptr<uint8_t>(), x8.stride(0), yt.data_ptr<uint8_t>(), yt.stride(0), (int)x8.size(0), (int)x8.size(1),
+                          stream()),
+        "fp8_transpose");
+}
+
 // fp8 weight gradient partials: ws[s][N][K] = dscale_a * dscale_b * A8[N][Ks] . B8[K][Ks]^T over split s
 // of the (padded) token dim, A e5m2 (gradient^T), B e4m3 (activation^T)
 void gemm_fp8_wgrad(torch::Tensor A8, torch::Tensor B8, torch::Tensor ws, int64_t N, int64_t K, int64_t Tp, torch::Tensor scale_a,
@@ -812,6 +827,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("resid") = py::none(), py::arg("aux") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0,
         py::arg("drop_p") = 0.0, py::arg("colsum") = py::none(), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
         py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0);
+  m.def("fp8_transpose", &fp8_transpose);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);

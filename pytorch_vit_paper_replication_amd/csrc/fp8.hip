@@ -186,6 +186,35 @@ __global__ void __launch_bounds__(256) quant_t_kernel(const uint16_t* __restrict
   *(int4*)(y + (int64_t)(c0 + c) * ldy + t0 + tt) = make_int4(o[0], o[1], o[2], o[3]);
 }
 
+// Byte transpose of an fp8 tensor: x8 [T][C] (row stride ldx bytes) -> y [C][ldy], zero for
+// T <= t < ldy. The weight-gradient GEMM's transposed operands from the row-major fp8 copies the
+// forward / dgrad GEMMs already use (same slot, same scale: the bytes are exactly the transposing
+// quantize pass's), so the pass reads 1 byte per element instead of 2. 64 x 64 tiles through LDS.
+__global__ void __launch_bounds__(256) transpose8_kernel(const uint8_t* __restrict__ x, int64_t ldx, uint8_t* __restrict__ y,
+                                                         int64_t ldy, int T, int C) {
+  __shared__ uint8_t tile[64][64 + 4];
+  const int t0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  {  // load: row t0 + tid/4, cols c0 + 16 (tid%4) .. +15
+    const int r = tid >> 2, cc = (tid & 3) * 16;
+    const int t = t0 + r;
+    uint4 a = make_uint4(0u, 0u, 0u, 0u);
+    if (t < T && c0 + cc < C) a = *(const uint4*)(x + (int64_t)t * ldx + c0 + cc);  // C % 16 == 0 (host check)
+    uint32_t* d = (uint32_t*)&tile[r][cc];
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+  }
+  __syncthreads();
+  // store: output row c0 + tid/4, t range t0 + 16 (tid%4) .. +15
+  const int c = tid >> 2, tt = (tid & 3) * 16;
+  if (c0 + c >= C || t0 + tt >= ldy) return;
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = (uint32_t)tile[tt + 4 * q][c] | ((uint32_t)tile[tt + 4 * q + 1][c] << 8) | ((uint32_t)tile[tt + 4 * q + 2][c] << 16) |
+           ((uint32_t)tile[tt + 4 * q + 3][c] << 24);
+  *(uint4*)(y + (int64_t)(c0 + c) * ldy + t0 + tt) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // fp8 -> f32 (tests / debugging): y[i] = dscale * x[i]
 template <int FMT>
 __global__ void dequant_kernel(const uint8_t* __restrict__ x, float* __restrict__ y, int64_t n, const float* __restrict__ dscale) {
@@ -268,6 +297,15 @@ extern "C" hipError_t pvr_fp8_quant_t(const uint16_t* x, int64_t ldx, uint8_t* y
     hipLaunchKernelGGL(quant_t_kernel<0>, grid, dim3(256), 0, s, x, ldx, y, ldy, T, C, qscale);
   else
     hipLaunchKernelGGL(quant_t_kernel<1>, grid, dim3(256), 0, s, x, ldx, y, ldy, T, C, qscale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_fp8_transpose(const uint8_t* x, int64_t ldx, uint8_t* y, int64_t ldy, int T, int C, hipStream_t s) {
+  using namespace pvr;
+  if (T <= 0 || C <= 0) return hipSuccess;
+  if (C % 16 || ldx % 16 || ldy % 64 || ldy < T) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(ldy / 64), (unsigned)((C + 63) / 64));
+  hipLaunchKernelGGL(transpose8_kernel, grid, dim3(256), 0, s, x, ldx, y, ldy, T, C);
   return hipGetLastError();
 }
 

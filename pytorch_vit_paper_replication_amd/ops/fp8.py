@@ -121,9 +121,9 @@ class Fp8State:
                 and self.act.calibrated[block * self.ACT_PER_BLOCK + which_act])
 
     def linear_wgrad(self, dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, block: int, which_grad: int,
-                     which_act: int) -> torch.Tensor:
+                     which_act: int, dy8: Optional[torch.Tensor] = None, x8: Optional[torch.Tensor] = None) -> torch.Tensor:
         n = self.ACT_PER_BLOCK
-        return linear_wgrad_fp8(dy, self.grad, block * n + which_grad, x, self.act, block * n + which_act, out)
+        return linear_wgrad_fp8(dy, self.grad, block * n + which_grad, x, self.act, block * n + which_act, out, dy8, x8)
 
     def weight(self, w16: torch.Tensor, key: int, generation: int, layout=None) -> Tuple[torch.Tensor, torch.Tensor]:
         """fp8 (e4m3, current scaling) copy of a bf16 weight shadow, cached per store generation.
@@ -249,21 +249,29 @@ def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts:
 
 
 def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torch.Tensor, x_meta: "Fp8Meta", x_slot: int,
-                     out: torch.Tensor) -> torch.Tensor:
+                     out: torch.Tensor, dy8: Optional[torch.Tensor] = None, x8: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[N, K] += dequant(dy^T (e5m2) . x (e4m3)) over the tokens: the weight gradient in fp8.
 
-    Both operands are quantized TRANSPOSED ([features][tokens], the token dim padded to 128 with
-    zeros) with their slots' current delayed scales (the slots' amax is recorded by the
-    non-transposed passes of the same tensors), then the k-contiguous fp8 ping-pong GEMM runs
-    split-K over tokens into a workspace, reduced into ``out`` in a fixed order (deterministic)."""
+    Both operands are needed TRANSPOSED ([features][tokens], the token dim padded to 128 with zeros)
+    with their slots' current delayed scales. ``dy8`` / ``x8``: the row-major fp8 copies the dgrad /
+    forward GEMMs already used (same slots, same scales) -> a byte transpose (1 byte read per
+    element); otherwise a transposing quantize pass over the bf16 tensor (the slots' amax is recorded
+    by the non-transposed passes). Then the k-contiguous fp8 ping-pong GEMM runs split-K over tokens
+    into a workspace, reduced into ``out`` in a fixed order (deterministic)."""
     ext = _ext.ext()
     T, N = dy.shape
     K = x.shape[1]
     Tp = (T + 127) // 128 * 128
     dyt = torch.empty(N, Tp, dtype=torch.uint8, device=dy.device)
     xt = torch.empty(K, Tp, dtype=torch.uint8, device=dy.device)
-    ext.fp8_quant_t(dy, dyt, dy_meta.qscale[dy_slot:dy_slot + 1], E5M2)
-    ext.fp8_quant_t(x, xt, x_meta.qscale[x_slot:x_slot + 1], E4M3)
+    if dy8 is not None:
+        ext.fp8_transpose(dy8, dyt)
+    else:
+        ext.fp8_quant_t(dy, dyt, dy_meta.qscale[dy_slot:dy_slot + 1], E5M2)
+    if x8 is not None:
+        ext.fp8_transpose(x8, xt)
+    else:
+        ext.fp8_quant_t(x, xt, x_meta.qscale[x_slot:x_slot + 1], E4M3)
     splits = gemm.wgrad_splits(T, N, K, 12)
     ksplit = max(128, (Tp // splits + 127) // 128 * 128)
     nsplit = (Tp + ksplit - 1) // ksplit

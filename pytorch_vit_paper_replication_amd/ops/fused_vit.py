@@ -152,10 +152,13 @@ class EncoderBlockFn(torch.autograd.Function):
             gen = store.generation
             lay = store.layout_key()
             wq = [st.weight(store.bf16(w), id(w), gen, lay) for w in (wqkv, wo, w1, w2)]
+            acts8 = []  # the e4m3 operands xn1, o, xn2, h: kept for the fp8 weight gradients (byte transposes)
             a, s_ = xq1 if q1 is not None else st.act_quant(xn1, blk, 0)
+            acts8.append(a)
             qkv = F8.linear_fwd_fp8(a, s_, *wq[0], bqkv)
             o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
             a, s_ = st.act_quant(o, blk, 1)
+            acts8.append(a)
             x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
             q2 = st.act_producer(blk, 2)
             if q2 is not None:
@@ -163,16 +166,22 @@ class EncoderBlockFn(torch.autograd.Function):
             else:
                 xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
                 a, s_ = st.act_quant(xn2, blk, 2)
+            acts8.append(a)
             hq = st.act_producer(blk, 3)  # h's e4m3 copy from the fc1 epilogue (calibrated slot)
             h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq)
             if hq is not None:
                 h, (a, s_) = h
             else:
                 a, s_ = st.act_quant(h, blk, 3)
+            acts8.append(a)
             x2 = F8.linear_fwd_fp8(a, s_, *wq[3], b2, resid=x1, drop=drop2)
+            # for the fp8 weight gradients (only once every slot they use is calibrated)
+            ctx.acts8 = acts8 if st.wgrad and need_bwd else None
         if need_bwd:
             ctx.save_for_backward(x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h)
         ctx.meta = (B, N, H, scale, store, drop1, drop2, dropa, params)
+        if f8 is None:
+            ctx.acts8 = None
         return x2
 
     @staticmethod
@@ -189,6 +198,17 @@ class EncoderBlockFn(torch.autograd.Function):
         f8d = ctx.f8d
 
         pre_q = {}  # grad slot -> (e5m2 copy, dequant scale) written by the producing dgrad epilogue
+        grads8 = {}  # grad slot -> the e5m2 copy a dgrad GEMM consumed (reused by the fp8 weight gradients)
+        acts8 = ctx.acts8
+
+        def grad8(which):  # the e5m2 copy of gradient slot `which`, consumed or pending (None: none yet)
+            if which in grads8:
+                return grads8[which]
+            return pre_q[which][0] if which in pre_q else None
+
+        def side8(*whichs):  # fp8 copies a side-stream weight gradient reads (held until the join)
+            ts = [grad8(w) for w in whichs] + (list(acts8) if acts8 is not None else [])
+            return tuple(t for t in ts if t is not None)
 
         def dgrad(dy, w, which, dgelu_aux=None, colsum=None):
             wt = store.bf16_t(w)
@@ -197,6 +217,7 @@ class EncoderBlockFn(torch.autograd.Function):
 
                 st, blk = f8d
                 gq, gs = pre_q.pop(which) if which in pre_q else st.grad_quant(dy, blk, which)
+                grads8[which] = gq
                 wq, ws = st.weight(wt, ~id(w), store.generation, store.layout_key())
                 # the dGELU dgrad (fc2) also writes dU's e5m2 copy for the fc1 dgrad (grad slot 1)
                 nq = st.grad_producer(blk, 1) if dgelu_aux is not None else None
@@ -212,7 +233,8 @@ class EncoderBlockFn(torch.autograd.Function):
         def wgrad(dy, x, gw, which_grad, which_act):
             # fp8 weight gradient (e5m2 dy^T x e4m3 x) once the slots are calibrated, else bf16
             if f8d is not None and f8d[0].wgrad_ready(f8d[1], which_grad, which_act) and dy.shape[0] >= 256:
-                f8d[0].linear_wgrad(dy, x, gw, f8d[1], which_grad, which_act)
+                f8d[0].linear_wgrad(dy, x, gw, f8d[1], which_grad, which_act, grad8(which_grad),
+                                    acts8[which_act] if acts8 is not None else None)
             else:
                 gemm.linear_wgrad(dy, x, gw)
 
@@ -239,7 +261,7 @@ class EncoderBlockFn(torch.autograd.Function):
             if gw1 is not None:
                 wgrad(du, xn2, gw1, 1, 2)
 
-        store.on_side(mlp_wgrads, dz2, h, du, xn2)  # weight grads off the critical path
+        store.on_side(mlp_wgrads, dz2, h, du, xn2, *side8(0, 1))  # weight grads off the critical path
         dxn2 = dgrad(du, w1, 1)
         dx1 = torch.empty_like(dx2)
         # dx1 = dx2 + LN2'(dxn2); d(bo) = colsum(dx1) reduced in the same kernel
@@ -281,7 +303,10 @@ class EncoderBlockFn(torch.autograd.Function):
             if gwqkv is not None:
                 wgrad(dqkv, xn1, gwqkv, 3, 0)
 
-        store.on_side(attn_wgrads, dx1, o, dqkv, xn1, do, *(() if db_part is None else (db_part,)))
+        if f8d is not None and f8d[0].wgrad_ready(f8d[1], 3, 0) and store.bf16_t(wqkv) is not None:
+            # dQKV's e5m2 copy now, so the side-stream qkv weight gradient transposes it (the dgrad uses it too)
+            pre_q[3] = f8d[0].grad_quant(dqkv, f8d[1], 3)
+        store.on_side(attn_wgrads, dx1, o, dqkv, xn1, do, *(() if db_part is None else (db_part,)), *side8(2, 3))
         dxn1 = dgrad(dqkv, wqkv, 3)
         dx = torch.empty_like(dx2)
         if prev is not None:

@@ -591,6 +591,24 @@ def check_layernorm_fwd_q8(T=3000, D=1280):
     return (f"layernorm_fwd_q8 T{T} D{D}", m, {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "ln_not_identical": 0})
 
 
+def check_fp8_transpose(T=1000, C=1280, fmt=1):
+    """The fp8 weight gradient's transposed operand from the row-major fp8 copy (byte transpose) must be
+    byte-identical to the transposing quantize pass over the bf16 tensor with the same scale, zero
+    padding of the token dim included."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    x = bf(rnd(T, C))
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=fmt)
+    q, _ = meta.quantize(x, 0)
+    Tp = (T + 127) // 128 * 128
+    a = torch.full((C, Tp), 7, dtype=torch.uint8, device=DEV)
+    b = torch.full((C, Tp), 9, dtype=torch.uint8, device=DEV)
+    ext.fp8_transpose(q, a)
+    ext.fp8_quant_t(x, b, meta.qscale[0:1], fmt)
+    return (f"fp8_transpose T{T} C{C} fmt{fmt}", {"bytes_differ": float((a != b).sum().item())}, {"bytes_differ": 0})
+
+
 def check_wgrad_fp8(T, N, K):
     """dW = dequant(dy^T (e5m2) . x (e4m3)) from the transposed quantize passes + split-K fp8 GEMM,
     against the exact product of the same quantized operands and against bf16."""
@@ -1129,6 +1147,8 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_dgrad_fp8(1030, 1280, 768),
         lambda: check_gemm_fp8_producer(1000, 1280, 512),
         check_layernorm_fwd_q8,
+        check_fp8_transpose,
+        lambda: check_fp8_transpose(257, 768, 0),
         lambda: check_layernorm_fwd_q8(50, 768),
         lambda: check_gemm_fp8_producer(1030, 768, 1280, True),
         check_vit_fp8,
