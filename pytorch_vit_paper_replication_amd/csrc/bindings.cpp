@@ -586,6 +586,35 @@ void fp8_transpose(torch::Tensor x8, torch::Tensor yt) {
         "fp8_transpose");
 }
 
+// fp8 weight gradient partials straight from the row-major fp8 copies: ws[s][N][K] = dscale_a *
+// dscale_b * dy8[Ts][N]^T . x8[Ts][K] over token split s (ksplit tokens, a multiple of 128), dy8 e5m2
+// and x8 e4m3 [T][features] (mn-contiguous operands: transposed LDS reads, no transposed copies)
+void gemm_fp8_wgrad_mn(torch::Tensor dy8, torch::Tensor x8, torch::Tensor ws, int64_t N, int64_t K, int64_t T, torch::Tensor scale_a,
+                       torch::Tensor scale_b, int64_t ksplit) {
+  TORCH_CHECK(dy8.dim() == 2 && x8.dim() == 2 && dy8.size(0) >= T && x8.size(0) >= T && dy8.size(1) >= N && x8.size(1) >= K &&
+                  dy8.stride(1) == 1 && x8.stride(1) == 1,
+              "gemm_fp8_wgrad_mn: dy8 [T][N], x8 [T][K] row-major");
+  TORCH_CHECK(N % 16 == 0 && K % 16 == 0 && dy8.stride(0) % 16 == 0 && x8.stride(0) % 16 == 0 && ksplit % 128 == 0 &&
+                  reinterpret_cast<uintptr_t>(dy8.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x8.data_ptr()) % 16 == 0,
+              "gemm_fp8_wgrad_mn: 16-byte rows and bases, ksplit a multiple of 128");
+  TORCH_CHECK(T * std::max(dy8.stride(0), x8.stride(0)) < (1ll << 31), "gemm_fp8_wgrad_mn: 31-bit operand offsets");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.dim() == 3 && ws.stride(2) == 1 && ws.size(1) >= N &&
+                  ws.size(2) >= K && ws.size(0) >= (T + ksplit - 1) / ksplit,
+              "gemm_fp8_wgrad_mn: workspace [splits][N][K] f32");
+  pvr::GemmParams p{};
+  p.drop_scale = 1.f;
+  p.M = (int)N; p.N = (int)K; p.K = (int)T;
+  p.A = reinterpret_cast<const uint16_t*>(u8(dy8, "dy8")); p.lda = dy8.stride(0); p.a_kcontig = 0;
+  p.B = reinterpret_cast<const uint16_t*>(u8(x8, "x8")); p.ldb = x8.stride(0); p.b_kcontig = 0;
+  p.C = ws.data_ptr(); p.ldc = ws.stride(1); p.split_stride = ws.stride(0);
+  p.scale_a = f32(scale_a, "scale_a"); p.scale_b = f32(scale_b, "scale_b");
+  p.elem8 = 1; p.fmt_a = 1; p.fmt_b = 0;
+  p.k_split_len = (int)ksplit;
+  p.epi = 4;  // EPI_F32_STORE
+  p.tile_cfg = 14;
+  check(pvr_gemm(&p, stream()), "gemm_fp8_wgrad_mn");
+}
+
 // fp8 weight gradient partials: ws[s][N][K] = dscale_a * dscale_b * A8[N][Ks] . B8[K][Ks]^T over split s
 // of the (padded) token dim, A e5m2 (gradient^T), B e4m3 (activation^T)
 void gemm_fp8_wgrad(torch::Tensor A8, torch::Tensor B8, torch::Tensor ws, int64_t N, int64_t K, int64_t Tp, torch::Tensor scale_a,
@@ -828,6 +857,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("drop_p") = 0.0, py::arg("colsum") = py::none(), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
         py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0);
   m.def("fp8_transpose", &fp8_transpose);
+  m.def("gemm_fp8_wgrad_mn", &gemm_fp8_wgrad_mn);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);

@@ -782,7 +782,7 @@ constexpr int PP_BUF = 2 * 256 * 128;  // A + B image of one K-tile
 template <int W, bool AK, bool BKC, int ES>
 PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem,
                       int64_t lda, int64_t ldb, int t, int nk, int wave, int lane) {
-  static_assert(ES == 2 || (ES == 1 && AK && BKC), "fp8 operands: k-contiguous only");
+  static_assert(ES == 2 || ES == 1, "bf16 or fp8 operands");
   char* buf = smem + (t & 1) * PP_BUF;
   const int k0 = t * PP_BK;   // bf16 element offset (mn path)
   const int kb = t * 128;     // byte offset of this K-tile within a k-contiguous row (64 bf16 / 128 fp8)
@@ -797,6 +797,12 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
         const int row = rowb + (lane >> 3);
         const int c = (lane & 7) ^ swz_k(row);
         dma16(live ? ars : nul, to_lds(buf + rowb * 128), (uint32_t)(row * lda * ES + kb + c * 16));
+      } else if constexpr (ES == 1) {
+        // fp8 mn-contiguous half-tile: [128 k][128 B] image, 16-B chunk cl of k-row kr at byte 16 cl
+        // holds tile rows (cl >> 2) * 128 + hh * 64 + (cl & 3) * 16 .. +15 (lda in bytes)
+        const int kr = 8 * d + (lane >> 3), cl = lane & 7;
+        const int m = (cl >> 2) * 128 + hh * 64 + (cl & 3) * 16;
+        dma16(live ? ars : nul, to_lds(buf + hh * 16384 + d * 1024), (uint32_t)((int64_t)(t * 128 + kr) * lda + m));
       } else {
         const int kr = 4 * d + (lane >> 4);
         const int cl = (lane & 15) ^ swz_mn(kr);  // logical chunk stored at this lane's LDS slot
@@ -810,6 +816,11 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
         const int row = rowb + (lane >> 3);
         const int c = (lane & 7) ^ swz_k(row);
         dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * ES + kb + c * 16));
+      } else if constexpr (ES == 1) {
+        // chunk cl holds tile rows (cl >> 1) * 64 + hh * 32 + (cl & 1) * 16 .. +15
+        const int kr = 8 * d + (lane >> 3), cl = lane & 7;
+        const int n = (cl >> 1) * 64 + hh * 32 + (cl & 1) * 16;
+        dma16(live ? brs : nul, to_lds(buf + 256 * 128 + hh * 16384 + d * 1024), (uint32_t)((int64_t)(t * 128 + kr) * ldb + n));
       } else {
         const int kr = 4 * d + (lane >> 4);
         const int cl = (lane & 15) ^ swz_mn(kr);
@@ -835,6 +846,24 @@ PVR_DEV v8s frag_fp8(const char* img, int r0, int h, int lane) {
   return ds_read_b128(img + row * 128 + ((c ^ swz_k(row)) << 4));
 }
 
+typedef uint32_t v2u8 __attribute__((ext_vector_type(2)));
+// fp8 operand fragment of an mn-contiguous [128 k][128 B] image (4 x ds_read_b64_tr_b8, async: the
+// caller waits with lds_wait): lane (g = l >> 4, i = l & 15) gets image column c0 + i at k-rows
+// 32g + 8j .. +7 in r[j], i.e. k = 32g .. 32g + 31 of its row as frag_fp8 delivers it for a
+// k-contiguous image. Per 16-lane group, lane 2q + p supplies row q, bytes 8p .. 8p + 7.
+PVR_DEV void read_frag_mn8_async(const char* img, int c0, int lane, v2u8 (&r)[4]) {
+  const int g = lane >> 4, i = lane & 15;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(img + (32 * g + (i >> 1)) * 128 + c0 + 8 * (i & 1));
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r[0]) : "v"(a));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:1024" : "=v"(r[1]) : "v"(a));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:2048" : "=v"(r[2]) : "v"(a));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:3072" : "=v"(r[3]) : "v"(a));
+}
+PVR_DEV v8s cat8_fp8(v2u8 lo, v2u8 hi) {
+  typedef uint32_t v4u_ __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(v8s, (v4u_){lo.x, lo.y, hi.x, hi.y});
+}
+
 template <int FA, int FB>
 PVR_DEV v4f mfma_fp8(const v8s& a0, const v8s& a1, const v8s& b0, const v8s& b1, v4f c) {
   typedef int v8i __attribute__((ext_vector_type(8)));
@@ -855,7 +884,12 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
   // read (halves combined after the wait below): the builtin would make hipcc drain the in-flight
   // half-tile DMAs (vmcnt(0)) in front of the read.
   v4s alo[4][2], ahi[4][2], blo[2][2], bhi[2][2];
-  if constexpr (RD_A) {
+  constexpr bool MN8A = ES == 1 && !AK, MN8B = ES == 1 && !BKC;
+  v2u8 a8r[MN8A ? 4 : 1][4], b8r[MN8B ? 2 : 1][4];
+  if constexpr (RD_A && MN8A) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) read_frag_mn8_async(buf + QM * 16384, wm * 64 + 16 * ii, lane, a8r[ii]);
+  } else if constexpr (RD_A) {
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -868,7 +902,10 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           read_frag_mn_async<128>(buf + QM * 16384, wm * 64 + 16 * ii, ks, lane, alo[ii][ks], ahi[ii][ks]);
       }
   }
-  if constexpr (RD_B) {
+  if constexpr (RD_B && MN8B) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) read_frag_mn8_async(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, lane, b8r[jj]);
+  } else if constexpr (RD_B) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
@@ -888,6 +925,20 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   else
     lds_wait();  // asm reads in flight: the wait must also fence their consumers
+  if constexpr (RD_A && MN8A) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      af[ii][0] = cat8_fp8(a8r[ii][0], a8r[ii][1]);
+      af[ii][1] = cat8_fp8(a8r[ii][2], a8r[ii][3]);
+    }
+  }
+  if constexpr (RD_B && MN8B) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      bf[QN][jj][0] = cat8_fp8(b8r[jj][0], b8r[jj][1]);
+      bf[QN][jj][1] = cat8_fp8(b8r[jj][2], b8r[jj][3]);
+    }
+  }
   if constexpr (RD_A && !AK && ES == 2) {
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
@@ -1355,7 +1406,11 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
 
   const void* abase;
   uint32_t abytes;
-  if constexpr (ES == 1) {
+  if constexpr (ES == 1 && !AK) {  // fp8 mn-contiguous [K][M] bytes: rows past kend, columns past M read 0
+    const uint8_t* a8 = (const uint8_t*)p.A;
+    abase = a8 + (int64_t)kbeg * p.lda + m0;
+    abytes = rsrc_bytes((int64_t)(kend - 1) * p.lda + p.M, (int64_t)kbeg * p.lda + m0) / 2;
+  } else if constexpr (ES == 1) {
     const uint8_t* a8 = (const uint8_t*)p.A;
     abase = a8 + (int64_t)m0 * p.lda + kbeg;
     abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg) / 2;
@@ -1368,7 +1423,11 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   }
   const void* bbase;
   uint32_t bbytes;
-  if constexpr (ES == 1) {
+  if constexpr (ES == 1 && !BKC) {
+    const uint8_t* b8 = (const uint8_t*)p.B;
+    bbase = b8 + (int64_t)kbeg * p.ldb + n0;
+    bbytes = rsrc_bytes((int64_t)(kend - 1) * p.ldb + p.N, (int64_t)kbeg * p.ldb + n0) / 2;
+  } else if constexpr (ES == 1) {
     const uint8_t* b8 = (const uint8_t*)p.B;
     bbase = b8 + (int64_t)n0 * p.ldb + kbeg;
     bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg) / 2;
@@ -1713,7 +1772,16 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
   const bool ak = p.a_kcontig, bk = p.b_kcontig;
   if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad / wgrad e5m2 x e4m3)
     const int f = p.fmt_a * 2 + p.fmt_b;
-    if (!ak || !bk || p.K % 128 != 0 || (p.N & 3) || !p.scale_a || !p.scale_b) return hipErrorInvalidValue;
+    if ((p.N & 3) || !p.scale_a || !p.scale_b) return hipErrorInvalidValue;
+    if (!ak && !bk) {
+      // weight gradient straight from the row-major fp8 copies ([tokens][features], mn-contiguous,
+      // transposed LDS reads): split-K over the tokens, per-split partials (tile 14); 16-B rows
+      if (p.epi != EPI_F32_STORE || p.tile_cfg != 14 || p.k_split_len % 128 != 0 || f != 2 || (p.M & 15) || (p.N & 15) ||
+          (p.lda & 15) || (p.ldb & 15))
+        return hipErrorInvalidValue;
+      return launch_pp<false, false, true, EPI_F32_STORE, 1, 1, 0>(p, s);
+    }
+    if (!ak || !bk || p.K % 128 != 0) return hipErrorInvalidValue;
     if (p.epi == EPI_F32_STORE) {
       // weight gradient: split-K over the (128-padded) token dim, per-split partials (tile 14)
       if (p.tile_cfg != 14 || p.k_split_len % 128 != 0 || f != 2) return hipErrorInvalidValue;

@@ -32,6 +32,9 @@ from .. import _ext
 from . import gemm
 
 E4M3, E5M2 = 0, 1
+# fp8 weight gradients read the row-major fp8 copies directly (mn-contiguous GEMM operands); False:
+# byte-transposed copies + the k-contiguous GEMM (test hook / A-B)
+WGRAD_MN = True
 FMAX = {E4M3: 448.0, E5M2: 57344.0}
 
 
@@ -261,6 +264,15 @@ def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torc
     ext = _ext.ext()
     T, N = dy.shape
     K = x.shape[1]
+    if dy8 is not None and x8 is not None and WGRAD_MN:
+        # both row-major copies exist: the GEMM reads them as mn-contiguous operands (no transposes)
+        splits = gemm.wgrad_splits(T, N, K, 12)
+        ksplit = max(128, (T // splits + 127) // 128 * 128)
+        nsplit = (T + ksplit - 1) // ksplit
+        ws = gemm._workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
+        ext.gemm_fp8_wgrad_mn(dy8, x8, ws, N, K, T, dy_meta.dscale[dy_slot:dy_slot + 1], x_meta.dscale[x_slot:x_slot + 1], ksplit)
+        ext.splitk_reduce(ws, nsplit, out, True)
+        return out
     Tp = (T + 127) // 128 * 128
     dyt = torch.empty(N, Tp, dtype=torch.uint8, device=dy.device)
     xt = torch.empty(K, Tp, dtype=torch.uint8, device=dy.device)

@@ -609,6 +609,33 @@ def check_fp8_transpose(T=1000, C=1280, fmt=1):
     return (f"fp8_transpose T{T} C{C} fmt{fmt}", {"bytes_differ": float((a != b).sum().item())}, {"bytes_differ": 0})
 
 
+def check_wgrad_fp8_mn(T, N, K):
+    """fp8 weight gradient read straight from the row-major fp8 copies (mn-contiguous operands,
+    ds_read_b64_tr_b8 fragments) vs the byte-transposed copies through the k-contiguous GEMM (the same
+    fp8 operands: equal up to fp32 summation order) and vs the exact product of the dequantized
+    operands; token counts that are not multiples of 128 exercise the split tails."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    dy, x = bf(rnd(T, N)), bf(rnd(T, K))
+    gm, am = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2), F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+    dy8, _ = gm.quantize(dy, 0)
+    x8, _ = am.quantize(x, 0)
+    out_mn = torch.zeros(N, K, device=DEV)
+    out_t = torch.zeros(N, K, device=DEV)
+    F8.linear_wgrad_fp8(dy, gm, 0, x, am, 0, out_mn, dy8, x8)
+    F8.WGRAD_MN = False
+    try:
+        F8.linear_wgrad_fp8(dy, gm, 0, x, am, 0, out_t, dy8, x8)
+    finally:
+        F8.WGRAD_MN = True
+    dyd = ext.fp8_dequant(dy8.contiguous(), gm.dscale[0:1], 1)
+    xd = ext.fp8_dequant(x8.contiguous(), am.dscale[0:1], 0)
+    m = worst((out_mn, dyd.t() @ xd))
+    m["vs_transposed_l2"] = errs(out_mn, out_t)[0]
+    return (f"wgrad fp8 mn-contiguous T{T} N{N} K{K}", m, lim(2.5e-5, 5e-5, vs_transposed_l2=1e-6))
+
+
 def check_wgrad_fp8(T, N, K):
     """dW = dequant(dy^T (e5m2) . x (e4m3)) from the transposed quantize passes + split-K fp8 GEMM,
     against the exact product of the same quantized operands and against bf16."""
@@ -1148,6 +1175,9 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_fp8_producer(1000, 1280, 512),
         check_layernorm_fwd_q8,
         check_fp8_transpose,
+        lambda: check_wgrad_fp8_mn(1000, 1280, 512),
+        lambda: check_wgrad_fp8_mn(32896, 1280, 3840),
+        lambda: check_wgrad_fp8_mn(300, 768, 256),
         lambda: check_fp8_transpose(257, 768, 0),
         lambda: check_layernorm_fwd_q8(50, 768),
         lambda: check_gemm_fp8_producer(1030, 768, 1280, True),
