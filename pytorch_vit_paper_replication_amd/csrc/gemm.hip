@@ -46,6 +46,9 @@ constexpr int TK = 64;  // K depth of one LDS stage
 
 PVR_DEV int swz_k(int row) { return (row >> 1) & 7; }                                // 128-B rows
 PVR_DEV int swz_mn(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }  // 16-B chunk XOR
+// 16-B chunk XOR of the fp8 mn images' 128-B k-rows: the 16 rows a 32-lane half reads with
+// ds_read_b64_tr_b8 (rows 8q' + q of its two 16-lane groups, 32 apart) land on 64 distinct banks
+PVR_DEV int swz8(int row) { return ((row >> 1) & 3) | (((row >> 5) & 1) << 2); }
 
 // Issue the LDS-DMA of one operand tile (R rows of the operand x 64 k) into `lds`.
 template <int R, bool KC, int NW>
@@ -800,7 +803,7 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
       } else if constexpr (ES == 1) {
         // fp8 mn-contiguous half-tile: [128 k][128 B] image, 16-B chunk cl of k-row kr at byte 16 cl
         // holds tile rows (cl >> 2) * 128 + hh * 64 + (cl & 3) * 16 .. +15 (lda in bytes)
-        const int kr = 8 * d + (lane >> 3), cl = lane & 7;
+        const int kr = 8 * d + (lane >> 3), cl = (lane & 7) ^ swz8(kr);
         const int m = (cl >> 2) * 128 + hh * 64 + (cl & 3) * 16;
         dma16(live ? ars : nul, to_lds(buf + hh * 16384 + d * 1024), (uint32_t)((int64_t)(t * 128 + kr) * lda + m));
       } else {
@@ -818,7 +821,7 @@ PVR_DEV void pp_issue(__amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __
         dma16(live ? brs : nul, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * ES + kb + c * 16));
       } else if constexpr (ES == 1) {
         // chunk cl holds tile rows (cl >> 1) * 64 + hh * 32 + (cl & 1) * 16 .. +15
-        const int kr = 8 * d + (lane >> 3), cl = lane & 7;
+        const int kr = 8 * d + (lane >> 3), cl = (lane & 7) ^ swz8(kr);
         const int n = (cl >> 1) * 64 + hh * 32 + (cl & 1) * 16;
         dma16(live ? brs : nul, to_lds(buf + 256 * 128 + hh * 16384 + d * 1024), (uint32_t)((int64_t)(t * 128 + kr) * ldb + n));
       } else {
@@ -853,7 +856,9 @@ typedef uint32_t v2u8 __attribute__((ext_vector_type(2)));
 // k-contiguous image. Per 16-lane group, lane 2q + p supplies row q, bytes 8p .. 8p + 7.
 PVR_DEV void read_frag_mn8_async(const char* img, int c0, int lane, v2u8 (&r)[4]) {
   const int g = lane >> 4, i = lane & 15;
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(img + (32 * g + (i >> 1)) * 128 + c0 + 8 * (i & 1));
+  const int row = 32 * g + (i >> 1);  // + 8j for read j: swz8 is the same on all four
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(
+      img + row * 128 + ((((c0 >> 4) ^ swz8(row)) << 4) | 8 * (i & 1)));
   asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r[0]) : "v"(a));
   asm volatile("ds_read_b64_tr_b8 %0, %1 offset:1024" : "=v"(r[1]) : "v"(a));
   asm volatile("ds_read_b64_tr_b8 %0, %1 offset:2048" : "=v"(r[2]) : "v"(a));
