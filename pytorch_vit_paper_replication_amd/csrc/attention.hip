@@ -30,7 +30,7 @@ namespace {
 template <int DH, bool DROP>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
                                                         int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale,
-                                                        AttnDrop drop) {
+                                                        AttnDrop drop, AttnQ8 q8) {
   using C = Hd<DH>;
   // keys per tile: 64, or 32 for two-image head rows (dh > 64), so that the two K/V stages stay at
   // 32 KiB and four workgroups share a CU
@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
   const int q = q0 + li;
+  float qam = 0.f;
   if (q < N) {
     const float inv = 1.f / l_run;
     uint16_t* orow = out + ((int64_t)b * N + q) * ld_o + h * DH;
@@ -167,7 +168,23 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
       w.y = pack2bf(o[e][2] * inv, o[e][3] * inv);
       *(uint2*)(orow + 16 * e + 4 * g) = w;
     }
+    if (q8.out) {  // e4m3 copy for the fp8 out-proj GEMM
+      const float qs = *q8.qs;
+      uint8_t* qrow = q8.out + ((int64_t)b * N + q) * q8.ld + h * DH;
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e) {
+        const float v[4] = {o[e][0] * inv, o[e][1] * inv, o[e][2] * inv, o[e][3] * inv};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qam = nan_max(qam, fabsf(v[r]));
+        *(uint32_t*)(qrow + 16 * e + 4 * g) =
+            (uint32_t)pack2_fp8<0, true>(v[2] * qs, v[3] * qs, pack2_fp8<0, false>(v[0] * qs, v[1] * qs, 0));
+      }
+    }
     if (g == 0) lse[(int64_t)bh * N + q] = (m_run + __log2f(l_run)) * LN2;
+  }
+  if (q8.out) {
+    qam = wave_max_nan(qam);
+    if (lane == 0) amax_record(q8.amax, qam);
   }
 }
 
@@ -1260,14 +1277,14 @@ static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t
 
 template <int DH>
 static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
-                                  int D, float scale, const pvr::AttnDrop& drop, hipStream_t s) {
+                                  int D, float scale, const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
   using namespace pvr;
   if (drop.seed) {  // attention dropout: the tiled kernel with the in-register keep mask
     hipLaunchKernelGGL((attn_fwd_kernel<DH, true>), dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D,
-                       scale, drop);
+                       scale, drop, q8);
     return hipGetLastError();
   }
-  if (DH == 64 && N <= 256) {
+  if (DH == 64 && N <= 256 && !q8.out) {
     // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take
     // up to 128 KiB of LDS), ceil(N/16) waves
     switch ((N + 15) / 16) {
@@ -1282,7 +1299,7 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
   }
   // 1-D grid of (B*H) x query blocks, XCD-remapped in-kernel
   hipLaunchKernelGGL((attn_fwd_kernel<DH, false>), dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D,
-                     scale, drop);
+                     scale, drop, q8);
   return hipGetLastError();
 }
 
@@ -1290,15 +1307,17 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
 // backward must get the same seed / seed_off / thr16
 extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
                                    int H, int D, float scale, const uint64_t* seed, uint64_t seed_off, uint32_t thr16, float keep_scale,
-                                   hipStream_t s) {
+                                   uint8_t* q8_out, int64_t q8_ld, const float* q8_qs, unsigned* q8_amax, hipStream_t s) {
   using namespace pvr;
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
+  if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
   const AttnDrop drop{seed, seed_off, thr16, keep_scale};
+  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax};
   switch (D / H) {
-    case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
-    case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
-    case 96: return attn_fwd_launch<96>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
-    case 128: return attn_fwd_launch<128>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, s);
+    case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
+    case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
+    case 96: return attn_fwd_launch<96>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
+    case 128: return attn_fwd_launch<128>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -110,6 +110,18 @@ struct AttnDrop {
   uint32_t thr;          // round(p * 65536)
   float scale;           // 1 / keep probability
 };
+// Optional e4m3 copy of the attention output for an fp8 out-proj GEMM (producer-side quantization):
+// out[row][col] = fp8(o * (*qs)), *amax = max(*amax, max|o|); out == null: none
+struct AttnQ8 {
+  uint8_t* out;
+  int64_t ld;
+  const float* qs;
+  unsigned* amax;
+};
+// max|x| record with few same-address atomics: most waves find the running amax already larger
+PVR_DEV void amax_record(unsigned* amax, float m) {
+  if (!(m <= 0.f) && !(m <= __uint_as_float(__builtin_nontemporal_load(amax)))) atomicMax(amax, __float_as_uint(m));
+}
 PVR_DEV uint32_t attn_drop_key(const AttnDrop& d, int bh) {
   return rng_mix32(rng_key(*d.seed + d.off) ^ (0x9E3779B9u * (uint32_t)(bh + 1)));
 }

@@ -63,7 +63,7 @@ int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
 int pvr_attn_bwd_part_rows(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, const uint64_t*, uint64_t,
-                        uint32_t, float, hipStream_t);
+                        uint32_t, float, uint8_t*, int64_t, const float*, unsigned*, hipStream_t);
 int pvr_attn_dbias_splits(int, int);
 hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float*, const uint16_t*, int64_t, int, uint16_t*, int64_t,
                                hipStream_t);
@@ -694,14 +694,32 @@ void fp8_scale_update(torch::Tensor hist, torch::Tensor amax, torch::Tensor qsca
 
 // seed / seed_offset / drop_p: attention-probability dropout (the backward gets the same three)
 std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int64_t H, double scale, c10::optional<torch::Tensor> seed,
-                                    int64_t seed_offset, double drop_p) {
+                                    int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
+                                    c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax) {
   const int64_t D = qkv.size(1) / 3;
   auto out = torch::empty({B * N, D}, qkv.options());
   auto lse = torch::empty({B * H, N}, qkv.options().dtype(torch::kFloat32));
   TORCH_CHECK(qkv.size(0) == B * N, "attn_fwd: qkv rows != B*N");
   const DropArgs d = drop_args(seed, drop_p, "attn_fwd");
+  uint8_t* q8 = nullptr;
+  int64_t q8_ld = 0;
+  const float* q8_qs = nullptr;
+  unsigned* q8_amax = nullptr;
+  if (q_out.has_value() && q_out->defined()) {
+    // e4m3 copy of the output (producer-side quantization for an fp8 out-proj GEMM)
+    TORCH_CHECK(q_out->is_cuda() && q_out->scalar_type() == torch::kUInt8 && q_out->dim() == 2 && q_out->size(0) >= B * N &&
+                    q_out->size(1) >= D && q_out->stride(1) == 1 && q_out->stride(0) % 4 == 0,
+                "attn_fwd: q_out uint8 [B*N][D]");
+    TORCH_CHECK(q_scale.has_value() && q_scale->defined() && q_amax.has_value() && q_amax->defined() &&
+                    q_amax->scalar_type() == torch::kInt32,
+                "attn_fwd: q_out needs q_scale (f32) and q_amax (int32)");
+    q8 = reinterpret_cast<uint8_t*>(q_out->data_ptr());
+    q8_ld = q_out->stride(0);
+    q8_qs = f32(*q_scale, "q_scale");
+    q8_amax = reinterpret_cast<unsigned*>(q_amax->data_ptr<int32_t>());
+  }
   check(pvr_attn_fwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf_mut(out, "out"), D, f32_mut(lse, "lse"), (int)B, (int)N, (int)H, (int)D,
-                     (float)scale, d.seed, (uint64_t)seed_offset, d.thr, d.scale, stream()),
+                     (float)scale, d.seed, (uint64_t)seed_offset, d.thr, d.scale, q8, q8_ld, q8_qs, q8_amax, stream()),
         "attn_fwd");
   return {out, lse};
 }
@@ -866,7 +884,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_quant_multi", &fp8_quant_multi, py::arg("segs"), py::arg("nchunks"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"),
         py::arg("amax_only"));
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("B"), py::arg("N"), py::arg("H"), py::arg("scale"),
-        py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
+        py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0, py::arg("q_out") = py::none(),
+        py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
         py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none(),
         py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);

@@ -156,8 +156,15 @@ class EncoderBlockFn(torch.autograd.Function):
             a, s_ = xq1 if q1 is not None else st.act_quant(xn1, blk, 0)
             acts8.append(a)
             qkv = F8.linear_fwd_fp8(a, s_, *wq[0], bqkv)
-            o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
-            a, s_ = st.act_quant(o, blk, 1)
+            qo = st.act_producer(blk, 1)  # o's e4m3 copy from the attention forward (calibrated slot)
+            if qo is not None:
+                a = torch.empty(T, D, dtype=torch.uint8, device=x.device)
+                o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap, a, qo[0].qscale[qo[1]:qo[1] + 1],
+                                      qo[0].amax[qo[1]:qo[1] + 1])
+                s_ = qo[0].dscale[qo[1]:qo[1] + 1]
+            else:
+                o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
+                a, s_ = st.act_quant(o, blk, 1)
             acts8.append(a)
             x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
             q2 = st.act_producer(blk, 2)

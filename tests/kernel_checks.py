@@ -591,6 +591,36 @@ def check_layernorm_fwd_q8(T=3000, D=1280):
     return (f"layernorm_fwd_q8 T{T} D{D}", m, {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "ln_not_identical": 0})
 
 
+def check_attn_fwd_q8(B=2, N=257, H=4, dh=80):
+    """Attention forward with the fused e4m3 output copy: O / lse bit-identical to the plain forward,
+    the copy within one fp8 step of quantizing O, amax = max|O| (up to O's bf16 rounding)."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    D = H * dh
+    qkv = bf(rnd(B * N, 3 * D) * 2)
+    sc = 1.0 / math.sqrt(dh)
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+    meta.calibrated[0] = True
+    meta.qscale.fill_(300.0)
+    meta.dscale.copy_(1.0 / meta.qscale)
+    o0, l0 = ext.attn_fwd(qkv, B, N, H, sc)
+    q = torch.empty(B * N, D, dtype=torch.uint8, device=DEV)
+    o1, l1 = ext.attn_fwd(qkv, B, N, H, sc, None, 0, 0.0, q, meta.qscale[0:1], meta.amax[0:1])
+    ref = torch.empty(B * N, D, dtype=torch.uint8, device=DEV)
+    ext.fp8_quant(o1, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), 0)
+    amax = meta.amax.view(torch.float32)[0].item()
+    m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
+         "amax_rel": abs(amax - o1.float().abs().max().item()) / o1.float().abs().max().item(),
+         "not_identical": float(not (torch.equal(o0, o1) and torch.equal(l0, l1)))}
+    lim_ = {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "not_identical": 0}
+    if dh == 64 and N <= 256:  # the plain call takes the whole-head kernel, the copy the generic one
+        del m["not_identical"], lim_["not_identical"]
+        m["o_vs_head_kernel_l2"] = errs(o1, o0)[0]
+        lim_["o_vs_head_kernel_l2"] = 5e-3
+    return (f"attn_fwd_q8 B{B} N{N} H{H} dh{dh}", m, lim_)
+
+
 def check_fp8_transpose(T=1000, C=1280, fmt=1):
     """The fp8 weight gradient's transposed operand from the row-major fp8 copy (byte transpose) must be
     byte-identical to the transposing quantize pass over the bf16 tensor with the same scale, zero
@@ -1175,6 +1205,8 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_fp8_producer(1000, 1280, 512),
         check_layernorm_fwd_q8,
         check_fp8_transpose,
+        check_attn_fwd_q8,
+        lambda: check_attn_fwd_q8(3, 197, 2, 64),  # dh 64, N <= 256: the generic kernel takes the copy
         lambda: check_wgrad_fp8_mn(1000, 1280, 512),
         lambda: check_wgrad_fp8_mn(32896, 1280, 3840),
         lambda: check_wgrad_fp8_mn(300, 768, 256),
