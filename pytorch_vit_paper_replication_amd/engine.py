@@ -14,7 +14,9 @@ MI355X-oriented differences (no behaviour change):
   * with :class:`~..optim.FusedAdam` the clip runs inside the optimizer (device-side coefficient,
     no sync) and ``nn.CrossEntropyLoss()`` is executed by the fused softmax-xent kernel, whose
     per-row argmax == label flags also give the accuracy (no separate argmax / eq / sum);
-  * under ``torch.distributed`` metrics are all-reduced across ranks and only rank 0 prints.
+  * under ``torch.distributed`` metrics are all-reduced across ranks and only rank 0 prints;
+  * on a GPU the next batch's host->device copy runs on a copy stream while the current step
+    computes (:class:`~.data.prefetch.DevicePrefetcher`, K17) instead of a blocking ``.to(device)``.
 """
 from __future__ import annotations
 
@@ -29,6 +31,7 @@ except Exception:  # pragma: no cover
     def tqdm(x, **_):
         return x
 
+from .data.prefetch import prefetch
 from .ops import fused_vit
 from .ops.fused_vit import cross_entropy
 from .utils.profiling import range_push
@@ -111,7 +114,7 @@ def train_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, opt
     lf = _fused_loss(loss_fn)
     sums = torch.zeros(2, dtype=torch.float32, device=device)
     nb = 0
-    for X, y in dataloader:
+    for X, y in prefetch(dataloader, device):
         if step_logger is not None:
             step_logger.begin()
         X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
@@ -141,7 +144,7 @@ def test_step(model: torch.nn.Module, dataloader, loss_fn: torch.nn.Module, devi
     sums = torch.zeros(2, dtype=torch.float32, device=device)
     nb = 0
     with torch.inference_mode():
-        for X, y in dataloader:
+        for X, y in prefetch(dataloader, device):
             X, y = X.to(device, non_blocking=True), y.to(device, non_blocking=True)
             logits = model(X)
             loss = lf(logits, y)

@@ -451,3 +451,23 @@ def test_summary_on_gpu_model_matches_notebook():
     x = torch.randn(2, 3, 224, 224, device="cuda")
     assert _ext.use_fused(x)
     assert m(x).shape == (2, 3)
+
+
+def test_device_prefetcher_copies_on_side_stream():
+    """K17: the prefetcher's batches equal a blocking .to(device), land on the current device, and
+    the engine consumes them (next batch's copy in flight on the copy stream)."""
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from pytorch_vit_paper_replication_amd.data import DevicePrefetcher
+
+    xs, ys = torch.randn(37, 3, 8, 8), torch.randint(0, 5, (37,))
+    dl = DataLoader(TensorDataset(xs, ys), batch_size=8, pin_memory=True)
+    pf = DevicePrefetcher(dl, "cuda")
+    outs = [(x.clone(), y.clone()) for x, y in pf]
+    torch.cuda.synchronize()
+    assert len(outs) == 5 and all(x.is_cuda and y.is_cuda for x, y in outs)
+    assert torch.equal(torch.cat([x for x, _ in outs]).cpu(), xs)
+    assert torch.equal(torch.cat([y for _, y in outs]).cpu(), ys)
+    # unpinned host tensors are pinned on the way (copy stays asynchronous)
+    dl2 = DataLoader(TensorDataset(xs, ys), batch_size=16, pin_memory=False)
+    assert torch.equal(torch.cat([x.cpu() for x, _ in DevicePrefetcher(dl2, "cuda")]), xs)

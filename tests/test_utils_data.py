@@ -184,3 +184,21 @@ def test_summary_encoder_block_and_frozen_rows():
     assert "(2,362,368)" in mlp and "False" in mlp
     top = s2.splitlines()[3]
     assert "Partial" in top
+
+
+def test_device_prefetcher_cpu_passthrough():
+    """K17 prefetcher: on a CPU device it yields the loader's batches unchanged, keeps len() and
+    the sampler reachable (DistributedSampler.set_epoch), and is a no-op wrapper for prefetch()."""
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from pytorch_vit_paper_replication_amd.data import DevicePrefetcher, prefetch
+
+    xs, ys = torch.randn(10, 3, 4, 4), torch.arange(10)
+    dl = DataLoader(TensorDataset(xs, ys), batch_size=4)
+    assert prefetch(dl, "cpu") is dl
+    pf = DevicePrefetcher(dl, "cpu")
+    assert len(pf) == 3 and pf.sampler is dl.sampler and pf.dataset is dl.dataset
+    got = list(pf)
+    assert len(got) == 3
+    assert torch.equal(torch.cat([b[0] for b in got]), xs) and torch.equal(torch.cat([b[1] for b in got]), ys)
+    assert list(pf)[0][0].shape == (4, 3, 4, 4)  # re-iterable
