@@ -24,9 +24,15 @@ event-gated the same way; ``"native-mesh"`` runs that communicator's own reduce-
 schedule (``csrc/comm_core.h``: grouped point-to-point transfers to every peer at once, fp32). gloo /
 CPU always uses ``torch.distributed``. World-1 A/B at ViT-B/16 b512 (profiles/r3/ddp_transport_world1_b512.log):
 no DDP 8082 / 8075 img/s, torch 8053, torch with the bf16 wire 8034 — RCCL's one-rank kernel
-(``oneRankReduce``, ~0.2 ms per bucket) hides under the backward. The native transport's stream was
-high-priority there (7411 img/s): RCCL's kernels then pre-empted the overlapped GEMMs; it now runs
-at normal priority.
+(``oneRankReduce``, ~0.2 ms per bucket) hides under the backward. The native transport stays opt-in:
+it is 8 % slower at world 1 (7306-7337 vs torch 7936, no DDP 7990-8002 img/s,
+profiles/r3/ddp_native/transport_ab.log) and the cause is not identified. Ruled out by measurement:
+stream priority (normal, like ProcessGroupNCCL's), HW-queue aliasing (GPU_MAX_HW_QUEUES=8: no
+change), a second RCCL communicator in the process (idle: no effect, scripts/probes/idle_comm_probe.py),
+a second RCCL runtime (it resolves torch's librccl.so), collective placement (the same 11
+``oneRankReduce`` per step, all inside the backward, the optimizer after the last one). The in-step
+traces (profiles/r3/ddp_native/) show the FORWARD kernels 10-100 % slower with no other kernel on
+the GPU, i.e. a device-wide effect, not stream ordering.
 
 Wire format (``comm_dtype``): fp32 by default. ``torch.bfloat16`` keeps a persistent bf16 mirror of
 the gradient buffer (no per-step allocation): each bucket is cast into its slice, all-reduced in
