@@ -210,8 +210,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dsum,
                                                       uint16_t* __restrict__ dz, int64_t dz_stride,
                                                       const uint64_t* __restrict__ seed_ptr, uint64_t seed_off, uint32_t thr,
-                                                      float dscale, int rows, int D) {
+                                                      float dscale, uint8_t* __restrict__ qout, int64_t q_stride,
+                                                      const float* __restrict__ qscale, unsigned* __restrict__ amax, int rows,
+                                                      int D) {
   __shared__ float red[4][MAXCH * 64 * W > 1280 ? 1280 : MAXCH * 64 * W];  // one partial at a time
+  __shared__ float qred[4];
+  const float qs = qout ? *qscale : 1.f;
+  float qam = 0.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = D / W;
   float gw[MAXCH][W], gb[MAXCH][W], gs[MAXCH][W];
@@ -308,6 +313,20 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
           for (int j = 0; j < W; j += 2) q.u[j >> 1] = pack2bf(o[j], o[j + 1]);
           q.store(dz + (int64_t)row * dz_stride + c * W);
         }
+        if (qout) {  // uniform: e5m2 copy of the gradient written last (dz, else dx) for the next fp8 dgrad GEMM
+          uint32_t b4[W / 4];
+#pragma unroll
+          for (int j = 0; j < W; j += 4) {
+            b4[j >> 2] = (uint32_t)pack2_fp8<1, true>(o[j + 2] * qs, o[j + 3] * qs, pack2_fp8<1, false>(o[j] * qs, o[j + 1] * qs, 0));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) qam = nan_max(qam, fabsf(o[j + e]));
+          }
+          uint8_t* qp = qout + (int64_t)row * q_stride + c * W;
+          if constexpr (W == 8)
+            *(uint2*)qp = make_uint2(b4[0], b4[1]);
+          else
+            *(uint32_t*)qp = b4[0];
+        }
 #pragma unroll
         for (int j = 0; j < W; ++j) gs[i][j] += o[j];  // column sums of dx (or dz): a fused bias gradient
       }
@@ -340,6 +359,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
     __syncthreads();
     for (int col = threadIdx.x; col < D; col += 256)
       atomicAdd(outs[qn] + col, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
+  }
+  if (qout) {  // max |gradient| of the block's rows: one atomic per workgroup (delayed-scaling amax record)
+    qam = wave_max_nan(qam);
+    if (lane == 0) qred[wave] = qam;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = nan_max(nan_max(qred[0], qred[1]), nan_max(qred[2], qred[3]));
+      if (!(m <= 0.f)) atomicMax(amax, __float_as_uint(m));
+    }
   }
 }
 
@@ -398,10 +426,12 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
                                         const float* mean, const float* rstd, const float* w, const uint16_t* dres,
                                         int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
                                         float* dsum, uint16_t* dz, int64_t dz_stride, const uint64_t* seed_ptr,
-                                        uint64_t seed_off, uint32_t thr, float dscale, int rows, int D, hipStream_t s) {
+                                        uint64_t seed_off, uint32_t thr, float dscale, uint8_t* q, int64_t q_stride,
+                                        const float* qscale, unsigned* amax, int rows, int D, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
+  if (q && (!qscale || !amax || q_stride % 8 != 0 || reinterpret_cast<uintptr_t>(q) % 8 != 0)) return hipErrorInvalidValue;
   // 4-column chunks (D = 768, profiles/r2s/ln_bwd_w4_ab.log): 79 -> 64 us per call (91 -> 79 with the
   // linked dropout backward); forcing 4 waves/SIMD (<= 128 VGPRs) spilled 18 VGPRs and took 114 us.
   // 4-column chunks when they tile the row over the 64 lanes exactly and 8-column ones do not
@@ -417,7 +447,7 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   const dim3 grid(nblk), block(256);
 #define PVR_LN_BWD(MC, W)                                                                                                   \
   hipLaunchKernelGGL((ln_bwd_kernel<MC, W>), grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, \
-                     dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, rows, D)
+                     dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, q, q_stride, qscale, amax, rows, D)
   if (use_w4) {
     switch (D / 256) {
       case 3: PVR_LN_BWD(3, 4); break;  // D = 768

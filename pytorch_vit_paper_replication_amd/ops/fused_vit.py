@@ -89,16 +89,34 @@ class PatchEmbedFn(torch.autograd.Function):
         return (None,) * 10
 
 
+LN_BWD_FP8_COPY = True  # the LayerNorm backward writes dx1 / dz2's e5m2 copies (False: quantize passes, A/B)
+
+
+def _ln_grad_quant(f8d, which: int, shape, device):
+    """Producer-side e5m2 copy of a LayerNorm-backward output for gradient slot ``which`` of the fp8
+    block ``f8d = (Fp8State, block)``: (layernorm_bwd kwargs, (copy, dequant scale)) once the slot is
+    calibrated, else ({}, None) (the first step calibrates it through the quantize pass)."""
+    if f8d is None or not LN_BWD_FP8_COPY:
+        return {}, None
+    prod = f8d[0].grad_producer(f8d[1], which)
+    if prod is None:
+        return {}, None
+    meta, slot = prod
+    q = torch.empty(shape, dtype=torch.uint8, device=device)
+    kw = dict(q_out=q, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1])
+    return kw, (q, meta.dscale[slot:slot + 1])
+
+
 class BlockLink:
     """Backward hand-off between consecutive encoder blocks. Block i's final LayerNorm backward
     produces dx for block i-1 and, in the same pass, block i-1's fc2 dropout backward (dz2) and fc2
     bias gradient; block i-1's backward then starts from dz2 instead of re-reading dx with a
     column-sum kernel."""
 
-    __slots__ = ("drop2", "b2", "dz2", "done")
+    __slots__ = ("drop2", "b2", "dz2", "dz2_q", "done")
 
     def __init__(self, drop2, b2):
-        self.drop2, self.b2, self.dz2, self.done = drop2, b2, None, False
+        self.drop2, self.b2, self.dz2, self.dz2_q, self.done = drop2, b2, None, None, False
 
 
 def block_links(blocks, drops2):
@@ -247,9 +265,14 @@ class EncoderBlockFn(torch.autograd.Function):
 
         # ---- MLP branch: x2 = x1 + drop2(h . W2^T + b2),  h = drop1(gelu(u)),  u = xn2 . W1^T + b1
         if own is not None and own.done:
-            # the next block's LayerNorm backward already produced dz2 and d(b2)
+            # the next block's LayerNorm backward already produced dz2 and d(b2) (and, on the fp8
+            # path, dz2's e5m2 copy: no quantize pass before the fc2 dgrad)
             dz2 = own.dz2 if own.dz2 is not None else dx2
             own.dz2 = None
+            if own.dz2_q is not None:
+                if f8d is not None:
+                    pre_q[0] = own.dz2_q
+                own.dz2_q = None
         elif drop2 is not None:
             dz2 = torch.empty_like(dx2)
             gemm.bias_grad(dx2, g(b2), drop=drop2, dz=dz2)
@@ -271,8 +294,12 @@ class EncoderBlockFn(torch.autograd.Function):
         store.on_side(mlp_wgrads, dz2, h, du, xn2, *side8(0, 1))  # weight grads off the critical path
         dxn2 = dgrad(du, w1, 1)
         dx1 = torch.empty_like(dx2)
-        # dx1 = dx2 + LN2'(dxn2); d(bo) = colsum(dx1) reduced in the same kernel
-        ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T, dsum=g(bo))
+        # dx1 = dx2 + LN2'(dxn2); d(bo) = colsum(dx1) reduced in the same kernel; on the fp8 path the
+        # kernel also writes dx1's e5m2 copy for the out-proj dgrad (grad slot 2) once it is calibrated
+        q_kw, q_dx1 = _ln_grad_quant(f8d, 2, dx1.shape, dx1.device)
+        ext.layernorm_bwd(dxn2, D, x1, D, mean2, rstd2, ln2w, dx2, D, dx1, D, g(ln2w), g(ln2b), T, dsum=g(bo), **q_kw)
+        if q_dx1 is not None:
+            pre_q[2] = q_dx1
         store.grad_ready([w2, b2, w1, b1, ln2w, ln2b])
         # ---- attention branch: x1 = x + (attn(qkv(xn1)) . Wo^T + bo)
         gwo, gwqkv = g(wo), g(wqkv)
@@ -320,9 +347,12 @@ class EncoderBlockFn(torch.autograd.Function):
             # the previous block's fc2 dropout backward and bias gradient ride along with dx
             seed, soff, p = gemm._drop_args(prev.drop2)
             dzp = torch.empty_like(dx2) if seed is not None else None
+            # fp8: the previous block's dz2 (= dz, or dx without dropout) leaves as e5m2 too (its grad slot 0)
+            pf8 = (f8d[0], f8d[1] - 1) if f8d is not None and f8d[1] > 0 else None
+            q_kw, q_dz = _ln_grad_quant(pf8, 0, dx.shape, dx.device)
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T,
-                              dsum=g(prev.b2), dz=dzp, seed=seed, seed_offset=soff, drop_p=p)
-            prev.dz2, prev.done = dzp, True
+                              dsum=g(prev.b2), dz=dzp, seed=seed, seed_offset=soff, drop_p=p, **q_kw)
+            prev.dz2, prev.dz2_q, prev.done = dzp, q_dz, True
         else:
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)
         store.grad_ready([bo, wo, bqkv, wqkv, ln1w, ln1b])

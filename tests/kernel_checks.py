@@ -591,6 +591,48 @@ def check_layernorm_fwd_q8(T=3000, D=1280):
     return (f"layernorm_fwd_q8 T{T} D{D}", m, {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "ln_not_identical": 0})
 
 
+def check_layernorm_bwd_q8(T=3000, D=1280, linked=False, p=0.1):
+    """LayerNorm backward with the fused e5m2 copy of the gradient it writes last (dz with the linked
+    dropout backward, else dx): dx / dz / dgamma / dbeta / dsum bit-identical to the plain backward
+    (f32 atomics aside: the same kernel order), the copy within one fp8 step of quantizing the bf16
+    output with the same scale, and amax = max|output| (to bf16 rounding)."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    x = bf(rnd(T, D) * 2 + 0.5)
+    w, b = rnd(D) * 0.5 + 1, rnd(D) * 0.1
+    _, mean, rstd = ext.layernorm_fwd(x, w, b, 1e-5, T, D)
+    dy, dres = bf(rnd(T, D)), bf(rnd(T, D))
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2)
+    meta.calibrated[0] = True
+    meta.qscale.fill_(2.0)
+    meta.dscale.copy_(1.0 / meta.qscale)
+    seed = torch.tensor([4242], dtype=torch.int64, device=DEV)
+    outs = []
+    for quant in (False, True):
+        dx, dz = torch.empty_like(x), (torch.empty_like(x) if linked else None)
+        dw, db, ds = (torch.zeros(D, device=DEV) for _ in range(3))
+        kw = dict(dsum=ds, dz=dz, seed=seed if linked else None, seed_offset=3 << 32, drop_p=p if linked else 0.0)
+        q = None
+        if quant:
+            q = torch.empty(T, D, dtype=torch.uint8, device=DEV)
+            kw.update(q_out=q, q_scale=meta.qscale[0:1], q_amax=meta.amax[0:1])
+        ext.layernorm_bwd(dy, D, x, D, mean, rstd, w, dres, D, dx, D, dw, db, T, **kw)
+        outs.append((dx, dz, dw, db, ds, q))
+    (dx0, dz0, dw0, db0, ds0, _), (dx1, dz1, dw1, db1, ds1, q) = outs
+    y = dz1 if linked else dx1
+    ref = torch.empty(T, D, dtype=torch.uint8, device=DEV)
+    ext.fp8_quant(y, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), F8.E5M2)
+    amax = meta.amax.view(torch.float32)[0].item()
+    same = torch.equal(dx0, dx1) and (not linked or torch.equal(dz0, dz1))
+    sums = max(errs(dw1, dw0)[0], errs(db1, db0)[0], errs(ds1, ds0)[0])
+    m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
+         "amax_rel": abs(amax - y.float().abs().max().item()) / y.float().abs().max().item(),
+         "grad_not_identical": float(not same), "sums_l2": sums}
+    return (f"layernorm_bwd_q8 e5m2 T{T} D{D} linked{int(linked)}", m,
+            {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 8e-3, "grad_not_identical": 0, "sums_l2": 1e-6})  # amax: bf16 rounding <= 2^-8
+
+
 def check_attn_fwd_q8(B=2, N=257, H=4, dh=80):
     """Attention forward with the fused e4m3 output copy: O / lse bit-identical to the plain forward,
     the copy within one fp8 step of quantizing O, amax = max|O| (up to O's bf16 rounding)."""
@@ -1212,6 +1254,9 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_wgrad_fp8_mn(300, 768, 256),
         lambda: check_fp8_transpose(257, 768, 0),
         lambda: check_layernorm_fwd_q8(50, 768),
+        check_layernorm_bwd_q8,                                   # D 1280 (H/14): 8-column chunks
+        lambda: check_layernorm_bwd_q8(2000, 768, linked=True),   # D 768: 4-column chunks + dz
+        lambda: check_layernorm_bwd_q8(3000, 1280, linked=True),
         lambda: check_gemm_fp8_producer(1030, 768, 1280, True),
         check_vit_fp8,
         check_vit_fp8_dgrad,
