@@ -196,7 +196,8 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, torch::Tensor w, torch
 // layernorm_fwd + the output's e4m3 copy q_out [rows][D] (uint8) quantized with *q_scale, amax
 // recorded into *q_amax (int32 float bits): the fp8 forward's quantize pass folded into the LayerNorm
 std::vector<torch::Tensor> layernorm_fwd_q8(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps, int64_t rows,
-                                            int64_t x_row_stride, torch::Tensor q_out, torch::Tensor q_scale, torch::Tensor q_amax) {
+                                            int64_t x_row_stride, torch::Tensor q_out, torch::Tensor q_scale, torch::Tensor q_amax,
+                                            bool skip_y) {
   const int64_t D = w.numel();
   auto y = torch::empty({rows, D}, x.options());
   auto mean = torch::empty({rows}, x.options().dtype(torch::kFloat32));
@@ -207,7 +208,8 @@ std::vector<torch::Tensor> layernorm_fwd_q8(torch::Tensor x, torch::Tensor w, to
                   reinterpret_cast<uintptr_t>(q_out.data_ptr()) % 8 == 0,
               "layernorm_fwd_q8: q_out uint8 [rows][D], 8-byte aligned rows");
   TORCH_CHECK(q_amax.is_cuda() && q_amax.scalar_type() == torch::kInt32, "layernorm_fwd_q8: q_amax int32");
-  check(pvr_layernorm_fwd_q8(bf(x, "x"), x_row_stride, f32(w, "w"), f32(b, "b"), bf_mut(y, "y"), D,
+  // skip_y: only the e4m3 copy is consumed (the bf16 y stays allocated, unwritten)
+  check(pvr_layernorm_fwd_q8(bf(x, "x"), x_row_stride, f32(w, "w"), f32(b, "b"), skip_y ? nullptr : bf_mut(y, "y"), D,
                              reinterpret_cast<uint8_t*>(q_out.data_ptr()), q_out.stride(0), f32(q_scale, "q_scale"),
                              reinterpret_cast<unsigned*>(q_amax.data_ptr<int32_t>()), f32_mut(mean, "mean"), f32_mut(rstd, "rstd"),
                              (int)rows, (int)D, (float)eps, stream()),
@@ -530,8 +532,12 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
               int64_t epi, torch::Tensor scale_a, torch::Tensor scale_b, c10::optional<torch::Tensor> bias,
               c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> seed, int64_t seed_offset,
               double drop_p, c10::optional<torch::Tensor> colsum, c10::optional<torch::Tensor> q_out,
-              c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, int64_t q_fmt) {
+              c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, int64_t q_fmt, bool c_skip) {
   pvr::GemmParams p{};
+  // c_skip: only the fp8 copy (or aux / column sums) of the output is consumed; the bf16 stores are
+  // dropped (register-direct epilogue; other epilogues still write C, which is allocated)
+  TORCH_CHECK(!c_skip || epi == 1 || epi == 2, "gemm_fp8: c_skip with the GELU / dGELU epilogues only");
+  p.c_skip = c_skip ? 1 : 0;
   p.drop_scale = 1.f;
   p.M = (int)M; p.N = (int)N; p.K = (int)K;
   p.A = reinterpret_cast<const uint16_t*>(u8(A, "A")); p.lda = A.stride(0); p.a_kcontig = 1;
@@ -894,7 +900,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("scale_a"), py::arg("scale_b"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("aux") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0,
         py::arg("drop_p") = 0.0, py::arg("colsum") = py::none(), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
-        py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0);
+        py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0, py::arg("c_skip") = false);
   m.def("fp8_transpose", &fp8_transpose);
   m.def("gemm_fp8_wgrad_mn", &gemm_fp8_wgrad_mn);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));

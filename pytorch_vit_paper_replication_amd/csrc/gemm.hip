@@ -1015,7 +1015,8 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   // rows [mb, min(M, mb + 128)) of C (and of the residual / aux tensors) from the wave's first row
   const int rows = max(0, min(128, p.M - mb));
   const uint32_t OOB = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t crs = make_rsrc((const uint16_t*)p.C + (int64_t)mb * p.ldc, rows ? (uint32_t)(((int64_t)(rows - 1) * p.ldc + p.N) * 2) : 0);
+  const __amdgpu_buffer_rsrc_t crs =
+      make_rsrc((const uint16_t*)p.C + (int64_t)mb * p.ldc, rows && !p.c_skip ? (uint32_t)(((int64_t)(rows - 1) * p.ldc + p.N) * 2) : 0);
   __amdgpu_buffer_rsrc_t xrs = crs;  // residual (BF16) / aux (GELU store, DGELU load)
   int64_t ldx = p.ldc;
   if constexpr (EPI == EPI_BF16 && RES) {

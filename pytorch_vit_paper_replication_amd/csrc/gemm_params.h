@@ -32,6 +32,9 @@ struct GemmParams {
   // quantization of the delayed-scaling recipe): q_out[m][n] = fp8(out * (*q_scale)) (fmt 0 e4m3,
   // 1 e5m2, row stride ld_q bytes), *q_amax = max(*q_amax, max |out|) (float bits, NaN-propagating)
   uint8_t* q_out; int64_t ld_q; const float* q_scale; unsigned* q_amax; int q_fmt;
+  // c_skip = 1: the bf16 output is not stored (register-direct epilogue: 0-byte C resource, every
+  // store dropped by the range check) - only its fp8 copy / aux / column sums are consumed
+  int c_skip;
 };
 
 }  // namespace pvr

@@ -206,25 +206,28 @@ def _quant_args(quant, rows: int, cols: int, device):
     return kw, (q, meta.dscale[slot:slot + 1])
 
 
-def layernorm_fwd_q8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, quant):
+def layernorm_fwd_q8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float, quant, skip_y: bool = False):
     """LayerNorm forward that also writes the output's e4m3 copy with a calibrated slot's delayed scale
     (``quant=(meta, slot)``, ``Fp8Meta.producer``) and records its amax:
     returns ``(y, mean, rstd, (y_fp8, dequant scale))``."""
     meta, slot = quant
     T, D = x.shape
     q = torch.empty(T, D, dtype=torch.uint8, device=x.device)
-    y, mean, rstd = _ext.ext().layernorm_fwd_q8(x, w, b, eps, T, D, q, meta.qscale[slot:slot + 1], meta.amax[slot:slot + 1])
+    y, mean, rstd = _ext.ext().layernorm_fwd_q8(x, w, b, eps, T, D, q, meta.qscale[slot:slot + 1], meta.amax[slot:slot + 1],
+                                                bool(skip_y))
     return y, mean, rstd, (q, meta.dscale[slot:slot + 1])
 
 
 def linear_fwd_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
                    bias: Optional[torch.Tensor] = None, *, resid: Optional[torch.Tensor] = None, drop=None,
-                   gelu_aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, quant=None):
+                   gelu_aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, quant=None,
+                   skip_out: bool = False):
     """y = resid + dropout(dequant(xq . wq^T) + bias), or the GELU variant (see gemm.linear_fwd).
 
     ``quant=(meta, slot)`` (GELU variant, a calibrated slot: ``Fp8Meta.producer``): the epilogue also
     writes y's fp8 copy with the slot's delayed scale and records y's amax, so the next GEMM needs no
-    quantize pass; returns ``(y, (y_fp8, dequant scale))`` then."""
+    quantize pass; returns ``(y, (y_fp8, dequant scale))`` then. ``skip_out`` (with ``quant``): the bf16
+    y is not stored (allocated, unwritten) - for when every consumer reads the fp8 copy."""
     T, K = xq.shape
     N = wq.shape[0]
     if out is None:
@@ -232,13 +235,14 @@ def linear_fwd_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: tor
     seed, soff, p = gemm._drop_args(drop)
     epi = gemm.EPI_GELU if gelu_aux is not None else gemm.EPI_BF16
     kw, q = _quant_args(quant, T, N, xq.device)
-    _ext.ext().gemm_fp8(xq, E4M3, wq, E4M3, out, T, N, K, epi, xs, ws, bias, resid, gelu_aux, seed, soff, p, **kw)
+    _ext.ext().gemm_fp8(xq, E4M3, wq, E4M3, out, T, N, K, epi, xs, ws, bias, resid, gelu_aux, seed, soff, p,
+                        c_skip=bool(skip_out and quant is not None), **kw)
     return out if quant is None else (out, q)
 
 
 def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts: torch.Tensor, *,
                      dgelu_aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
-                     out: Optional[torch.Tensor] = None, quant=None):
+                     out: Optional[torch.Tensor] = None, quant=None, skip_out: bool = False):
     """dx = dequant(gq (e5m2) . wtq^T (e4m3, W^T rows)) [* dgelu_aux]; ``quant`` as in linear_fwd_fp8
     (dGELU variant: the e5m2 copy of dx for the next dgrad GEMM)."""
     T, N = gq.shape
@@ -247,7 +251,8 @@ def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts:
         out = torch.empty(T, K, dtype=torch.bfloat16, device=gq.device)
     epi = gemm.EPI_DGELU if dgelu_aux is not None else gemm.EPI_BF16
     kw, q = _quant_args(quant, T, K, gq.device)
-    _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum, **kw)
+    _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum,
+                        c_skip=bool(skip_out and quant is not None), **kw)
     return out if quant is None else (out, q)
 
 

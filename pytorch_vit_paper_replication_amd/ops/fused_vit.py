@@ -148,10 +148,18 @@ class EncoderBlockFn(torch.autograd.Function):
         u = (torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
              if need_bwd or f8 is not None else None)
         q1 = f8[0].act_producer(f8[1], 0) if f8 is not None else None
+
+        def fp8_only(which_grad: int, which_act: int) -> bool:
+            # the bf16 activation is read by nothing but the weight gradient of (gradient slot, activation
+            # slot), and that one is certain to run in fp8 from the activation's e4m3 copy (both slots
+            # calibrated, so they stay so): the producer then stores only the fp8 copy (HBM writes saved)
+            return (need_bwd and ctx.f8d is not None and T >= 256 and DGRAD_TAP is None
+                    and f8[0].wgrad_ready(f8[1], which_grad, which_act))
+
         if q1 is not None:  # fp8 forward, calibrated: xn1's e4m3 copy from the LayerNorm itself
             from . import fp8 as F8
 
-            xn1, mean1, rstd1, xq1 = F8.layernorm_fwd_q8(x, ln1w, ln1b, eps1, q1)
+            xn1, mean1, rstd1, xq1 = F8.layernorm_fwd_q8(x, ln1w, ln1b, eps1, q1, skip_y=fp8_only(3, 0))
         else:
             xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
         if f8 is None:
@@ -187,13 +195,13 @@ class EncoderBlockFn(torch.autograd.Function):
             x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
             q2 = st.act_producer(blk, 2)
             if q2 is not None:
-                xn2, mean2, rstd2, (a, s_) = F8.layernorm_fwd_q8(x1, ln2w, ln2b, eps2, q2)
+                xn2, mean2, rstd2, (a, s_) = F8.layernorm_fwd_q8(x1, ln2w, ln2b, eps2, q2, skip_y=fp8_only(1, 2))
             else:
                 xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
                 a, s_ = st.act_quant(xn2, blk, 2)
             acts8.append(a)
             hq = st.act_producer(blk, 3)  # h's e4m3 copy from the fc1 epilogue (calibrated slot)
-            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq)
+            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq, skip_out=fp8_only(0, 3))
             if hq is not None:
                 h, (a, s_) = h
             else:
@@ -235,7 +243,7 @@ class EncoderBlockFn(torch.autograd.Function):
             ts = [grad8(w) for w in whichs] + (list(acts8) if acts8 is not None else [])
             return tuple(t for t in ts if t is not None)
 
-        def dgrad(dy, w, which, dgelu_aux=None, colsum=None):
+        def dgrad(dy, w, which, dgelu_aux=None, colsum=None, skip_out=False):
             wt = store.bf16_t(w)
             if f8d is not None and wt is not None:
                 from . import fp8 as F8
@@ -246,7 +254,8 @@ class EncoderBlockFn(torch.autograd.Function):
                 wq, ws = st.weight(wt, ~id(w), store.generation, store.layout_key())
                 # the dGELU dgrad (fc2) also writes dU's e5m2 copy for the fc1 dgrad (grad slot 1)
                 nq = st.grad_producer(blk, 1) if dgelu_aux is not None else None
-                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq)
+                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq,
+                                          skip_out=skip_out and DGRAD_TAP is None)
                 if nq is not None:
                     out, pre_q[1] = out
             else:
@@ -283,7 +292,11 @@ class EncoderBlockFn(torch.autograd.Function):
         # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
         gb1 = g(b1)
         gw2, gw1 = g(w2), g(w1)
-        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=gb1)
+        # dU's bf16 copy is not stored when both of its readers take the e5m2 copy the dGELU epilogue
+        # writes: the fc1 dgrad (fp8, W1^T shadow present) and the fc1 weight gradient (fp8, calibrated)
+        du_fp8_only = (f8d is not None and T >= 256 and store.bf16_t(w1) is not None
+                       and f8d[0].wgrad_ready(f8d[1], 1, 2) and f8d[0].grad_producer(f8d[1], 1) is not None)
+        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=gb1, skip_out=du_fp8_only)
 
         def mlp_wgrads():
             if gw2 is not None:

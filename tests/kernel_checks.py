@@ -793,6 +793,43 @@ def check_vit_fp8(B=4):
     return (f"vit fp8 fwd vs fp32, loss {losses[0]:.3f}->{losses[-1]:.3f}", m, lim(8.5e-2, 1e-1, loss_not_falling=0))
 
 
+def check_vit_fp8_bf16_skip(B=4, steps=4):
+    """fp8 training with the bf16 copies that only fp8 consumers read left unwritten (xn1, xn2, h in
+    the forward, dU in the backward, once their weight gradients run in fp8 from the e4m3 / e5m2
+    copies) against the same training with every bf16 copy written (a no-op DGRAD_TAP turns the skips
+    off): same losses and parameters (f32 atomics may reorder additions). A skipped tensor read by
+    anything would show up as garbage here."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops import fused_vit
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+
+    res = []
+    for skip in (True, False):
+        torch.manual_seed(0)
+        m = ViT(**dict(_FP8_CFG, mlp_dropout=0.1)).to(DEV).enable_fp8()
+        opt = FusedAdam(m.parameters(), lr=1e-3)
+        x = torch.rand(B * 64, 3, 64, 64, device=DEV)
+        y = torch.randint(0, 10, (B * 64,), device=DEV)
+        fused_vit.DGRAD_TAP = None if skip else (lambda which, t: None)
+        try:
+            losses = []
+            for _ in range(steps):
+                loss = cross_entropy(m(x), y)
+                opt.zero_grad()
+                loss.backward()
+                opt.step(clip_norm=1.0)
+                losses.append(loss.item())
+        finally:
+            fused_vit.DGRAD_TAP = None
+        res.append((losses, m._pvr_store.flat.detach().clone()))
+    (l0, p0), (l1, p1) = res
+    m = {"loss_diff": max(abs(a - b) for a, b in zip(l0, l1)), "param_l2": errs(p0, p1)[0],
+         "nonfinite": float(not (torch.isfinite(p0).all().item() and all(math.isfinite(v) for v in l0)))}
+    return (f"vit fp8 bf16-copy skips vs all copies written, {steps} steps (loss {l0[0]:.3f}->{l0[-1]:.3f})", m,
+            {"loss_diff": 2e-5, "param_l2": 5e-5, "nonfinite": 0})  # measured 1.7e-6 / 4.4e-6 (f32 atomics reorder)
+
+
 def check_vit_fp8_dgrad(B=4):
     """fp8 dgrad GEMMs (enable_fp8(dgrad=True): e5m2 gradients x e4m3 W^T) against the bf16 dgrads of the
     same fp8-forward model, PER dgrad output tensor (fc2 / fc1 / out-proj / qkv of every block, tapped
@@ -1261,6 +1298,7 @@ def all_checks() -> List[Callable[[], Result]]:
         check_vit_fp8,
         check_vit_fp8_dgrad,
         check_vit_fp8_wgrad,
+        check_vit_fp8_bf16_skip,
         check_fp8_nonfinite_recovery,
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
