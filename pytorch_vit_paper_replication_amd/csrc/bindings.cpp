@@ -26,7 +26,7 @@ hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
-hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t, const float*, unsigned*, int, int, hipStream_t);
+hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, uint8_t*, int64_t, const float*, unsigned*, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
 hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
@@ -243,7 +243,7 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
                    c10::optional<torch::Tensor> dw, c10::optional<torch::Tensor> db, int64_t rows,
                    c10::optional<torch::Tensor> dsum, c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> seed,
                    int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
-                   c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax) {
+                   c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool dz_nostore) {
   const int64_t D = w.numel();
   // optional e5m2 copy of the last-written gradient (dz if given, else dx) with a delayed scale
   // and an amax record: the producer-side quantization for the next fp8 dgrad GEMM
@@ -276,7 +276,7 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
   check(pvr_layernorm_bwd(bf(dy, "dy"), dy_stride, bf(x, "x"), x_stride, f32(mean, "mean"), f32(rstd, "rstd"), f32(w, "w"),
                           opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
                           opt_ptr<float>(db), opt_ptr<float>(dsum), dzp, ldz, d.seed, (uint64_t)seed_offset, d.thr, d.scale,
-                          qp, ldq, qs, qa, (int)rows, (int)D, stream()),
+                          dz_nostore ? 1 : 0, qp, ldq, qs, qa, (int)rows, (int)D, stream()),
         "layernorm_bwd");
 }
 
@@ -870,7 +870,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),
         py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none(),
         py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0,
-        py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none());
+        py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none(),
+        py::arg("dz_nostore") = false);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("splitk_epilogue", &splitk_epilogue);
   m.def("attn_bwd_bias_rows", &attn_bwd_bias_rows, py::arg("B"), py::arg("N"), py::arg("H"), py::arg("D"), py::arg("drop") = false);

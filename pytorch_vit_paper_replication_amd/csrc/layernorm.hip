@@ -200,7 +200,8 @@ struct RowVec<4> {
 // MAXCH chunks of W columns (chunk c = lane + 64 i). W = 4 where D / 8 is not a multiple of 64 but
 // D / 4 is (D = 768: 3 chunks of 4 per lane instead of 1.5 of 8, so no lane idles on the last chunk
 // and the smaller register footprint doubles the waves in flight: 4 per SIMD instead of 2).
-template <int MAXCH, int W>
+// Q8: the fp8-copy variant (qout / dz_nostore used); the bf16 instantiation carries none of it.
+template <int MAXCH, int W, bool Q8>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict__ dy, int64_t dy_stride,
                                                       const uint16_t* __restrict__ x, int64_t x_stride,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -210,12 +211,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dsum,
                                                       uint16_t* __restrict__ dz, int64_t dz_stride,
                                                       const uint64_t* __restrict__ seed_ptr, uint64_t seed_off, uint32_t thr,
-                                                      float dscale, uint8_t* __restrict__ qout, int64_t q_stride,
+                                                      float dscale, int dz_nostore, uint8_t* __restrict__ qout, int64_t q_stride,
                                                       const float* __restrict__ qscale, unsigned* __restrict__ amax, int rows,
                                                       int D) {
   __shared__ float red[4][MAXCH * 64 * W > 1280 ? 1280 : MAXCH * 64 * W];  // one partial at a time
   __shared__ float qred[4];
-  const float qs = qout ? *qscale : 1.f;
+  const float qs = Q8 ? *qscale : 1.f;
   float qam = 0.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = D / W;
@@ -309,11 +310,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
             o[j] = k0 ? o[j] * dscale : 0.f;
             o[j + 1] = k1 ? o[j + 1] * dscale : 0.f;
           }
+          if (!Q8 || !dz_nostore) {  // uniform; dz_nostore: only dz's e5m2 copy (qout) is consumed
 #pragma unroll
-          for (int j = 0; j < W; j += 2) q.u[j >> 1] = pack2bf(o[j], o[j + 1]);
-          q.store(dz + (int64_t)row * dz_stride + c * W);
+            for (int j = 0; j < W; j += 2) q.u[j >> 1] = pack2bf(o[j], o[j + 1]);
+            q.store(dz + (int64_t)row * dz_stride + c * W);
+          }
         }
-        if (qout) {  // uniform: e5m2 copy of the gradient written last (dz, else dx) for the next fp8 dgrad GEMM
+        if constexpr (Q8) {  // e5m2 copy of the gradient written last (dz, else dx) for the next fp8 dgrad GEMM
           uint32_t b4[W / 4];
 #pragma unroll
           for (int j = 0; j < W; j += 4) {
@@ -360,7 +363,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
     for (int col = threadIdx.x; col < D; col += 256)
       atomicAdd(outs[qn] + col, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
   }
-  if (qout) {  // max |gradient| of the block's rows: one atomic per workgroup (delayed-scaling amax record)
+  if constexpr (Q8) {  // max |gradient| of the block's rows: one atomic per workgroup (delayed-scaling amax record)
     qam = wave_max_nan(qam);
     if (lane == 0) qred[wave] = qam;
     __syncthreads();
@@ -426,12 +429,13 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
                                         const float* mean, const float* rstd, const float* w, const uint16_t* dres,
                                         int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
                                         float* dsum, uint16_t* dz, int64_t dz_stride, const uint64_t* seed_ptr,
-                                        uint64_t seed_off, uint32_t thr, float dscale, uint8_t* q, int64_t q_stride,
+                                        uint64_t seed_off, uint32_t thr, float dscale, int dz_nostore, uint8_t* q, int64_t q_stride,
                                         const float* qscale, unsigned* amax, int rows, int D, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
   if (q && (!qscale || !amax || q_stride % 8 != 0 || reinterpret_cast<uintptr_t>(q) % 8 != 0)) return hipErrorInvalidValue;
+  if (dz_nostore && (!dz || !q)) return hipErrorInvalidValue;  // skipping dz needs dz's fp8 copy
   // 4-column chunks (D = 768, profiles/r2s/ln_bwd_w4_ab.log): 79 -> 64 us per call (91 -> 79 with the
   // linked dropout backward); forcing 4 waves/SIMD (<= 128 VGPRs) spilled 18 VGPRs and took 114 us.
   // 4-column chunks when they tile the row over the 64 lanes exactly and 8-column ones do not
@@ -446,8 +450,9 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   if (nblk > cap) nblk = cap;
   const dim3 grid(nblk), block(256);
 #define PVR_LN_BWD(MC, W)                                                                                                   \
-  hipLaunchKernelGGL((ln_bwd_kernel<MC, W>), grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, \
-                     dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, q, q_stride, qscale, amax, rows, D)
+  hipLaunchKernelGGL(q ? (ln_bwd_kernel<MC, W, true>) : (ln_bwd_kernel<MC, W, false>), grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, \
+                     dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, dz_nostore, q, q_stride, qscale, amax, \
+                     rows, D)
   if (use_w4) {
     switch (D / 256) {
       case 3: PVR_LN_BWD(3, 4); break;  // D = 768

@@ -90,6 +90,14 @@ class PatchEmbedFn(torch.autograd.Function):
 
 
 LN_BWD_FP8_COPY = True  # the LayerNorm backward writes dx1 / dz2's e5m2 copies (False: quantize passes, A/B)
+# test hook: bf16 outputs left unwritten on the fp8 path (only their fp8 copies are consumed) are
+# filled with NaN, so any reader of one would poison the loss / gradients (tests/kernel_checks.py)
+POISON_SKIPPED = False
+
+
+def _poison(t: torch.Tensor, skipped: bool) -> None:
+    if skipped and POISON_SKIPPED:
+        t.fill_(float("nan"))
 
 
 def _ln_grad_quant(f8d, which: int, shape, device):
@@ -113,15 +121,15 @@ class BlockLink:
     bias gradient; block i-1's backward then starts from dz2 instead of re-reading dx with a
     column-sum kernel."""
 
-    __slots__ = ("drop2", "b2", "dz2", "dz2_q", "done")
+    __slots__ = ("drop2", "b2", "w2", "dz2", "dz2_q", "done")
 
-    def __init__(self, drop2, b2):
-        self.drop2, self.b2, self.dz2, self.dz2_q, self.done = drop2, b2, None, None, False
+    def __init__(self, drop2, b2, w2=None):
+        self.drop2, self.b2, self.w2, self.dz2, self.dz2_q, self.done = drop2, b2, w2, None, None, False
 
 
 def block_links(blocks, drops2):
     """(own link, previous block's link) per block, for EncoderBlockFn's ``links`` argument."""
-    own = [BlockLink(d, blk.mlp_block.mlp[3].bias) for blk, d in zip(blocks, drops2)]
+    own = [BlockLink(d, blk.mlp_block.mlp[3].bias, blk.mlp_block.mlp[3].weight) for blk, d in zip(blocks, drops2)]
     return [(own[i], own[i - 1] if i else None) for i in range(len(own))]
 
 
@@ -159,7 +167,9 @@ class EncoderBlockFn(torch.autograd.Function):
         if q1 is not None:  # fp8 forward, calibrated: xn1's e4m3 copy from the LayerNorm itself
             from . import fp8 as F8
 
-            xn1, mean1, rstd1, xq1 = F8.layernorm_fwd_q8(x, ln1w, ln1b, eps1, q1, skip_y=fp8_only(3, 0))
+            skip1 = fp8_only(3, 0)
+            xn1, mean1, rstd1, xq1 = F8.layernorm_fwd_q8(x, ln1w, ln1b, eps1, q1, skip_y=skip1)
+            _poison(xn1, skip1)
         else:
             xn1, mean1, rstd1 = ext.layernorm_fwd(x, ln1w, ln1b, eps1, T, D)
         if f8 is None:
@@ -195,15 +205,19 @@ class EncoderBlockFn(torch.autograd.Function):
             x1 = F8.linear_fwd_fp8(a, s_, *wq[1], bo, resid=x)
             q2 = st.act_producer(blk, 2)
             if q2 is not None:
-                xn2, mean2, rstd2, (a, s_) = F8.layernorm_fwd_q8(x1, ln2w, ln2b, eps2, q2, skip_y=fp8_only(1, 2))
+                skip2 = fp8_only(1, 2)
+                xn2, mean2, rstd2, (a, s_) = F8.layernorm_fwd_q8(x1, ln2w, ln2b, eps2, q2, skip_y=skip2)
+                _poison(xn2, skip2)
             else:
                 xn2, mean2, rstd2 = ext.layernorm_fwd(x1, ln2w, ln2b, eps2, T, D)
                 a, s_ = st.act_quant(xn2, blk, 2)
             acts8.append(a)
             hq = st.act_producer(blk, 3)  # h's e4m3 copy from the fc1 epilogue (calibrated slot)
-            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq, skip_out=fp8_only(0, 3))
+            skip_h = hq is not None and fp8_only(0, 3)
+            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq, skip_out=skip_h)
             if hq is not None:
                 h, (a, s_) = h
+                _poison(h, skip_h)
             else:
                 a, s_ = st.act_quant(h, blk, 3)
             acts8.append(a)
@@ -254,10 +268,11 @@ class EncoderBlockFn(torch.autograd.Function):
                 wq, ws = st.weight(wt, ~id(w), store.generation, store.layout_key())
                 # the dGELU dgrad (fc2) also writes dU's e5m2 copy for the fc1 dgrad (grad slot 1)
                 nq = st.grad_producer(blk, 1) if dgelu_aux is not None else None
-                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq,
-                                          skip_out=skip_out and DGRAD_TAP is None)
+                skip = skip_out and DGRAD_TAP is None and nq is not None
+                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq, skip_out=skip)
                 if nq is not None:
                     out, pre_q[1] = out
+                    _poison(out, skip)
             else:
                 out = gemm.linear_dgrad(dy, store.bf16(w), dgelu_aux=dgelu_aux, wt=wt, colsum=colsum)
             if DGRAD_TAP is not None:
@@ -363,8 +378,15 @@ class EncoderBlockFn(torch.autograd.Function):
             # fp8: the previous block's dz2 (= dz, or dx without dropout) leaves as e5m2 too (its grad slot 0)
             pf8 = (f8d[0], f8d[1] - 1) if f8d is not None and f8d[1] > 0 else None
             q_kw, q_dz = _ln_grad_quant(pf8, 0, dx.shape, dx.device)
+            # dz's bf16 copy is not stored when the previous block reads only its e5m2 copy: the fc2 dgrad
+            # (fp8, W2^T shadow present) and the fc2 weight gradient (fp8, calibrated slots)
+            dz_nostore = (q_dz is not None and dzp is not None and T >= 256 and DGRAD_TAP is None
+                          and prev.w2 is not None and store.bf16_t(prev.w2) is not None
+                          and pf8[0].wgrad_ready(pf8[1], 0, 3))
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T,
-                              dsum=g(prev.b2), dz=dzp, seed=seed, seed_offset=soff, drop_p=p, **q_kw)
+                              dsum=g(prev.b2), dz=dzp, seed=seed, seed_offset=soff, drop_p=p, dz_nostore=dz_nostore, **q_kw)
+            if dzp is not None:
+                _poison(dzp, dz_nostore)
             prev.dz2, prev.dz2_q, prev.done = dzp, q_dz, True
         else:
             ext.layernorm_bwd(dxn1, D, x, D, mean1, rstd1, ln1w, dx1, D, dx, D, g(ln1w), g(ln1b), T)

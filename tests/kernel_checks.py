@@ -795,10 +795,13 @@ def check_vit_fp8(B=4):
 
 def check_vit_fp8_bf16_skip(B=4, steps=4):
     """fp8 training with the bf16 copies that only fp8 consumers read left unwritten (xn1, xn2, h in
-    the forward, dU in the backward, once their weight gradients run in fp8 from the e4m3 / e5m2
-    copies) against the same training with every bf16 copy written (a no-op DGRAD_TAP turns the skips
-    off): same losses and parameters (f32 atomics may reorder additions). A skipped tensor read by
-    anything would show up as garbage here."""
+    the forward, dU and the linked dz in the backward, once their weight gradients run in fp8 from
+    the e4m3 / e5m2 copies). Those unwritten tensors are filled with NaN (POISON_SKIPPED), so a
+    reader of any of them would make the gradients non-finite. From the same state (one calibrating
+    step), the second step's gradients must equal those of the same step with every bf16 copy
+    written (a no-op DGRAD_TAP turns the skips off) up to f32-atomic reordering; a few more steps
+    must stay finite and close (the fp8 quantization amplifies reordered low bits into whole fp8
+    steps, so trajectories drift slightly between any two runs with different kernel timing)."""
     from pytorch_vit_paper_replication_amd.models import ViT
     from pytorch_vit_paper_replication_amd.ops import fused_vit
     from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
@@ -812,22 +815,27 @@ def check_vit_fp8_bf16_skip(B=4, steps=4):
         x = torch.rand(B * 64, 3, 64, 64, device=DEV)
         y = torch.randint(0, 10, (B * 64,), device=DEV)
         fused_vit.DGRAD_TAP = None if skip else (lambda which, t: None)
+        fused_vit.POISON_SKIPPED = skip
         try:
-            losses = []
-            for _ in range(steps):
+            losses, g2 = [], None
+            for i in range(steps):
                 loss = cross_entropy(m(x), y)
                 opt.zero_grad()
                 loss.backward()
+                if i == 1:  # first step with the skips active, from an identical state
+                    g2 = m._pvr_store.grad_flat.detach().clone()
                 opt.step(clip_norm=1.0)
                 losses.append(loss.item())
         finally:
             fused_vit.DGRAD_TAP = None
-        res.append((losses, m._pvr_store.flat.detach().clone()))
-    (l0, p0), (l1, p1) = res
-    m = {"loss_diff": max(abs(a - b) for a, b in zip(l0, l1)), "param_l2": errs(p0, p1)[0],
-         "nonfinite": float(not (torch.isfinite(p0).all().item() and all(math.isfinite(v) for v in l0)))}
-    return (f"vit fp8 bf16-copy skips vs all copies written, {steps} steps (loss {l0[0]:.3f}->{l0[-1]:.3f})", m,
-            {"loss_diff": 2e-5, "param_l2": 5e-5, "nonfinite": 0})  # measured 1.7e-6 / 4.4e-6 (f32 atomics reorder)
+            fused_vit.POISON_SKIPPED = False
+        res.append((losses, g2, m._pvr_store.flat.detach().clone()))
+    (l0, g0, p0), (l1, g1, p1) = res
+    m = {"grad_l2": errs(g0, g1)[0], "nonfinite": float(not (torch.isfinite(g0).all().item() and torch.isfinite(p0).all().item()
+                                                          and all(math.isfinite(v) for v in l0))),
+         "loss_diff": max(abs(a - b) for a, b in zip(l0, l1)), "param_l2": errs(p0, p1)[0]}
+    return (f"vit fp8 bf16-copy skips (NaN-poisoned) vs all copies written, {steps} steps (loss {l0[0]:.3f}->{l0[-1]:.3f})", m,
+            {"grad_l2": 1e-6, "nonfinite": 0, "loss_diff": 2e-3, "param_l2": 1e-3})  # measured grad_l2 2.9e-8
 
 
 def check_vit_fp8_dgrad(B=4):
