@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
     p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
     p.add_argument("--pg-only", action="store_true", help="initialise a world-1 RCCL process group but do not wrap in DDP (A/B)")
-    p.add_argument("--comm", choices=["auto", "native", "native-mesh", "torch"], default="auto", help="DDP gradient transport")
+    p.add_argument("--comm", choices=["auto", "torch"], default="auto", help="DDP gradient transport (torch.distributed / RCCL)")
     p.add_argument("--bucket-mb", type=float, default=28.0)
     p.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                    help="gradient wire format of the DDP all-reduce (bf16: persistent bf16 mirror of the buckets)")
@@ -52,6 +52,8 @@ def parse():
                    help="serving throughput instead: eval-mode forward under inference_mode (no backward / optimizer)")
     p.add_argument("--serial-wgrad", action="store_true",
                    help="weight-gradient GEMMs on the main stream (no side stream): clean per-kernel times for profiles")
+    p.add_argument("--no-gemm-tail", action="store_true",
+                   help="A/B: no split-K tail on the last dispatch round of the one-tile-per-workgroup GEMMs")
     p.add_argument("--main-prio", type=int, default=-1,
                    help="run the step on a stream of this priority: -1 (default) puts the dgrad chain above the weight-gradient side stream; 0 = default stream")
     return p.parse_args()
@@ -91,6 +93,10 @@ def main():
 
         param_store.SIDE_WGRAD = False
     rank, world, device = init_distributed()
+    if args.no_gemm_tail and args.impl == "fused":
+        from pytorch_vit_paper_replication_amd import _ext
+
+        _ext.ext().set_gemm_tail(False)
     if args.gpus > 1 and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU (torch.distributed.run)")
     if (args.force_ddp or args.pg_only) and not torch.distributed.is_initialized():

@@ -77,6 +77,8 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
     hip_flags = [
         f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
         "-munsafe-fp-atomics", "-Wno-unused-result",
+        # a kernel parameter shadowed by a local array faulted a GPU in round 3: shadowing is an error
+        "-Wshadow", "-Werror=shadow",
     ] + list(extra_flags)
     for src in hip_srcs:
         obj = build_dir / (src.stem + ".o")

@@ -625,9 +625,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
             sv += dv[e][f][r];
           }
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          sk += __shfl_xor(sk, o, 64);
-          sv += __shfl_xor(sv, o, 64);
+        for (int sh = 1; sh < 16; sh <<= 1) {
+          sk += __shfl_xor(sk, sh, 64);
+          sv += __shfl_xor(sv, sh, 64);
         }
         if (li == 0) {
           rk[wave * DH + 16 * e + 4 * g + r] = sk * scale;
@@ -685,9 +685,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + u * (int)blockDim.x + (int)threadIdx.x;
-        const int q = i < n4 ? i / C4 : N, c = 4 * (i - (i / C4) * C4);
-        ao[u] = ((uint32_t)q * (uint32_t)D + (uint32_t)(h * DH + c)) * 4;
-        oo[u] = ((uint32_t)q * (uint32_t)ld_dq + (uint32_t)c) * 2;
+        const int qrow = i < n4 ? i / C4 : N, col = 4 * (i - (i / C4) * C4);
+        ao[u] = ((uint32_t)qrow * (uint32_t)D + (uint32_t)(h * DH + col)) * 4;
+        oo[u] = ((uint32_t)qrow * (uint32_t)ld_dq + (uint32_t)col) * 2;
         v[u] = __builtin_amdgcn_raw_buffer_load_b128(dqrs, ao[u], 0, 0);
       }
 #pragma unroll

@@ -9,8 +9,6 @@
 
 #include "gemm_params.h"
 
-namespace pybind11 { class module_; }
-namespace pvr_comm { void register_comm(pybind11::module_& m); }
 
 namespace pvr {
 
@@ -120,6 +118,32 @@ int64_t ld_of(const torch::Tensor& t, const char* name) {
   return t.size(0) == 1 ? t.size(1) : t.stride(0);
 }
 
+// Split-K tail of the one-tile-per-workgroup GEMMs (GemmParams::tail_*): per (device, stream) a
+// slab workspace of CUs x 256x256 fp32 partial tiles and CUs arrival counters (zeroed once; each
+// launch leaves them zero). GEMMs on one stream are serialised, so they share the buffers.
+bool g_gemm_tail = true;
+struct TailBufs {
+  torch::Tensor ws, cnt;
+};
+void attach_tail(pvr::GemmParams& p, const torch::Tensor& like) {
+  if (!g_gemm_tail) return;
+  static std::map<std::pair<int, hipStream_t>, TailBufs> bufs;
+  const auto key = std::make_pair((int)like.get_device(), stream());
+  auto it = bufs.find(key);
+  if (it == bufs.end()) {
+    const int64_t cus = num_cus();
+    TailBufs b;
+    b.ws = torch::empty({cus * 65536}, like.options().dtype(torch::kFloat32));
+    b.cnt = torch::zeros({cus}, like.options().dtype(torch::kInt32));
+    it = bufs.emplace(key, b).first;
+  }
+  p.tail_ws = it->second.ws.data_ptr<float>();
+  p.tail_cnt = reinterpret_cast<unsigned*>(it->second.cnt.data_ptr<int32_t>());
+  p.tail_ws_elems = it->second.ws.numel();
+  p.tail_cnt_elems = (int)it->second.cnt.numel();
+}
+void set_gemm_tail(bool on) { g_gemm_tail = on; }
+
 // C = A . B^T with the given operand layouts; see csrc/gemm.hip for the epilogue contract.
 void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torch::Tensor C, int64_t M, int64_t N, int64_t K,
           int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> addend,
@@ -177,6 +201,7 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   p.k_split_len = k_split > 0 ? (int)(((k_split + 63) / 64) * 64) : (int)(((K + 63) / 64) * 64);
   p.epi = (int)epi;
   p.tile_cfg = (int)tile_cfg;
+  if (epi <= 2 && p.k_split_len >= K) attach_tail(p, C);
   check(pvr_gemm(&p, stream()), "gemm");
 }
 
@@ -584,6 +609,7 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
   p.k_split_len = (int)K;
   p.epi = (int)epi;
   p.tile_cfg = 12;
+  if (epi <= 2) attach_tail(p, C);
   check(pvr_gemm(&p, stream()), "gemm_fp8");
 }
 
@@ -855,9 +881,9 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  pvr_comm::register_comm(m);
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
-  m.def("gemm", &gemm, py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
+  m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
+  m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),
         py::arg("addend_period"), py::arg("aux"), py::arg("row_group"), py::arg("row_stride_group"),
         py::arg("row_offset"), py::arg("seed"), py::arg("seed_offset"), py::arg("drop_p"), py::arg("k_split"),

@@ -352,26 +352,6 @@ extern "C" hipError_t pvr_splitk_reduce(const float* ws, int S, int64_t stride, 
   return hipGetLastError();
 }
 
-// dst[i] = scale * (dst[i] + sum_{j < k} src[j * stride + i]): the local reduction of the native
-// communicator's mesh reduce-scatter (csrc/comm_core.h), k = world - 1 received chunks
-__global__ void __launch_bounds__(256) sum_chunks_kernel(float* __restrict__ dst, const float* __restrict__ src, int k, int64_t n,
-                                                         int64_t stride, float scale) {
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    float a = dst[i];
-    for (int j = 0; j < k; ++j) a += src[(int64_t)j * stride + i];
-    dst[i] = a * scale;
-  }
-}
-
-extern "C" hipError_t pvr_sum_chunks(float* dst, const float* src, int k, int64_t n, int64_t stride, float scale, hipStream_t s) {
-  using namespace pvr;
-  if (n <= 0) return hipSuccess;
-  int64_t blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(sum_chunks_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, k, n, stride, scale);
-  return hipGetLastError();
-}
-
 // meta: int64 [nmat][5] = {src_off, dst_off, rows, cols, tile_prefix}; total_tiles = sum of tiles
 extern "C" hipError_t pvr_transpose_batched(const uint16_t* src, uint16_t* dst, const int64_t* meta, int nmat, int total_tiles,
                                             hipStream_t s) {

@@ -398,10 +398,8 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ===================================================================================== multistage
-// 4-stage LDS ring, BK = 32, counted vmcnt (LDS-DMA for up to STAGES-2 future stages stays in flight
-// across the barrier), one raw s_barrier per stage, 8 waves. 256-row tiles halve the L2->LDS bytes
-// per MFMA against 128x128 (which needs ~64 B/clk/CU at peak MFMA rate, the whole L2 bandwidth).
+// ===================================================================================== BK = 32 staging
+// (the 4-stage ring of the v3 kernel below)
 constexpr int BK32 = 32;
 // LDS-DMA wave-instructions per wave per BK=32 stage of a BM x BN tile (1 KiB each)
 #define LPS_OF(BM, BN, NW) (((BM) * BK32 * 2 / 1024 + (BN) * BK32 * 2 / 1024) / (NW))
@@ -450,110 +448,6 @@ PVR_DEV v8s frag32(const char* lds, int r0, int lane) {
   }
 }
 
-
-template <int BM, int BN, int WM, int WN, int STAGES, bool AK, bool BKC, bool SWAP, int EPI>
-__global__ void __launch_bounds__(WM* WN * 64) gemm_ms_kernel(GemmParams p) {
-  constexpr int NW = WM * WN;
-  constexpr int A_BYTES = BM * BK32 * 2, B_BYTES = BN * BK32 * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int LPS = (A_BYTES / 1024 + B_BYTES / 1024) / NW;  // LDS-DMA instructions per wave per stage
-  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-
-  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = t / ntn, tn = t % ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * p.k_split_len;
-  const int kend = min(p.K, kbeg + p.k_split_len);
-  const int nk = (kend - kbeg + BK32 - 1) / BK32;
-
-  const uint16_t* abase;
-  uint32_t abytes;
-  if constexpr (AK) {
-    abase = p.A + (int64_t)m0 * p.lda + kbeg;
-    abytes = rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)m0 * p.lda + kbeg);
-  } else {
-    abase = p.A + (int64_t)kbeg * p.lda + m0;
-    abytes = rsrc_bytes((int64_t)(p.K - 1) * p.lda + p.M, (int64_t)kbeg * p.lda + m0);
-  }
-  const uint16_t* bbase;
-  uint32_t bbytes;
-  if constexpr (BKC) {
-    bbase = p.B + (int64_t)n0 * p.ldb + kbeg;
-    bbytes = rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)n0 * p.ldb + kbeg);
-  } else {
-    bbase = p.B + (int64_t)kbeg * p.ldb + n0;
-    bbytes = rsrc_bytes((int64_t)(p.K - 1) * p.ldb + p.N, (int64_t)kbeg * p.ldb + n0);
-  }
-  const __amdgpu_buffer_rsrc_t ars = make_rsrc(abase, abytes);
-  const __amdgpu_buffer_rsrc_t brs = make_rsrc(bbase, bbytes);
-
-  v4f acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: stages 0 .. STAGES-2
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s) {
-    if (s < nk) {
-      char* dst = smem + s * STAGE_BYTES;
-      stage32<BM, AK, NW>(ars, dst, p.lda, s * BK32, wave, lane);
-      stage32<BN, BKC, NW>(brs, dst + A_BYTES, p.ldb, s * BK32, wave, lane);
-    }
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + STAGES - 2 < nk)
-      wait_barrier<(STAGES - 2) * LPS>();  // steady state: STAGES-2 future stages stay in flight
-    else
-      wait_barrier<0>();
-    const int ks = kt + STAGES - 1;
-    if (ks < nk) {
-      char* dst = smem + (ks % STAGES) * STAGE_BYTES;
-      stage32<BM, AK, NW>(ars, dst, p.lda, ks * BK32, wave, lane);
-      stage32<BN, BKC, NW>(brs, dst + A_BYTES, p.ldb, ks * BK32, wave, lane);
-    }
-    const char* cur = smem + (kt % STAGES) * STAGE_BYTES;
-    v8s af[FM], bf[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = frag32<BM, AK>(cur, wm * WTM + 16 * i, lane);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = frag32<BN, BKC>(cur + A_BYTES, wn * WTN + 16 * j, lane);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if constexpr (SWAP)
-          acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
-        else
-          acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
-      }
-    __builtin_amdgcn_s_setprio(0);
-  }
-  epilogue<FM, FN, SWAP, EPI>(p, acc, m0 + wm * WTM, n0 + wn * WTN, lane);
-}
-
-template <int BM, int BN, int WM, int WN, int STAGES, bool AK, bool BKC, bool SWAP, int EPI>
-hipError_t launch_ms(const GemmParams& p, hipStream_t s) {
-  constexpr int SMEM = STAGES * (BM + BN) * BK32 * 2;
-  auto kern = gemm_ms_kernel<BM, BN, WM, WN, STAGES, AK, BKC, SWAP, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-  const int nsplit = (p.K + p.k_split_len - 1) / p.k_split_len;
-  hipLaunchKernelGGL(kern, dim3(ntm * ntn, 1, nsplit), dim3(WM * WN * 64), SMEM, s, p);
-  return hipGetLastError();
-}
 
 // ===================================================================================== v3
 // 4 waves (2x2) per workgroup, wave tile (BM/2)x(BN/2) (128x128 at 256x256: 256 fp32 accumulators
@@ -1391,6 +1285,70 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   }
 }
 
+// Split-tail hand-off (see GemmParams::tail_*): this K-part of tail tile `tloc` publishes its fp32
+// partial tile, and the part that arrives last adds every other part's partial into `acc` and
+// returns true (it then runs the epilogue); the others return false. Partials are stored in
+// register order (accumulator (i, j) of thread t at float4 (i*4 + j)*512 + t of the part's 256 KiB
+// slab): every wave instruction moves one contiguous KiB and each thread re-reads only its own
+// values. Publication follows the agent-scope recipe: plain stores, every wave's vmcnt(0), barrier,
+// release fence, arrival counter; the last arriver acquires before it reads the slabs.
+// acc <- the sum of the S parts' slabs in the fixed order 0..S-1 (own slab included, re-read from
+// L2): the result does not depend on which part arrived last, and the accumulators are dead while
+// the loads are in flight (no register selects, no spills).
+template <int S>
+PVR_DEV void tail_sum(v4f (&acc)[8][4], __amdgpu_buffer_rsrc_t rs, int tid) {
+  constexpr int SLAB_BYTES = 256 * 256 * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t off = (uint32_t)(((i * 4 + j) * 512 + tid) * 16);
+      v4f s = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+#pragma unroll
+      for (int q = 1; q < S; ++q) s += __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, off, q * SLAB_BYTES, 0));
+      acc[i][j] = s;
+    }
+}
+
+PVR_DEV bool tail_gather(const GemmParams& p, v4f (&acc)[8][4], char* smem, int tloc, int tpart) {
+  constexpr int SLAB = 256 * 256;  // floats per part
+  const int tid = threadIdx.x;
+  const int S = p.tail_split;
+  float* base = p.tail_ws + (int64_t)tloc * S * SLAB;
+  v4f* mine = (v4f*)(base + (int64_t)tpart * SLAB);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mine[(i * 4 + j) * 512 + tid] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* flag = (unsigned*)smem;  // K-tile buffers are idle: every DMA and read has retired
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the release's own wait (see the guide)
+    const unsigned old = __hip_atomic_fetch_add(p.tail_cnt + tloc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = old == (unsigned)(S - 1) ? 1u : 0u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every part of this tile has arrived: re-arm the counter for the next launch
+      __hip_atomic_store(p.tail_cnt + tloc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *(volatile unsigned*)flag = last;
+  }
+  __syncthreads();
+  const unsigned last = *(volatile unsigned*)flag;
+  if (!last) return false;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, (uint32_t)S * SLAB * 4);
+  switch (S) {
+    case 2: tail_sum<2>(acc, rs, tid); break;
+    case 3: tail_sum<3>(acc, rs, tid); break;
+    default: tail_sum<4>(acc, rs, tid); break;
+  }
+  __syncthreads();  // the flag word is LDS the epilogue may reuse
+  return true;
+}
+
 template <bool AK, bool BKC, bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
 __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1399,14 +1357,31 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   const int wm = wave >> 2, wn = wave & 3;  // group = wm
 
   const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
-  PVR_ASSERT(blockDim.x == 512 && (int)blockIdx.x < ntm * ntn);
-  PVR_ASSERT(ES == 2 || (p.K % 128 == 0 && p.scale_a && p.scale_b));
-  const int tt = xcd_remap(blockIdx.x, ntm * ntn);
-  const int m0 = (tt / ntn) * 256, n0 = (tt % ntn) * 256;
-  // split-K (wgrad over tokens): this workgroup reduces k in [kbeg, kend)
-  const int kbeg = blockIdx.z * p.k_split_len;
-  const int kend = min(p.K, kbeg + p.k_split_len);
   constexpr int BKE = 128 / ES;  // K-tile depth in elements (64 bf16 / 128 fp8)
+  PVR_ASSERT(blockDim.x == 512);
+  PVR_ASSERT(ES == 2 || (p.K % 128 == 0 && p.scale_a && p.scale_b));
+  // Tile and K range of this workgroup. Plain grid: one whole tile per workgroup (split-K over
+  // blockIdx.z for the weight gradients). Split tail (tail_split > 1): workgroups < tail_from own
+  // one whole tile each; the rest are K-parts of the tail tiles, the parts of one tile on
+  // consecutive remapped ids (one XCD, so the last part reads the others' partials from its L2).
+  int tt, kbeg, kend, tloc = 0, tpart = -1;
+  if (p.tail_split > 1 && (int)blockIdx.x >= p.tail_from) {
+    const int units = (ntm * ntn - p.tail_from) * p.tail_split;
+    PVR_ASSERT((int)blockIdx.x - p.tail_from < units);
+    const int u = xcd_remap((int)blockIdx.x - p.tail_from, units);
+    tloc = u / p.tail_split;
+    tpart = u % p.tail_split;
+    tt = p.tail_from + tloc;
+    const int nkt = p.K / BKE;  // k-contiguous operands: K % BKE == 0 (host check)
+    kbeg = (tpart * nkt / p.tail_split) * BKE;
+    kend = ((tpart + 1) * nkt / p.tail_split) * BKE;
+  } else {
+    PVR_ASSERT((int)blockIdx.x < (p.tail_split > 1 ? p.tail_from : ntm * ntn));
+    tt = xcd_remap(blockIdx.x, p.tail_split > 1 ? p.tail_from : ntm * ntn);
+    kbeg = blockIdx.z * p.k_split_len;
+    kend = min(p.K, kbeg + p.k_split_len);
+  }
+  const int m0 = (tt / ntn) * 256, n0 = (tt % ntn) * 256;
   const int nk = (kend - kbeg + BKE - 1) / BKE;  // k-contiguous operands: K % BKE == 0 (host check)
   PVR_ASSERT(!(AK || BKC) || (p.K % BKE == 0 && kbeg % BKE == 0));
 
@@ -1479,6 +1454,9 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
   stamp(p, 2);
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU) {
+    if (tpart >= 0 && !tail_gather(p, acc, smem, tloc, tpart)) return;  // another part finishes the tile
+  }
   if constexpr (SWAP && (EPI == EPI_F32_ATOMIC || EPI == EPI_F32_STORE)) {
     if ((p.N & 3) == 0 && !p.row_group)
       epilogue_staged<EPI, 128, false>(p, acc, smem, m0, n0, wm, wn, lane);
@@ -1505,6 +1483,42 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   stamp(p, 3);
 }
 
+// compute units of the current device (cached per device)
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    hipDeviceProp_t prop;
+    const int n = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 0;
+    cache[dev] = n > 0 ? n : 256;
+  }
+  return cache[dev];
+}
+
+// Split of the last, partial dispatch round into K-parts (GemmParams::tail_*). A 256x256 tile owns a
+// CU for its whole K loop, so with R full rounds and r < CUs tiles left over the last round runs r
+// tiles on CUs / r times fewer CUs than it could: e.g. the N = 768 GEMMs of ViT-B/16 at batch 256
+// (591 tiles) spend 3 tile-times on 2.31 rounds of work. Splitting each leftover tile's K loop into
+// S parts puts S*r <= CUs workgroups on the last round, at the price of an fp32 partial-tile
+// exchange (256 KiB per part). Parts keep >= 3 K-tiles each (prologue amortisation) and S <= 4.
+void plan_tail(GemmParams& q, int ntiles, int bke) {
+  q.tail_from = 0;
+  q.tail_split = 0;
+  if (!q.tail_ws || !q.tail_cnt) return;
+  const int cus = device_cus();
+  const int rem = ntiles % cus;
+  if (ntiles < cus || rem == 0) return;
+  int S = cus / rem;
+  S = S < 4 ? S : 4;
+  const int nkt = q.K / bke;
+  while (S > 1 && nkt / S < 3) --S;
+  if (S < 2) return;
+  if ((int64_t)rem * S * 65536 > q.tail_ws_elems || rem > q.tail_cnt_elems) return;
+  q.tail_from = ntiles - rem;
+  q.tail_split = S;
+}
+
 template <bool AK, bool BKC, bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
 hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
   constexpr int SMEM = 2 * PP_BUF;
@@ -1517,7 +1531,16 @@ hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
   }
   const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256;
   const int nsplit = (p.K + p.k_split_len - 1) / p.k_split_len;
-  hipLaunchKernelGGL(kern, dim3(ntm * ntn, 1, nsplit), dim3(512), SMEM, s, p);
+  GemmParams q = p;
+  q.tail_from = q.tail_split = 0;
+  int grid = ntm * ntn;
+  if constexpr (AK && BKC && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
+    if (nsplit == 1) {
+      plan_tail(q, ntm * ntn, 128 / ES);
+      if (q.tail_split > 1) grid = q.tail_from + (ntm * ntn - q.tail_from) * q.tail_split;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(grid, 1, nsplit), dim3(512), SMEM, s, q);
   return hipGetLastError();
 }
 
@@ -1716,38 +1739,18 @@ hipError_t launch_ppp(const GemmParams& p, hipStream_t s) {
   const bool direct = !p.epi_staged && direct_ok(p);
   auto kern = direct ? kd : ks;
   const int ntiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  int cus = 256;
-  {
-    static int n_cu = 0;
-    if (!n_cu) {
-      int dev = 0;
-      hipDeviceProp_t prop;
-      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) n_cu = prop.multiProcessorCount;
-      if (n_cu <= 0) n_cu = 256;
-    }
-    cus = n_cu;
-  }
+  const int cus = device_cus();
   const int grid = ntiles < cus ? ntiles : cus;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, s, p);
   return hipGetLastError();
 }
 
+// Tile configs (ops/gemm.py `_tile`): 0 = 128x128 (small GEMMs), 6 = 256x256 BK-32 ring (K % 64 != 0),
+// 12 = 256x256 8-wave ping-pong (one tile per workgroup, split-K tail), 13 = its persistent form.
 template <bool AK, bool BKC, bool SWAP, int EPI>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   switch (p.tile_cfg) {
-    case 1: return launch_cfg<256, 128, 4, 2, AK, BKC, SWAP, EPI>(p, s);
-    case 2: return launch_cfg<128, 256, 2, 4, AK, BKC, SWAP, EPI>(p, s);
-    case 3: return launch_ms<256, 256, 2, 4, 4, AK, BKC, SWAP, EPI>(p, s);
-    case 4: return launch_ms<256, 128, 4, 2, 4, AK, BKC, SWAP, EPI>(p, s);
-    case 5: return launch_ms<128, 256, 2, 4, 4, AK, BKC, SWAP, EPI>(p, s);
     case 6: return launch_v3<256, 256, 2, 4, 4, 2, AK, BKC, SWAP, EPI>(p, s);
-    case 7: return launch_v3<256, 128, 2, 2, 4, 1, AK, BKC, SWAP, EPI>(p, s);
-    case 8: return launch_v3<256, 256, 2, 2, 4, 1, AK, BKC, SWAP, EPI>(p, s);
-    // 4-wave tiles with a 3-deep ring (72 KB LDS): two workgroups per CU, so one's epilogue overlaps
-    // the other's main loop, and half-size tiles cut the last-round quantisation at N = 768
-    case 9: return launch_v3<256, 128, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
-    case 10: return launch_v3<128, 256, 2, 2, 3, 2, AK, BKC, SWAP, EPI>(p, s);
-    case 11: return launch_v3<256, 256, 2, 4, 3, 2, AK, BKC, SWAP, EPI>(p, s);
     case 13:  // persistent ping-pong (k-contiguous bf16, bf16-output epilogues, no split-K)
       if constexpr (AK && BKC && SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
         if (p.K % PP_BK == 0 && p.K >= 2 * PP_BK && p.k_split_len >= p.K && !p.addend && !p.row_group && (p.N & 3) == 0)

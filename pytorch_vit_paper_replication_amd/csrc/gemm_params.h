@@ -35,6 +35,14 @@ struct GemmParams {
   // c_skip = 1: the bf16 output is not stored (register-direct epilogue: 0-byte C resource, every
   // store dropped by the range check) - only its fp8 copy / aux / column sums are consumed
   int c_skip;
+  // split-K tail of the one-tile-per-workgroup ping-pong (bf16-output epilogues): the output tiles of
+  // the last, partial dispatch round (tiles >= tail_from) are computed as tail_split K-parts each;
+  // every part stores its fp32 partial tile into tail_ws and the last part to arrive (per-tile
+  // arrival counter in tail_cnt, zero between launches) sums them and runs the epilogue. tail_ws /
+  // tail_cnt are per-stream buffers from the host (null: no tail split); tail_from / tail_split are
+  // chosen by the launcher from the tile and CU counts.
+  float* tail_ws; unsigned* tail_cnt; int64_t tail_ws_elems; int tail_cnt_elems;
+  int tail_from, tail_split;
 };
 
 }  // namespace pvr

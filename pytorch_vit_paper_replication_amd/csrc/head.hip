@@ -138,7 +138,9 @@ __global__ void __launch_bounds__(256) head_bwd_gemm_kernel(const float* __restr
   const int r = lane & 15, kq = (lane >> 4) * 4;
   const int ntd = D / 16;
   if (tile < nA) {
-    const int c0 = (tile / ntd) * 16, d0 = (tile % ntd) * 16;
+    // dW tiles (c-block, d-block); with dW null (frozen weight, trainable bias) only the d-block-0
+    // tile of each c-block runs, for db
+    const int c0 = dW ? (tile / ntd) * 16 : tile * 16, d0 = dW ? (tile % ntd) * 16 : 0;
     const int ca = min(c0 + r, C - 1);  // A[m = c][k = b] = dl[b][c]; B[k = b][n = d] = xc[b][d]
     const float gd = gamma[d0 + r], bd = beta[d0 + r];
     v4f acc = {0.f, 0.f, 0.f, 0.f};
@@ -160,10 +162,12 @@ __global__ void __launch_bounds__(256) head_bwd_gemm_kernel(const float* __restr
     }
     if (!splitk_reduce(acc, bs, wave, lane)) return;
     const int d = d0 + r;
+    if (dW) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = c0 + (lane >> 4) * 4 + q;
-      if (c < C) dW[(int64_t)c * D + d] += acc[q];
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + (lane >> 4) * 4 + q;
+        if (c < C) dW[(int64_t)c * D + d] += acc[q];
+      }
     }
     if (d0 == 0 && db) {
       // bs: this lane's share (b = kq + j mod 16) of sum_b dl[b][c0 + r]; add the 4 lane groups
@@ -323,7 +327,9 @@ extern "C" hipError_t pvr_head_bwd(const float* dl, const float* xhat, const flo
   if (B <= 0) return hipSuccess;
   if (D % 16 != 0 || C <= 0) return hipErrorInvalidValue;
   const int ntd = D / 16;
-  const int nA = dW ? ((C + 15) / 16) * ntd : 0;
+  // dW tiles; without dW but with db (classifier weight frozen, bias trainable): one tile per
+  // 16 classes for the bias gradient alone
+  const int nA = dW ? ((C + 15) / 16) * ntd : db ? (C + 15) / 16 : 0;
   const int nB = ((B + 15) / 16) * ntd;
   hipLaunchKernelGGL(head_bwd_gemm_kernel, dim3(nA + nB), dim3(256), 0, s, dl, xhat, gamma, beta, W, B, C, D, nA, nB, dW, db,
                      dy, dgamma, dbeta);

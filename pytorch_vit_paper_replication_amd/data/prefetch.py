@@ -7,8 +7,11 @@ The reference moves every batch with a blocking ``X.to(device)`` at the top of t
 * the destination tensors are allocated on the consumer (compute) stream, so the caching allocator
   ties them to that stream and no ``record_stream`` is needed (cross-stream ``record_stream`` defers
   frees and was measured to stall the allocator at large batch, see runtime/param_store.py);
-* the copy itself runs on a dedicated low-priority HIP stream (a separate SDMA-backed queue), after
-  an event that orders it behind the allocation;
+* the copy itself runs on a dedicated HIP stream of the default priority (0, the lowest torch
+  offers; ``bench.py`` runs the step on a priority -1 stream above it), after an event that orders it
+  behind the allocation. A host-to-device copy is executed by a DMA (SDMA) engine, not a compute
+  queue, so it does not take compute-queue slots from the step (the process has
+  ``GPU_MAX_HW_QUEUES`` = 4 hardware compute queues, which the compute streams share);
 * the consumer stream waits on the copy's event right before the batch is handed out — no host
   synchronisation anywhere.
 

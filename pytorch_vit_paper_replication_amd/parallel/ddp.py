@@ -16,23 +16,14 @@ Design, MI355X-first rather than a copy of torch 
     autograd end-of-backward callback flushes the rest and joins the stream before the optimizer
     (the global-norm clip therefore sees averaged gradients, C3).
 
-Transport (``comm``): ``"torch"`` (the default, ``"auto"``) all-reduces each bucket with
-``torch.distributed`` (ProcessGroupNCCL = RCCL on ROCm, its own HIP stream, ``ReduceOp.AVG``), joined
-into the compute stream by ``work.wait()`` — no host synchronisation. ``"native"`` uses the
-framework's C++ RCCL communicator (``parallel/comm.py`` -> ``csrc/comm.cpp``) on its own stream,
-event-gated the same way; ``"native-mesh"`` runs that communicator's own reduce-scatter + all-gather
-schedule (``csrc/comm_core.h``: grouped point-to-point transfers to every peer at once, fp32). gloo /
-CPU always uses ``torch.distributed``. World-1 A/B at ViT-B/16 b512 (profiles/r3/ddp_transport_world1_b512.log):
-no DDP 8082 / 8075 img/s, torch 8053, torch with the bf16 wire 8034 — RCCL's one-rank kernel
-(``oneRankReduce``, ~0.2 ms per bucket) hides under the backward. The native transport stays opt-in:
-it is 8 % slower at world 1 (7306-7337 vs torch 7936, no DDP 7990-8002 img/s,
-profiles/r3/ddp_native/transport_ab.log) and the cause is not identified. Ruled out by measurement:
-stream priority (normal, like ProcessGroupNCCL's), HW-queue aliasing (GPU_MAX_HW_QUEUES=8: no
-change), a second RCCL communicator in the process (idle: no effect, scripts/probes/idle_comm_probe.py),
-a second RCCL runtime (it resolves torch's librccl.so), collective placement (the same 11
-``oneRankReduce`` per step, all inside the backward, the optimizer after the last one). The in-step
-traces (profiles/r3/ddp_native/) show the FORWARD kernels 10-100 % slower with no other kernel on
-the GPU, i.e. a device-wide effect, not stream ordering.
+Transport: each bucket is all-reduced with ``torch.distributed`` (ProcessGroupNCCL = RCCL on ROCm,
+its own HIP stream, ``ReduceOp.AVG``), joined into the compute stream by ``work.wait()`` — no host
+synchronisation; gloo / CPU the same way with a SUM + divide. World-1 A/B at ViT-B/16 b512
+(profiles/r3/ddp_transport_world1_b512.log): no DDP 8082 / 8075 img/s, torch 8053, torch with the bf16
+wire 8034 — RCCL's one-rank kernel (``oneRankReduce``, ~0.2 ms per bucket) hides under the backward.
+(A framework-owned C++ RCCL communicator with its own mesh reduce-scatter schedule existed through
+round 3; it was 8 % slower than this transport at world 1 with no identified cause, never used by
+default, and was removed in round 4: ``comm`` accepts "auto" / "torch" only.)
 
 Wire format (``comm_dtype``): fp32 by default. ``torch.bfloat16`` keeps a persistent bf16 mirror of
 the gradient buffer (no per-step allocation): each bucket is cast into its slice, all-reduced in
@@ -50,7 +41,6 @@ from __future__ import annotations
 
 import contextlib
 import time
-import warnings
 from typing import Dict, List, Optional
 
 import torch
@@ -85,32 +75,15 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._hooks = []
         self._avg = dist.get_backend(process_group) == "nccl"
-        self._comm_mode = comm
-        self._native = None          # parallel.comm.NativeCommunicator when the native transport is used
+        if comm not in ("auto", "torch"):
+            raise ValueError(f"DistributedDataParallel: unknown transport {comm!r} (torch.distributed only: 'auto' / 'torch')")
         self._comm_buf: Optional[torch.Tensor] = None  # persistent low-precision gradient mirror
-        # native transport's all-reduce schedule: "rccl" (RCCL's algorithm) or "mesh" (comm="native-mesh":
-        # csrc/comm_core.h grouped point-to-point reduce-scatter + all-gather over every xGMI link)
-        self._algo = "mesh" if comm == "native-mesh" else "rccl"
         # per-bucket all-reduce timing (utils.metrics.StepLogger): (bytes, start, end) per launched
         # bucket, start = bucket ready on the compute stream, end = collective complete (HIP events
         # on GPU, host clock with gloo)
         self.timing = timing
         self._timings: List[tuple] = []
         self._timing_stream: Optional[torch.cuda.Stream] = None
-
-    def _pick_transport(self, device):
-        mode = self._comm_mode
-        if mode not in ("native", "native-mesh") or device.type != "cuda" or not self._avg:
-            return None
-        from .comm import NativeCommunicator
-
-        try:
-            return NativeCommunicator.create(device, self.process_group)
-        except Exception as e:  # pragma: no cover - only on GPU boxes
-            if mode.startswith("native"):
-                raise
-            warnings.warn(f"native RCCL communicator unavailable ({e}); using torch.distributed collectives")
-            return None
 
     # ------------------------------------------------------------------ setup
     def _plan(self, params) -> List[List[int]]:
@@ -169,20 +142,12 @@ class DistributedDataParallel(nn.Module):
         if self._store is not None:
             self._store.remove_listener(self._on_ready)
         self._store = store
-        if self._native is None:
-            self._native = self._pick_transport(device)
         if self.broadcast_parameters:
             with torch.no_grad():
-                if self._native is not None:
-                    self._native.wait(self._native.broadcast(store.flat, root=0))
-                    for b in self.module.buffers():
-                        if b.is_cuda and b.is_contiguous():
-                            self._native.wait(self._native.broadcast(b, root=0))
-                else:
-                    src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
-                    dist.broadcast(store.flat, src=src, group=self.process_group)
-                    for b in self.module.buffers():
-                        dist.broadcast(b, src=src, group=self.process_group)
+                src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+                dist.broadcast(store.flat, src=src, group=self.process_group)
+                for b in self.module.buffers():
+                    dist.broadcast(b, src=src, group=self.process_group)
             store.refresh_shadow(force=True)
         if self.comm_dtype is not None and self.comm_dtype != store.grad_flat.dtype:
             self._comm_buf = torch.empty(store.numel, dtype=self.comm_dtype, device=store.grad_flat.device)
@@ -195,8 +160,6 @@ class DistributedDataParallel(nn.Module):
             self._buckets.append((lo, hi, idxs))
             for i in idxs:
                 self._bucket_of[id(store.params[i])] = bi
-        if self._native is not None and self._algo == "mesh" and self._buckets:
-            self._native.reserve_mesh(max(hi - lo for lo, hi, _ in self._buckets))
         store.add_listener(self._on_ready)
         for p in store.params:
             if p.requires_grad:
@@ -262,11 +225,8 @@ class DistributedDataParallel(nn.Module):
             tmp = self._comm_buf[lo:hi]
             tmp.copy_(buf)
         wire = buf if tmp is None else tmp
-        if self._native is not None:
-            w = self._native.all_reduce(wire, algo=self._algo if tmp is None else "rccl")
-        else:
-            op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
-            w = dist.all_reduce(wire, op=op, group=self.process_group, async_op=True)
+        op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+        w = dist.all_reduce(wire, op=op, group=self.process_group, async_op=True)
         self._works.append((w, buf, tmp))
         if t0 is not None:
             self._timing_end(w, t0, wire.numel() * wire.element_size())
@@ -288,10 +248,7 @@ class DistributedDataParallel(nn.Module):
         ts = self._timing_stream
         e = torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(ts):  # ts waits for the collective (no host sync), then stamps it
-            if self._native is not None:
-                self._native.wait(w)
-            else:
-                w.wait()
+            w.wait()
             e.record(ts)
         self._timings.append((nbytes, t0, e))
 
@@ -305,13 +262,6 @@ class DistributedDataParallel(nn.Module):
         while self._next_launch < len(self._buckets):
             self._launch(self._next_launch)
             self._next_launch += 1
-        if self._native is not None:
-            for h, buf, tmp in self._works:
-                self._native.wait(h)  # compute stream waits on the comm stream: no host sync
-                if tmp is not None:
-                    buf.copy_(tmp)
-            self._works = []
-            return
         for w, buf, tmp in self._works:
             w.wait()
             for t in self._timings:  # gloo: completion stamped on the host clock when its wait returns
@@ -325,7 +275,7 @@ class DistributedDataParallel(nn.Module):
 
     @property
     def transport(self) -> str:
-        return "native-rccl" if self._native is not None else f"torch-{dist.get_backend(self.process_group)}"
+        return f"torch-{dist.get_backend(self.process_group)}"
 
     # convenience passthroughs
     def state_dict(self, *a, **k):

@@ -119,9 +119,11 @@ class StepLogger:
     def flush(self) -> None:
         if not self.enabled or not self._pending:
             return
-        last = self._pending[-1]["t1"]
-        if not isinstance(last, float):
-            last.synchronize()
+        if self.cuda:
+            # every pending event must have completed before elapsed_time: the DDP per-bucket end
+            # events live on the all-reduce timing stream, which the compute stream's last event does
+            # not order ("device not ready" otherwise); one device sync per flush
+            torch.cuda.synchronize()
         with open(self.path, "a") as f:
             for r in self._pending:
                 ms = self._elapsed_ms(r["t0"], r["t1"])

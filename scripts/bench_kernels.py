@@ -37,11 +37,11 @@ def timeit(fn, iters=20, warmup=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--tiles", default="0,1,2")
+    ap.add_argument("--tiles", default="0,12")
     ap.add_argument("--only", default="gemm,attn,ln")
     ap.add_argument("--attn-shape", default="197,12,64", help="N,H,dh of the attention cases (batch: --batch)")
-    ap.add_argument("--epi-tiles", default="12,13,15", help="tile configs of the per-epilogue cases (--only epi)")
-    ap.add_argument("--gelu-tiles", default="9,10,11,6,13,15", help="tile configs of the fc1 GELU case (--only epi)")
+    ap.add_argument("--epi-tiles", default="12,13", help="tile configs of the per-epilogue cases (--only epi)")
+    ap.add_argument("--gelu-tiles", default="6,12,13", help="tile configs of the fc1 GELU case (--only epi)")
     ap.add_argument("--rounds", type=int, default=1, help="repeat the epilogue cases (interleaved A/B)")
     a = ap.parse_args()
     dev = "cuda"

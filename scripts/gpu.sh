@@ -76,7 +76,6 @@ case "$MODE" in
     TAILN=1 run 240 "$TAG/none.log" $B
     TAILN=1 run 240 "$TAG/torch.log" $B --force-ddp --metrics-jsonl "gpurun_out/$TAG/steps_torch.jsonl"
     TAILN=1 run 240 "$TAG/torch_bf16.log" $B --force-ddp --comm-dtype bf16
-    TAILN=1 run 240 "$TAG/native.log" $B --force-ddp --comm native
     TAILN=1 run 240 "$TAG/none2.log" $B ;;
   conv)
     TAILN=2 run 1000 conv.log python -u scripts/convergence_check.py "$@" ;;

@@ -176,6 +176,99 @@ def check_gemm_patch_embed_epilogue(B=20, n_p=196, D=768, K=768, p=0.1):
             lim(1e-3, 8e-3, cls_or_mask_bad=0, rate_dev=rate_limit(p, B * n_p * D)))
 
 
+class gemm_tail:
+    """Context: split-K tail of the last dispatch round on / off (ext.set_gemm_tail)."""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    def __enter__(self):
+        _ext.ext().set_gemm_tail(self.on)
+
+    def __exit__(self, *exc):
+        _ext.ext().set_gemm_tail(True)
+
+
+def check_gemm_tail_split(M=50432, N=768, K=768, kind="resid_drop", p=0.1):
+    """Split-K tail (the leftover tiles of the last dispatch round as K-parts, fp32 partial tiles
+    handed to the last part through an agent-scope release / acquire) on the ping-pong kernel vs the
+    same GEMM with one workgroup per tile: same dropout masks, values within fp32 reassociation
+    (bf16 1-ulp flips), bitwise identical across two runs (fixed summation order), and vs fp32.
+    kind: resid_drop (fc2 forward), gelu (fc1 forward + aux), dgelu (dGELU dgrad + column sum),
+    patch (position-embedding addend, row remap, dropout)."""
+    seed = torch.tensor([4242], dtype=torch.int64, device=DEV)
+    drop = (seed, 9 << 32, p)
+    if kind == "dgelu":
+        dy, w, g = bf(rnd(M, K)), bf(rnd(K, N, scale=0.05)), bf(rnd(M, N))
+        wt = w.t().contiguous()
+
+        def run():
+            cs = torch.zeros(N, device=DEV)
+            out = G.linear_dgrad(dy, w, dgelu_aux=g, wt=wt, colsum=cs)
+            return out, cs
+        ref = (dy.float() @ w.float()) * g.float()
+        refs = (ref, ref.sum(0))
+    else:
+        x, w, b = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05)), rnd(N)
+        if kind == "gelu":
+            def run():
+                u = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+                h = G.linear_fwd(x, w, b, gelu_aux=u, drop=drop)
+                return h, u
+        elif kind == "patch":
+            n_p = 196
+            ntok = n_p + 1
+            Bimg = M // n_p
+            x = x[:Bimg * n_p]
+            pos = rnd(ntok, N)
+
+            def run():
+                out = torch.full((Bimg * ntok, N), 7.0, dtype=torch.bfloat16, device=DEV)
+                G.linear_fwd(x, w, b, addend=pos, addend_period=ntok, row_remap=(n_p, ntok, 1), drop=drop, out=out)
+                return (out,)
+        else:
+            r = bf(rnd(M, N))
+
+            def run():
+                return (G.linear_fwd(x, w, b, resid=r, drop=drop),)
+        refs = None
+    with tile(12):
+        with gemm_tail(False):
+            base = run()
+        a = run()
+        c = run()
+    m = worst(*zip(a, base))
+    m["nondeterministic"] = float(not all(torch.equal(u, v) for u, v in zip(a, c)))
+    m["mask_differs"] = float(not all(torch.equal(u == 0, v == 0) for u, v in zip(a[:1], base[:1]))) if kind != "dgelu" else 0.0
+    if refs is not None:
+        l2, mx = errs(a[0], refs[0])
+        l2c, mxc = errs(a[1], refs[1])
+        m.update(ref_l2=l2, ref_max=mx, colsum_l2=l2c)
+        lims = lim(1e-3, 8e-3, nondeterministic=0, mask_differs=0, ref_l2=3.5e-3, ref_max=7e-3, colsum_l2=1.5e-6)
+    else:
+        lims = lim(1e-3, 8e-3, nondeterministic=0, mask_differs=0)
+    tiles = math.ceil(M / 256) * math.ceil(N / 256)
+    return (f"gemm split-K tail {kind} M{M} N{N} K{K} ({tiles} tiles) vs one workgroup per tile", m, lims)
+
+
+def check_gemm_tail_split_fp8(M=65792, N=1280, K=1280):
+    """The split-K tail on the fp8 (e4m3) forward GEMM (ViT-H/14 shape: 1285 tiles = 5 rounds + 5)."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    x, w, b, r = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05)), rnd(N), bf(rnd(M, N))
+    xq, xs, _ = _fp8_operand(x)
+    wq, ws, _ = _fp8_operand(w)
+
+    def run():
+        return F8.linear_fwd_fp8(xq, xs, wq, ws, b, resid=r)
+    with gemm_tail(False):
+        base = run()
+    a, c = run(), run()
+    m = worst((a, base))
+    m["nondeterministic"] = float(not torch.equal(a, c))
+    return (f"gemm_fp8 split-K tail M{M} N{N} K{K} vs one workgroup per tile", m, lim(1e-3, 8e-3, nondeterministic=0))
+
+
 def check_gemm_dgrad(M, N, K, t=0, transposed=False):
     dy, w = bf(rnd(M, N)), bf(rnd(N, K, scale=0.05))
     with tile(t):
@@ -974,9 +1067,10 @@ def check_xent(B, C):
     return (f"xent B{B} C{C}", m, lim(2e-7, 2e-7, acc_flags_bad=0))
 
 
-def check_head(B=37, N=5, D=192, C=1000):
+def check_head(B=37, N=5, D=192, C=1000, frozen_w=False):
     """Classifier head kernels (final LayerNorm of the CLS rows + fp32 Linear, csrc/head.hip) vs
-    PyTorch fp32 autograd: logits, dW, db, dgamma, dbeta, d(tokens) (CLS rows; all other rows 0)."""
+    PyTorch fp32 autograd: logits, dW, db, dgamma, dbeta, d(tokens) (CLS rows; all other rows 0).
+    frozen_w: no dW (classifier weight frozen) while the bias still trains: db must be written."""
     ext = _ext.ext()
     tok = bf(rnd(B * N, D))
     gam, bet = 1 + 0.1 * rnd(D), 0.1 * rnd(D)
@@ -988,12 +1082,13 @@ def check_head(B=37, N=5, D=192, C=1000):
     dl = rnd(B, C)
     ref.backward(dl)
     dW, db, dg, dbt = (torch.zeros_like(x) for x in (W, b, gam, bet))
-    dtok = ext.head_bwd(dl.contiguous(), xhat, rstd, gam, bet, W, B, N, dW, db, dg, dbt)
+    dtok = ext.head_bwd(dl.contiguous(), xhat, rstd, gam, bet, W, B, N, None if frozen_w else dW, db, dg, dbt)
     dt = dtok.float().view(B, N, D)
-    m = worst((logits, ref), (dW, Wr.grad), (db, bbr.grad), (dg, gr.grad), (dbt, br.grad))
+    pairs = [(logits, ref), (db, bbr.grad), (dg, gr.grad), (dbt, br.grad)] + ([] if frozen_w else [(dW, Wr.grad)])
+    m = worst(*pairs)
     m["dtok_l2"], m["dtok_max"] = errs(dt[:, 0], t.grad[:, 0])  # bf16 output rows
     m["other_rows_nonzero"] = float(not bool((dt[:, 1:] == 0).all().item()))
-    return (f"head fwd/bwd B{B} N{N} D{D} C{C}", m, lim(1.5e-6, 2e-6, dtok_l2=3.5e-3, dtok_max=5e-3, other_rows_nonzero=0))
+    return (f"head fwd/bwd B{B} N{N} D{D} C{C}{' (weight frozen, bias trained)' if frozen_w else ''}", m, lim(1.5e-6, 2e-6, dtok_l2=3.5e-3, dtok_max=5e-3, other_rows_nonzero=0))
 
 
 def _adam_pair(cfg, freeze=None):
@@ -1196,6 +1291,14 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_gelu_dropout(5000, 3072, 768),
         lambda: check_gemm_dropout(3000, 768, 128, 0.1, 13),
         lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
+        # split-K tail of the last dispatch round (ViT-B/16 b256 shapes: 591 tiles -> 2 rounds + 79
+        # tiles as 3 K-parts; 2364 tiles -> 9 rounds + 60 tiles as 4 K-parts; 588 patch-embed tiles)
+        lambda: check_gemm_tail_split(50432, 768, 768, "resid_drop"),
+        lambda: check_gemm_tail_split(50432, 768, 3072, "resid_drop"),
+        lambda: check_gemm_tail_split(50432, 3072, 768, "gelu"),
+        lambda: check_gemm_tail_split(50432, 3072, 768, "dgelu"),
+        lambda: check_gemm_tail_split(50176, 768, 768, "patch"),
+        check_gemm_tail_split_fp8,
         lambda: check_gemm_fwd(100, 64, 128, 0, True, True),
         lambda: check_gemm_dgelu(394, 768, 3072),
         lambda: check_gemm_dgelu(4096, 768, 3072, True),
@@ -1312,6 +1415,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_xent(3, 3),
         check_head,
         lambda: check_head(256, 197, 768, 1000),
+        lambda: check_head(37, 5, 192, 1000, frozen_w=True),
         lambda: check_head(5, 3, 1280, 10),
         check_adam,
         check_adam_transposed,
