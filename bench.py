@@ -52,11 +52,35 @@ def parse():
                    help="serving throughput instead: eval-mode forward under inference_mode (no backward / optimizer)")
     p.add_argument("--serial-wgrad", action="store_true",
                    help="weight-gradient GEMMs on the main stream (no side stream): clean per-kernel times for profiles")
+    p.add_argument("--side-window", type=int, default=None,
+                   help="A/B: weight-gradient batches whose inputs stay held at once (0 = until the end of backward)")
     p.add_argument("--no-gemm-tail", action="store_true",
                    help="A/B: no split-K tail on the last dispatch round of the one-tile-per-workgroup GEMMs")
     p.add_argument("--main-prio", type=int, default=-1,
                    help="run the step on a stream of this priority: -1 (default) puts the dgrad chain above the weight-gradient side stream; 0 = default stream")
     return p.parse_args()
+
+
+MODEL_NAMES = {"vit_b16": "ViT-B/16", "vit_l16": "ViT-L/16", "vit_h14": "ViT-H/14"}
+
+
+def describe(args, world: int) -> dict:
+    """The run's configuration as reported (and as BASELINE.json names it), from the arguments and the
+    world size alone: no GPU or model needed (tests/test_bench_cli.py checks configs 2-5 with it)."""
+    from pytorch_vit_paper_replication_amd.models.presets import PRESETS
+
+    per_gpu = args.batch or (256 if world == 1 else 512)
+    name = MODEL_NAMES.get(args.model, args.model)
+    patch = int(PRESETS[args.model]["patch_size"]) if args.model in PRESETS else 16
+    if args.infer:
+        metric = f"inference images/sec (whole node) {name} {args.image_size}px {args.dtype}"
+    elif (name, args.image_size, args.dtype) == ("ViT-B/16", 224, "bf16"):
+        metric = "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
+    else:
+        metric = f"images/sec (whole node) {name} {args.image_size}px {args.dtype}"
+    return {"name": name, "metric": metric, "per_gpu_batch": per_gpu, "global_batch": per_gpu * world,
+            "seq_len": (args.image_size // patch) ** 2 + 1, "parallelism": f"dp{world}",
+            "ddp": world > 1 or args.force_ddp}
 
 
 def _relaunch_distributed(n: int) -> int:
@@ -88,10 +112,13 @@ def main():
     from pytorch_vit_paper_replication_amd.ops.fused_vit import backward, cross_entropy
     from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
 
-    if args.serial_wgrad:
+    if args.serial_wgrad or args.side_window is not None:
         from pytorch_vit_paper_replication_amd.runtime import param_store
 
-        param_store.SIDE_WGRAD = False
+        if args.serial_wgrad:
+            param_store.SIDE_WGRAD = False
+        if args.side_window is not None:
+            param_store.SIDE_WINDOW = args.side_window
     rank, world, device = init_distributed()
     if args.no_gemm_tail and args.impl == "fused":
         from pytorch_vit_paper_replication_amd import _ext
@@ -106,7 +133,8 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29531")
         torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=device,
                                              timeout=datetime.timedelta(seconds=600))
-    per_gpu = args.batch or (256 if world == 1 else 512)
+    desc = describe(args, world)
+    per_gpu = desc["per_gpu_batch"]
     torch.manual_seed(1234)
 
     model = vit(args.model, image_size=args.image_size, num_classes=args.num_classes).to(device)
@@ -119,7 +147,7 @@ def main():
     else:
         opt = torch.optim.Adam(groups, lr=1e-3, betas=(0.9, 0.999))
     sched = warmup_linear_decay(opt, max(total_steps, 20), 0.05)
-    use_ddp = world > 1 or args.force_ddp
+    use_ddp = desc["ddp"]
     net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb, comm=args.comm,
                                   comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None,
                                   timing=bool(args.metrics_jsonl)) if use_ddp else model
@@ -228,16 +256,13 @@ def main():
 
         profile_steps(step, steps=2, out_path=args.profile_out)
 
-    global_batch = per_gpu * world
+    global_batch = desc["global_batch"]
     ips = global_batch * args.steps / elapsed
-    name = {"vit_b16": "ViT-B/16", "vit_l16": "ViT-L/16", "vit_h14": "ViT-H/14"}.get(args.model, args.model)
-    seq = (args.image_size // int(model.config["patch_size"])) ** 2 + 1
+    name = desc["name"]
+    seq = desc["seq_len"]
     if rank == 0:
         out = {
-            "metric": (f"inference images/sec (whole node) {name} {args.image_size}px {args.dtype}" if args.infer else
-                       "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
-                       if (name, args.image_size, args.dtype) == ("ViT-B/16", 224, "bf16")
-                       else f"images/sec (whole node) {name} {args.image_size}px {args.dtype}"),
+            "metric": desc["metric"],
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -254,12 +279,13 @@ def main():
             "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
-                       "image_size": args.image_size, "parallelism": f"dp{world}", "impl": args.impl + ("+hipgraph" if args.graph else ""),
+                       "image_size": args.image_size, "parallelism": desc["parallelism"], "impl": args.impl + ("+hipgraph" if args.graph else ""),
                        "grad_transport": (net.transport + f" {args.comm_dtype} wire") if use_ddp else "none",
                        "optimizer": "none (inference: eval forward under inference_mode)" if args.infer else
                        "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
                        "dropout": "off (eval)" if args.infer else "0.1 (mlp, embedding)",
-                       "final_loss": round(final_loss, 4)},
+                       "final_loss": round(final_loss, 4),
+                       "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2)},
         }
         print(json.dumps(out), flush=True)
     if use_ddp:

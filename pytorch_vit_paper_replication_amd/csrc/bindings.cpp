@@ -21,6 +21,7 @@ struct AdamGroup {
 
 extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
+int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
@@ -882,6 +883,8 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
+  m.def("gemm_tail_split", [](int64_t M, int64_t N, int64_t K, int64_t elem_bytes) {
+    return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes); }, "K-parts of the split tail round this GEMM shape gets (0: none)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

@@ -1286,15 +1286,18 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
 }
 
 // Split-tail hand-off (see GemmParams::tail_*): this K-part of tail tile `tloc` publishes its fp32
-// partial tile, and the part that arrives last adds every other part's partial into `acc` and
-// returns true (it then runs the epilogue); the others return false. Partials are stored in
-// register order (accumulator (i, j) of thread t at float4 (i*4 + j)*512 + t of the part's 256 KiB
-// slab): every wave instruction moves one contiguous KiB and each thread re-reads only its own
-// values. Publication follows the agent-scope recipe: plain stores, every wave's vmcnt(0), barrier,
-// release fence, arrival counter; the last arriver acquires before it reads the slabs.
-// acc <- the sum of the S parts' slabs in the fixed order 0..S-1 (own slab included, re-read from
-// L2): the result does not depend on which part arrived last, and the accumulators are dead while
-// the loads are in flight (no register selects, no spills).
+// partial tile, and the part that arrives last adds every part's partial in the fixed order 0..S-1
+// into `acc` and returns true (it then runs the epilogue); the others return false. Partials are
+// stored in register order (accumulator (i, j) of thread t at float4 (i*4 + j)*512 + t of the
+// part's 256 KiB slab): every wave instruction moves one contiguous KiB and each thread re-reads
+// only its own values. Publication is the write-through form of the agent-scope hand-off (one
+// workgroup per CU, hipMalloc'ed buffers, 16-B accesses): every slab byte is stored sc1, every
+// storing wave drains (vmcnt(0)) before the workgroup barrier, one lane then adds to the tile's
+// arrival counter (agent scope), and the last arriver's waves read every slab with sc1 loads. No
+// release / acquire fences: a release writes back the XCD's whole L2, which with the GEMM's own
+// output dirty in it measured ~30 us per tail tile (profiles/r4/tail_ab.md).
+constexpr int CPOL_SC1 = 16;  // buffer-instruction cache policy: sc1 (write-through / L2-bypassing read)
+
 template <int S>
 PVR_DEV void tail_sum(v4f (&acc)[8][4], __amdgpu_buffer_rsrc_t rs, int tid) {
   constexpr int SLAB_BYTES = 256 * 256 * 4;
@@ -1303,43 +1306,40 @@ PVR_DEV void tail_sum(v4f (&acc)[8][4], __amdgpu_buffer_rsrc_t rs, int tid) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t off = (uint32_t)(((i * 4 + j) * 512 + tid) * 16);
-      v4f s = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      v4f s = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, CPOL_SC1));
 #pragma unroll
-      for (int q = 1; q < S; ++q) s += __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, off, q * SLAB_BYTES, 0));
+      for (int q = 1; q < S; ++q)
+        s += __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(rs, off, q * SLAB_BYTES, CPOL_SC1));
       acc[i][j] = s;
     }
 }
 
 PVR_DEV bool tail_gather(const GemmParams& p, v4f (&acc)[8][4], char* smem, int tloc, int tpart) {
+  typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
   constexpr int SLAB = 256 * 256;  // floats per part
   const int tid = threadIdx.x;
   const int S = p.tail_split;
   float* base = p.tail_ws + (int64_t)tloc * S * SLAB;
-  v4f* mine = (v4f*)(base + (int64_t)tpart * SLAB);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, (uint32_t)S * SLAB * 4);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) mine[(i * 4 + j) * 512 + tid] = acc[i][j];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, acc[i][j]), rs, (uint32_t)(((i * 4 + j) * 512 + tid) * 16),
+                                             tpart * SLAB * 4, CPOL_SC1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
   __syncthreads();
   unsigned* flag = (unsigned*)smem;  // K-tile buffers are idle: every DMA and read has retired
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the release's own wait (see the guide)
     const unsigned old = __hip_atomic_fetch_add(p.tail_cnt + tloc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned last = old == (unsigned)(S - 1) ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // every part of this tile has arrived: re-arm the counter for the next launch
-      __hip_atomic_store(p.tail_cnt + tloc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // every part of this tile has arrived: re-arm the counter for the next launch
+    if (last) __hip_atomic_store(p.tail_cnt + tloc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *(volatile unsigned*)flag = last;
   }
-  __syncthreads();
+  __syncthreads();  // the other waves load only after the adding lane's result is in
   const unsigned last = *(volatile unsigned*)flag;
   if (!last) return false;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(base, (uint32_t)S * SLAB * 4);
   switch (S) {
     case 2: tail_sum<2>(acc, rs, tid); break;
     case 3: tail_sum<3>(acc, rs, tid); break;
@@ -1501,7 +1501,10 @@ int device_cus() {
 // tiles on CUs / r times fewer CUs than it could: e.g. the N = 768 GEMMs of ViT-B/16 at batch 256
 // (591 tiles) spend 3 tile-times on 2.31 rounds of work. Splitting each leftover tile's K loop into
 // S parts puts S*r <= CUs workgroups on the last round, at the price of an fp32 partial-tile
-// exchange (256 KiB per part). Parts keep >= 3 K-tiles each (prologue amortisation) and S <= 4.
+// exchange (256 KiB written per part, S x 256 KiB read by the last). That exchange runs at a
+// workgroup's own bandwidth (~60-120 GB/s), i.e. ~10 us per tail tile, so the split only pays where a
+// tile's K loop is long: each part keeps >= 12 K-tiles (K >= 2304 at S = 3) and S <= 4. Measured on
+// ViT-B/16 b256 (profiles/r4/tail_ab.md): the K = 768 GEMMs lost 20-35 us with 3 x 4-K-tile parts.
 void plan_tail(GemmParams& q, int ntiles, int bke) {
   q.tail_from = 0;
   q.tail_split = 0;
@@ -1512,7 +1515,7 @@ void plan_tail(GemmParams& q, int ntiles, int bke) {
   int S = cus / rem;
   S = S < 4 ? S : 4;
   const int nkt = q.K / bke;
-  while (S > 1 && nkt / S < 3) --S;
+  while (S > 1 && nkt / S < 12) --S;
   if (S < 2) return;
   if ((int64_t)rem * S * 65536 > q.tail_ws_elems || rem > q.tail_cnt_elems) return;
   q.tail_from = ntiles - rem;
@@ -1772,6 +1775,18 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
 }  // namespace
 
 }  // namespace pvr
+
+// The split-K tail plan a one-tile-per-workgroup GEMM of this shape gets (0: none): tests / tools.
+extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes) {
+  pvr::GemmParams q{};
+  q.K = K;
+  q.tail_ws = reinterpret_cast<float*>(16);  // any non-null: plan only
+  q.tail_cnt = reinterpret_cast<unsigned*>(16);
+  q.tail_ws_elems = (int64_t)pvr::device_cus() * 65536;
+  q.tail_cnt_elems = pvr::device_cus();
+  pvr::plan_tail(q, ((M + 255) / 256) * ((N + 255) / 256), elem_bytes == 1 ? 128 : 64);
+  return q.tail_split;
+}
 
 // Host entry. Returns hipSuccess, or hipErrorInvalidValue for an unsupported layout/epilogue pair.
 extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {

@@ -21,6 +21,17 @@ attention, residual adds and the optimizer stay in bf16 / fp32.
 Non-finite values: an Inf element makes its tensor's amax non-finite and a NaN element propagates
 through the NaN-aware amax reduction (csrc/fp8.hip); the scale update then leaves that slot's
 history and scales unchanged, and FusedAdam's non-finite check skips the step.
+
+Data parallelism: the amax histories and scales stay per rank, with no cross-rank max. A scale only
+chooses how one rank's own activations / gradients are represented; every fp8 GEMM output is
+dequantized in its epilogue, so the weight gradients that enter the all-reduce are plain fp32 values,
+the averaged gradients are identical on every rank, and so are the global-norm clip, the non-finite
+skip decision (taken on the all-reduced gradients: an overflow on one rank skips the step on all)
+and the Adam update. Weight scales come from the weights themselves (current scaling), hence agree
+across ranks. A cross-rank amax reduction would only matter for tensors sharded across ranks
+(tensor / sequence parallelism), which this framework does not use. Pinned by
+``tests/test_gpu_train.py::test_ddp_two_ranks_recipe`` (bitwise-equal parameters on both ranks after
+every fp8 step, the overflowing step skipped on both).
 """
 from __future__ import annotations
 

@@ -17,7 +17,7 @@ bucketer) as soon as a group of parameters has its final gradient.
 from __future__ import annotations
 
 import weakref
-from typing import Callable, Dict, Iterable, List, Optional, Tuple
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
 
 import torch
 
@@ -27,6 +27,12 @@ ALIGN = 64  # elements; keeps every parameter 256-B aligned and 4-element vector
 # weight-gradient GEMMs on a second stream (module attribute, not an env knob: the side-stream
 # ordering test switches it off to compare against the serial schedule)
 SIDE_WGRAD = True
+# Side-stream weight-gradient batches whose input tensors stay referenced at once (0: all of them
+# until the end-of-backward join). Older batches are released as new ones are queued: the stream that
+# produced the tensors first waits for that batch's completion event, so their blocks are reused in
+# stream order. Bounds the backward's extra peak memory to a few blocks' activations instead of the
+# whole network's.
+SIDE_WINDOW = 4
 
 
 def _norm_device(device) -> torch.device:
@@ -113,7 +119,8 @@ class ParamStore:
         self._side: Optional[torch.cuda.Stream] = None
         self._side_pending = False
         self._join_queued = False
-        self._side_refs: List[Tuple[torch.cuda.Stream, Tuple[torch.Tensor, ...]]] = []  # held until join_side
+        # (producing stream, held tensors, side-stream completion event) per queued batch
+        self._side_refs: List[Tuple[torch.cuda.Stream, Tuple[torch.Tensor, ...], Any]] = []
         self.refresh_shadow(force=True)
 
     # ------------------------------------------------------------------ validity
@@ -285,7 +292,8 @@ class ParamStore:
         instead keep each block out of reuse until the GPU has passed the side-stream work, so every
         step the host runs ahead of the GPU would hold a whole step of activations: at ViT-L/16 384 px
         batch 128 that exhausted the 288 GB and the allocator's free-and-retry stalled steps for
-        seconds.)"""
+        seconds.) At most ``SIDE_WINDOW`` batches are held at once: queueing another releases the
+        oldest after its producer stream has waited for that batch's completion event."""
         side = self.side_stream()
         if side is None:
             fn()
@@ -294,8 +302,16 @@ class ParamStore:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             fn()
-        self._side_refs.append((main, tensors))
+        done = None
+        if SIDE_WINDOW > 0:
+            done = torch.cuda.Event()
+            done.record(side)
+        self._side_refs.append((main, tensors, done))
         self._side_pending = True
+        while SIDE_WINDOW > 0 and len(self._side_refs) > SIDE_WINDOW:
+            # release the oldest batch's inputs: their producer waits for the batch's wgrads first
+            st, _, ev = self._side_refs.pop(0)
+            st.wait_event(ev)
         self._queue_join()
 
     def _queue_join(self) -> None:
@@ -314,7 +330,7 @@ class ParamStore:
         if self._side_pending and self._side is not None:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_stream(self._side)
-            for s in {st for st, _ in self._side_refs}:
+            for s in {st for st, _, _ in self._side_refs}:
                 if s != cur:
                     s.wait_stream(self._side)
             self._side_refs.clear()

@@ -1,0 +1,52 @@
+"""bench.py's run description for BASELINE.json configs 1-5 without a GPU: per-GPU batch, metric
+string, sequence length and data-parallel settings (the 2/4/8-GPU runs are made by the round driver,
+so their plumbing is pinned here as data)."""
+import importlib.util
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _desc(argv, world):
+    bench = _bench()
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py"] + argv
+        return bench.describe(bench.parse(), world=world)
+    finally:
+        sys.argv = old
+
+
+def test_headline_config_one_and_eight_gpus():
+    d = _desc([], 1)
+    assert d["per_gpu_batch"] == 256 and d["global_batch"] == 256 and not d["ddp"] and d["parallelism"] == "dp1"
+    assert d["metric"] == "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X" and d["seq_len"] == 197
+    d = _desc(["--gpus", "8"], 8)
+    assert d["per_gpu_batch"] == 512 and d["global_batch"] == 4096 and d["ddp"] and d["parallelism"] == "dp8"
+    assert d["metric"] == "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
+
+
+def test_vit_h14_fp8_eight_gpus():
+    d = _desc(["--gpus", "8", "--model", "vit_h14", "--dtype", "fp8"], 8)
+    assert d["per_gpu_batch"] == 512 and d["global_batch"] == 4096 and d["ddp"]
+    assert d["metric"] == "images/sec (whole node) ViT-H/14 224px fp8" and d["seq_len"] == 257
+
+
+def test_vit_l16_384_eight_gpus():
+    d = _desc(["--gpus", "8", "--model", "vit_l16", "--image-size", "384", "--batch", "128"], 8)
+    assert d["seq_len"] == 577 and d["global_batch"] == 1024
+    assert d["metric"] == "images/sec (whole node) ViT-L/16 384px bf16"
+
+
+def test_world1_forced_ddp_and_inference():
+    assert _desc(["--force-ddp"], 1)["ddp"]
+    d = _desc(["--infer"], 1)
+    assert d["metric"] == "inference images/sec (whole node) ViT-B/16 224px bf16"

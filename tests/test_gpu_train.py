@@ -394,6 +394,83 @@ def test_ddp_two_ranks_fused_path_matches_single_process(tmp_path):
         assert err < 2e-2, f"{n}: DDP(2 ranks) vs single-process gradient rel err {err:.3e}"
 
 
+def _gloo_gpu_recipe_worker(rank, world, port, out_dir, cfg, fp8, steps, poison_step, batch):
+    """One rank of a 2-process DDP run sharing cuda:0 (gloo transport) with the full recipe: FusedAdam,
+    clip 1.0, optionally fp8 GEMMs (per-rank delayed scaling) and a non-finite step on rank 1 only
+    (its loss times Inf): the all-reduced gradients are then non-finite on BOTH ranks, so both skip."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+    from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(100 + rank)  # different init per rank: the rank-0 broadcast must fix it
+    m = ViT(**cfg).to(dev)
+    if fp8:
+        m.enable_fp8()
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.25)
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(11 + rank)  # each rank its own data
+    snaps, skipped, losses = [], [], []
+    main = torch.cuda.Stream(device=dev, priority=-1)
+    main.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(main):
+        for step in range(steps):
+            x = torch.rand(batch, 3, cfg["image_size"], cfg["image_size"], generator=g).to(dev)
+            y = torch.randint(0, 10, (batch,), generator=g).to(dev)
+            before = m._pvr_store.flat.clone() if step else None
+            loss = cross_entropy(ddp(x), y)
+            if step == poison_step and rank == 1:
+                loss = loss * float("inf")
+            opt.zero_grad()
+            loss.backward()
+            opt.step(clip_norm=1.0)
+            torch.cuda.synchronize()
+            losses.append(float(loss.item()))
+            skipped.append(bool(before is not None and torch.equal(before, m._pvr_store.flat)))
+            snaps.append(m._pvr_store.flat.detach().cpu().clone())
+    torch.save({"snaps": snaps, "skipped": skipped, "losses": losses, "fp8_on": m._fp8 is not None,
+                "grad_finite": bool(torch.isfinite(m._pvr_store.grad_flat).all().item())},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["fp8_nonfinite", "fp8_generic_attention"])
+def test_ddp_two_ranks_recipe(case, tmp_path):
+    """BASELINE configs 4-5 under data parallelism on the fused path: fp8 GEMMs (ViT-H/14's dtype) and
+    a long sequence on the generic attention path (257 tokens: the in_proj bias gradient from column
+    sums on the weight-gradient stream). Parameters stay bitwise identical across ranks after every
+    step (each rank's fp8 scales are its own; the averaged gradients, hence the global-norm skip
+    decision and the Adam update, are the same everywhere), and a step that overflows on one rank
+    is skipped on both."""
+    import torch.multiprocessing as mp
+
+    if case == "fp8_nonfinite":
+        cfg = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=256, mlp_size=512,
+                   num_classes=10, mlp_dropout=0.1, embedding_dropout=0.1)
+        steps, poison, batch = 5, 2, 16  # 16 x 17 = 272 tokens: the fp8 path needs >= 256
+    else:
+        cfg = dict(image_size=64, patch_size=4, num_transformer_layer=2, num_heads=4, embedding_dim=256, mlp_size=512,
+                   num_classes=10, mlp_dropout=0.1, embedding_dropout=0.1)
+        steps, poison, batch = 3, -1, 4
+    world = 2
+    mp.spawn(_gloo_gpu_recipe_worker, args=(world, _free_port(), str(tmp_path), cfg, True, steps, poison, batch),
+             nprocs=world, join=True)
+    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
+    assert r[0]["fp8_on"] and r[1]["fp8_on"], "fp8 path did not engage"
+    for s in range(steps):
+        assert torch.equal(r[0]["snaps"][s], r[1]["snaps"][s]), f"parameters differ across ranks after step {s}"
+    for i in range(world):
+        for s in range(1, steps):
+            assert r[i]["skipped"][s] == (s == poison), (case, i, r[i]["skipped"])
+        assert r[i]["grad_finite"], "the step after the overflow must be finite again"
+        assert all(v == v and abs(v) != float("inf") for s, v in enumerate(r[i]["losses"]) if s != poison)
+
+
 def test_summary_on_gpu_model_matches_notebook():
     # torchinfo-style summary of a cuda model: the per-module path runs inside the summary (the fused
     # encoder would bypass the hooks), the fused path is back afterwards
