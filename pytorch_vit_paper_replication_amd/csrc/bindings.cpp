@@ -29,7 +29,8 @@ hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t,
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
 hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
-hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t,
+                      const float*, unsigned*, hipStream_t);
 hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
 hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
@@ -354,13 +355,32 @@ void transpose_batched(torch::Tensor src, torch::Tensor dst, torch::Tensor meta,
 }
 
 void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tensor> db, c10::optional<torch::Tensor> dz,
-            c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p) {
+            c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
+            c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax) {
   const DropArgs d = drop_args(seed, drop_p, "colsum");
   int64_t ldz = 0;
   uint16_t* dzp = nullptr;
   if (dz.has_value() && dz->defined()) { dzp = const_cast<uint16_t*>(bf(*dz, "dz")); ldz = ld_of(*dz, "dz"); }
+  // optional e5m2 copy of the (masked) gradient + amax record (the fp8 dgrad operand)
+  uint8_t* qp = nullptr;
+  int64_t ldq = 0;
+  const float* qs = nullptr;
+  unsigned* qa = nullptr;
+  if (q_out.has_value() && q_out->defined()) {
+    TORCH_CHECK(q_out->is_cuda() && q_out->scalar_type() == torch::kUInt8 && q_out->dim() == 2 && q_out->stride(1) == 1 &&
+                    q_out->size(0) >= rows && q_out->size(1) >= N && q_out->stride(0) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(q_out->data_ptr()) % 8 == 0,
+                "colsum: q_out uint8 [>= rows][>= N], row stride a multiple of 8, 8-byte aligned");
+    TORCH_CHECK(q_scale.has_value() && q_scale->defined() && q_amax.has_value() && q_amax->defined() && q_amax->is_cuda() &&
+                    q_amax->scalar_type() == torch::kInt32,
+                "colsum: q_out needs q_scale (f32) and q_amax (int32)");
+    qp = q_out->data_ptr<uint8_t>();
+    ldq = q_out->stride(0);
+    qs = f32(*q_scale, "q_scale");
+    qa = reinterpret_cast<unsigned*>(q_amax->data_ptr());
+  }
   check(pvr_colsum(bf(dy, "dy"), ld_of(dy, "dy"), (int)rows, (int)N, opt_ptr<float>(db), dzp, ldz, d.seed, (uint64_t)seed_offset,
-                   d.thr, d.scale, stream()),
+                   d.thr, d.scale, qp, ldq, qs, qa, stream()),
         "colsum");
 }
 
@@ -907,7 +927,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_dbias_reduce", &attn_dbias_reduce);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("transpose_batched", &transpose_batched);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("dy"), py::arg("rows"), py::arg("N"), py::arg("db"), py::arg("dz"), py::arg("seed"),
+        py::arg("seed_offset"), py::arg("drop_p"), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
+        py::arg("q_amax") = py::none());
   m.def("im2col", &im2col);
   m.def("cls_rows", &cls_rows);
   m.def("patch_bwd", &patch_bwd);

@@ -25,10 +25,17 @@ __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restr
 
 // dY [rows][N] (row stride ld) -> db[N] += column sums of (mask * dY); if dz != null also writes
 // the masked gradient dz (= dropout backward) with row stride ld_dz.
+// Q8: also the e5m2 copy of the (masked) gradient, q[r][n] = fp8(v * *qscale), and its amax record
+// (the fp8 dgrad operand of the same tensor whose column sums are the bias gradient: one read, two uses)
+template <bool Q8>
 __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict__ dy, int64_t ld, int rows, int N,
                                                       float* __restrict__ db, uint16_t* __restrict__ dz, int64_t ld_dz,
-                                                      const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale) {
+                                                      const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
+                                                      uint8_t* __restrict__ qout, int64_t ld_q, const float* __restrict__ qscale,
+                                                      unsigned* __restrict__ amax) {
   __shared__ float red[4][64 * 8];
+  const float qs = Q8 ? *qscale : 1.f;
+  float qam = 0.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;  // 8-column chunk
   const bool act = c * 8 < N;
@@ -69,6 +76,11 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
           o.z = pack2bf(v[4], v[5]); o.w = pack2bf(v[6], v[7]);
           *(uint4*)(dz + (int64_t)r * ld_dz + c * 8) = o;
         }
+        if constexpr (Q8) {
+          *(uint2*)(qout + (int64_t)r * ld_q + c * 8) = pack8_fp8<1>(v, qs);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qam = nan_max(qam, fabsf(v[j]));
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += v[j];
       }
@@ -80,6 +92,16 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
   for (int i = threadIdx.x; i < 64 * 8; i += 256) {
     const int col = blockIdx.x * 64 * 8 + i;
     if (col < N && db) atomicAdd(db + col, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  }
+  if constexpr (Q8) {  // one amax atomic per workgroup
+    qam = wave_max_nan(qam);
+    __syncthreads();  // red[] reads above are done: reuse red[0][0..3]
+    if (lane == 0) red[0][wave] = qam;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = nan_max(nan_max(red[0][0], red[0][1]), nan_max(red[0][2], red[0][3]));
+      if (!(m <= 0.f)) atomicMax(amax, __float_as_uint(m));
+    }
   }
 }
 
@@ -372,14 +394,17 @@ extern "C" hipError_t pvr_cast_f32_bf16(const float* in, uint16_t* out, int64_t 
 }
 
 extern "C" hipError_t pvr_colsum(const uint16_t* dy, int64_t ld, int rows, int N, float* db, uint16_t* dz, int64_t ld_dz,
-                                 const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale, hipStream_t s) {
+                                 const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale, uint8_t* q, int64_t ld_q,
+                                 const float* qscale, unsigned* amax, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (N % 8 != 0) return hipErrorInvalidValue;
+  if (q && (!qscale || !amax || ld_q % 8 != 0 || reinterpret_cast<uintptr_t>(q) % 8 != 0)) return hipErrorInvalidValue;
   const int gx = (N / 8 + 63) / 64;
   int gy = (rows + 63) / 64;
   if (gy > 256) gy = 256;
-  hipLaunchKernelGGL(colsum_kernel, dim3(gx, gy), dim3(256), 0, s, dy, ld, rows, N, db, dz, ld_dz, seed_ptr, seed_off, thr, scale);
+  hipLaunchKernelGGL(q ? colsum_kernel<true> : colsum_kernel<false>, dim3(gx, gy), dim3(256), 0, s, dy, ld, rows, N, db, dz, ld_dz,
+                     seed_ptr, seed_off, thr, scale, q, ld_q, qscale, amax);
   return hipGetLastError();
 }
 

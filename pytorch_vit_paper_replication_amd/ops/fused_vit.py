@@ -366,8 +366,16 @@ class EncoderBlockFn(torch.autograd.Function):
                 wgrad(dqkv, xn1, gwqkv, 3, 0)
 
         if f8d is not None and f8d[0].wgrad_ready(f8d[1], 3, 0) and store.bf16_t(wqkv) is not None:
-            # dQKV's e5m2 copy now, so the side-stream qkv weight gradient transposes it (the dgrad uses it too)
-            pre_q[3] = f8d[0].grad_quant(dqkv, f8d[1], 3)
+            # dQKV's e5m2 copy now, so the side-stream qkv weight gradient transposes it (the dgrad uses it too).
+            # With a column-sum in_proj bias gradient (generic attention path) and a calibrated slot, ONE
+            # pass over dQKV writes both: the bias gradient (all three slices, exact with or without
+            # attention dropout) and the e5m2 copy; the side stream then has no bias work
+            prod = f8d[0].grad_producer(f8d[1], 3)
+            if side_db and prod is not None:
+                pre_q[3] = gemm.bias_grad(dqkv, gbqkv, quant=prod)
+                side_db = False
+            else:
+                pre_q[3] = f8d[0].grad_quant(dqkv, f8d[1], 3)
         store.on_side(attn_wgrads, dx1, o, dqkv, xn1, do, *(() if db_part is None else (db_part,)), *side8(2, 3))
         dxn1 = dgrad(dqkv, wqkv, 3)
         dx = torch.empty_like(dx2)

@@ -734,6 +734,31 @@ def check_layernorm_bwd_q8(T=3000, D=1280, linked=False, p=0.1):
             {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 8e-3, "grad_not_identical": 0, "sums_l2": 1e-6})  # amax: bf16 rounding <= 2^-8
 
 
+def check_colsum_q8(T=4000, N=3840):
+    """Column sums (the in_proj bias gradient over all of dQKV) fused with dQKV's e5m2 copy: the sums
+    as the plain column-sum pass, the copy as the quantize pass with the same scale (the inputs are
+    the bf16 values themselves, so the bytes should agree), amax = max|dy|."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    dy = bf(rnd(T, N) * 0.3)
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2)
+    meta.calibrated[0] = True
+    meta.qscale.fill_(8.0)
+    meta.dscale.copy_(1.0 / meta.qscale)
+    db0, db1 = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+    G.bias_grad(dy, db0)
+    q, ds = G.bias_grad(dy, db1, quant=meta.producer(0))
+    ref = torch.empty(T, N, dtype=torch.uint8, device=DEV)
+    ext.fp8_quant(dy, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), F8.E5M2)
+    amax = meta.amax.view(torch.float32)[0].item()
+    m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
+         "amax_rel": abs(amax - dy.float().abs().max().item()) / dy.float().abs().max().item(),
+         "colsum_l2": errs(db1, db0)[0], "colsum_vs_fp32_l2": errs(db1, dy.float().sum(0))[0]}
+    return (f"colsum + e5m2 copy T{T} N{N}", m,
+            {"fp8_steps": 1, "mismatch_frac": 1e-3, "amax_rel": 1e-6, "colsum_l2": 1e-6, "colsum_vs_fp32_l2": 1e-5})
+
+
 def check_attn_fwd_q8(B=2, N=257, H=4, dh=80):
     """Attention forward with the fused e4m3 output copy: O / lse bit-identical to the plain forward,
     the copy within one fp8 step of quantizing O, amax = max|O| (up to O's bf16 rounding)."""
@@ -1411,6 +1436,8 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_fp8_transpose(257, 768, 0),
         lambda: check_layernorm_fwd_q8(50, 768),
         check_layernorm_bwd_q8,                                   # D 1280 (H/14): 8-column chunks
+        check_colsum_q8,
+        lambda: check_colsum_q8(1001, 2304),
         lambda: check_layernorm_bwd_q8(2000, 768, linked=True),   # D 768: 4-column chunks + dz
         lambda: check_layernorm_bwd_q8(3000, 1280, linked=True),
         lambda: check_gemm_fp8_producer(1030, 768, 1280, True),
