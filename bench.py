@@ -53,7 +53,9 @@ def parse():
     p.add_argument("--serial-wgrad", action="store_true",
                    help="weight-gradient GEMMs on the main stream (no side stream): clean per-kernel times for profiles")
     p.add_argument("--side-window", type=int, default=None,
-                   help="A/B: weight-gradient batches whose inputs stay held at once (0 = until the end of backward)")
+                   help="A/B: weight-gradient batches whose inputs stay held at once (0 = no count bound)")
+    p.add_argument("--side-hold-gb", type=float, default=None,
+                   help="A/B: GB of weight-gradient inputs held at once (0 = until the end of backward)")
     p.add_argument("--no-gemm-tail", action="store_true",
                    help="A/B: no split-K tail on the last dispatch round of the one-tile-per-workgroup GEMMs")
     p.add_argument("--main-prio", type=int, default=-1,
@@ -112,13 +114,15 @@ def main():
     from pytorch_vit_paper_replication_amd.ops.fused_vit import backward, cross_entropy
     from pytorch_vit_paper_replication_amd.parallel import DistributedDataParallel, barrier, init_distributed
 
-    if args.serial_wgrad or args.side_window is not None:
+    if args.serial_wgrad or args.side_window is not None or args.side_hold_gb is not None:
         from pytorch_vit_paper_replication_amd.runtime import param_store
 
         if args.serial_wgrad:
             param_store.SIDE_WGRAD = False
         if args.side_window is not None:
             param_store.SIDE_WINDOW = args.side_window
+        if args.side_hold_gb is not None:
+            param_store.SIDE_HOLD_BYTES = int(args.side_hold_gb * 2**30)
     rank, world, device = init_distributed()
     if args.no_gemm_tail and args.impl == "fused":
         from pytorch_vit_paper_replication_amd import _ext

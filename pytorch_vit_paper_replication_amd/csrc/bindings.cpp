@@ -21,7 +21,7 @@ struct AdamGroup {
 
 extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
-int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes);
+int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
@@ -152,7 +152,7 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
           int64_t addend_period, c10::optional<torch::Tensor> aux, int64_t row_group, int64_t row_stride_group,
           int64_t row_offset, c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, int64_t k_split,
           int64_t tile_cfg, c10::optional<torch::Tensor> dbg, c10::optional<torch::Tensor> colsum,
-          int64_t epi_staged) {
+          int64_t epi_staged, int64_t tail_limit) {
   pvr::GemmParams p{};
   p.epi_staged = (int)epi_staged;
   if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
@@ -203,7 +203,11 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   p.k_split_len = k_split > 0 ? (int)(((k_split + 63) / 64) * 64) : (int)(((K + 63) / 64) * 64);
   p.epi = (int)epi;
   p.tile_cfg = (int)tile_cfg;
-  if (epi <= 2 && p.k_split_len >= K) attach_tail(p, C);
+  // tail_limit: -1 = no split tail, 0 = unlimited, n > 0 = at most n workgroups in the split round
+  if (epi <= 2 && p.k_split_len >= K && tail_limit >= 0) {
+    attach_tail(p, C);
+    p.tail_max_units = (int)tail_limit;
+  }
   check(pvr_gemm(&p, stream()), "gemm");
 }
 
@@ -578,7 +582,8 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
               int64_t epi, torch::Tensor scale_a, torch::Tensor scale_b, c10::optional<torch::Tensor> bias,
               c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> seed, int64_t seed_offset,
               double drop_p, c10::optional<torch::Tensor> colsum, c10::optional<torch::Tensor> q_out,
-              c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, int64_t q_fmt, bool c_skip) {
+              c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, int64_t q_fmt, bool c_skip,
+              int64_t tail_limit) {
   pvr::GemmParams p{};
   // c_skip: only the fp8 copy (or aux / column sums) of the output is consumed; the bf16 stores are
   // dropped (register-direct epilogue; other epilogues still write C, which is allocated)
@@ -630,7 +635,10 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
   p.k_split_len = (int)K;
   p.epi = (int)epi;
   p.tile_cfg = 12;
-  if (epi <= 2) attach_tail(p, C);
+  if (epi <= 2 && tail_limit >= 0) {  // tail_limit: as for gemm()
+    attach_tail(p, C);
+    p.tail_max_units = (int)tail_limit;
+  }
   check(pvr_gemm(&p, stream()), "gemm_fp8");
 }
 
@@ -903,15 +911,17 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
-  m.def("gemm_tail_split", [](int64_t M, int64_t N, int64_t K, int64_t elem_bytes) {
-    return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes); }, "K-parts of the split tail round this GEMM shape gets (0: none)");
+  m.def("gemm_tail_split", [](int64_t M, int64_t N, int64_t K, int64_t elem_bytes, int64_t max_units) {
+    return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes, (int)max_units); },
+    py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
+    "K-parts of the split tail round this GEMM shape gets (0: none)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),
         py::arg("addend_period"), py::arg("aux"), py::arg("row_group"), py::arg("row_stride_group"),
         py::arg("row_offset"), py::arg("seed"), py::arg("seed_offset"), py::arg("drop_p"), py::arg("k_split"),
         py::arg("tile_cfg"), py::arg("dbg") = py::none(), py::arg("colsum") = py::none(),
-        py::arg("epi_staged") = 0);
+        py::arg("epi_staged") = 0, py::arg("tail_limit") = 0);
   m.def("num_cus", &num_cus);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_fwd_q8", &layernorm_fwd_q8);
@@ -952,7 +962,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("scale_a"), py::arg("scale_b"), py::arg("bias") = py::none(),
         py::arg("resid") = py::none(), py::arg("aux") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0,
         py::arg("drop_p") = 0.0, py::arg("colsum") = py::none(), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
-        py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0, py::arg("c_skip") = false);
+        py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0, py::arg("c_skip") = false, py::arg("tail_limit") = 0);
   m.def("fp8_transpose", &fp8_transpose);
   m.def("gemm_fp8_wgrad_mn", &gemm_fp8_wgrad_mn);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));

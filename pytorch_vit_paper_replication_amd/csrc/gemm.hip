@@ -1517,6 +1517,10 @@ void plan_tail(GemmParams& q, int ntiles, int bke) {
   const int nkt = q.K / bke;
   while (S > 1 && nkt / S < 12) --S;
   if (S < 2) return;
+  if (q.tail_max_units > 0) {
+    while (S > 1 && rem * S > q.tail_max_units) --S;
+    if (S < 2) return;
+  }
   if ((int64_t)rem * S * 65536 > q.tail_ws_elems || rem > q.tail_cnt_elems) return;
   q.tail_from = ntiles - rem;
   q.tail_split = S;
@@ -1777,9 +1781,10 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
 }  // namespace pvr
 
 // The split-K tail plan a one-tile-per-workgroup GEMM of this shape gets (0: none): tests / tools.
-extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes) {
+extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units) {
   pvr::GemmParams q{};
   q.K = K;
+  q.tail_max_units = max_units;
   q.tail_ws = reinterpret_cast<float*>(16);  // any non-null: plan only
   q.tail_cnt = reinterpret_cast<unsigned*>(16);
   q.tail_ws_elems = (int64_t)pvr::device_cus() * 65536;

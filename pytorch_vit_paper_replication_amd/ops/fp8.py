@@ -263,7 +263,7 @@ def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts:
     epi = gemm.EPI_DGELU if dgelu_aux is not None else gemm.EPI_BF16
     kw, q = _quant_args(quant, T, K, gq.device)
     _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum,
-                        c_skip=bool(skip_out and quant is not None), **kw)
+                        c_skip=bool(skip_out and quant is not None), tail_limit=gemm.DGRAD_TAIL_UNITS, **kw)
     return out if quant is None else (out, q)
 
 

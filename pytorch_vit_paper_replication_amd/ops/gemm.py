@@ -76,8 +76,15 @@ def _small_splitk(T: int, N: int, K: int) -> int:
     return s if s >= 2 else 0
 
 
-def _gemm(*args, tile: int, colsum=None):
-    _ext.ext().gemm(*args, tile, colsum=colsum)
+# Split-K tail of the last dispatch round (csrc/gemm.hip plan_tail): forward GEMMs take it without a
+# limit (nothing runs beside them); the backward's dgrad GEMMs only when the split round stays this
+# small, because the weight-gradient side stream's long workgroups hold the CUs a wide split round
+# needs (ViT-B/16 b256: unlimited -0.6 % per step, profiles/r4/tail_ab.md). -1 disables (A/B).
+DGRAD_TAIL_UNITS = 64
+
+
+def _gemm(*args, tile: int, colsum=None, tail_limit: int = 0):
+    _ext.ext().gemm(*args, tile, colsum=colsum, tail_limit=tail_limit)
 
 
 def _drop_args(drop: Drop):
@@ -134,10 +141,12 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
         raise ValueError("colsum is fused only into the GELU-backward epilogue")
     if wt is not None and N % 64 == 0:
         _gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t", dgelu=dgelu_aux is not None), colsum=colsum)
+              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t", dgelu=dgelu_aux is not None), colsum=colsum,
+              tail_limit=DGRAD_TAIL_UNITS)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-                        seed, soff, p, 0, _tile(T, K, N, "dgrad") if tile is None else tile, colsum=colsum)
+                        seed, soff, p, 0, _tile(T, K, N, "dgrad") if tile is None else tile, colsum=colsum,
+                        tail_limit=DGRAD_TAIL_UNITS)
     return out
 
 

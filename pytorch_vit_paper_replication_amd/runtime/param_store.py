@@ -27,12 +27,15 @@ ALIGN = 64  # elements; keeps every parameter 256-B aligned and 4-element vector
 # weight-gradient GEMMs on a second stream (module attribute, not an env knob: the side-stream
 # ordering test switches it off to compare against the serial schedule)
 SIDE_WGRAD = True
-# Side-stream weight-gradient batches whose input tensors stay referenced at once (0: all of them
-# until the end-of-backward join). Older batches are released as new ones are queued: the stream that
-# produced the tensors first waits for that batch's completion event, so their blocks are reused in
-# stream order. Bounds the backward's extra peak memory to a few blocks' activations instead of the
-# whole network's.
-SIDE_WINDOW = 4
+# Bytes of side-stream weight-gradient inputs held at once (0: every batch until the end-of-backward
+# join). Once more is held, the oldest batches are released: the stream that produced their tensors
+# first waits for that batch's completion event, so the blocks are reused in stream order. Each such
+# wait can stall the dgrad chain behind the low-priority side stream, so the bound is in bytes and
+# generous: ViT-B/16 b256 holds ~1 GB and never waits (a 4-batch window there cost 1.2 % per step),
+# ViT-H/14 fp8 b256 peaked at 158.5 GB unbounded vs 133 GB with a 4-batch window (ADVICE r3,
+# profiles/r4/side_window.md).
+SIDE_HOLD_BYTES = 16 << 30
+SIDE_WINDOW = 0  # alternatively a batch-count bound (A/B)
 
 
 def _norm_device(device) -> torch.device:
@@ -120,7 +123,8 @@ class ParamStore:
         self._side_pending = False
         self._join_queued = False
         # (producing stream, held tensors, side-stream completion event) per queued batch
-        self._side_refs: List[Tuple[torch.cuda.Stream, Tuple[torch.Tensor, ...], Any]] = []
+        self._side_refs: List[Tuple[torch.cuda.Stream, Tuple[torch.Tensor, ...], Any, int]] = []
+        self._side_bytes = 0
         self.refresh_shadow(force=True)
 
     # ------------------------------------------------------------------ validity
@@ -292,8 +296,9 @@ class ParamStore:
         instead keep each block out of reuse until the GPU has passed the side-stream work, so every
         step the host runs ahead of the GPU would hold a whole step of activations: at ViT-L/16 384 px
         batch 128 that exhausted the 288 GB and the allocator's free-and-retry stalled steps for
-        seconds.) At most ``SIDE_WINDOW`` batches are held at once: queueing another releases the
-        oldest after its producer stream has waited for that batch's completion event."""
+        seconds.) At most ``SIDE_HOLD_BYTES`` (or ``SIDE_WINDOW`` batches) are held at once: queueing
+        more releases the oldest after its producer stream has waited for that batch's completion
+        event."""
         side = self.side_stream()
         if side is None:
             fn()
@@ -303,15 +308,19 @@ class ParamStore:
         with torch.cuda.stream(side):
             fn()
         done = None
-        if SIDE_WINDOW > 0:
+        if SIDE_WINDOW > 0 or SIDE_HOLD_BYTES > 0:
             done = torch.cuda.Event()
             done.record(side)
-        self._side_refs.append((main, tensors, done))
+        nbytes = sum(t.untyped_storage().nbytes() for t in tensors if isinstance(t, torch.Tensor))
+        self._side_refs.append((main, tensors, done, nbytes))
+        self._side_bytes += nbytes
         self._side_pending = True
-        while SIDE_WINDOW > 0 and len(self._side_refs) > SIDE_WINDOW:
+        while len(self._side_refs) > 1 and ((SIDE_WINDOW > 0 and len(self._side_refs) > SIDE_WINDOW) or
+                                            (SIDE_HOLD_BYTES > 0 and self._side_bytes > SIDE_HOLD_BYTES)):
             # release the oldest batch's inputs: their producer waits for the batch's wgrads first
-            st, _, ev = self._side_refs.pop(0)
+            st, _, ev, nb = self._side_refs.pop(0)
             st.wait_event(ev)
+            self._side_bytes -= nb
         self._queue_join()
 
     def _queue_join(self) -> None:
@@ -330,10 +339,11 @@ class ParamStore:
         if self._side_pending and self._side is not None:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_stream(self._side)
-            for s in {st for st, _, _ in self._side_refs}:
+            for s in {r[0] for r in self._side_refs}:
                 if s != cur:
                     s.wait_stream(self._side)
             self._side_refs.clear()
+            self._side_bytes = 0
             self._side_pending = False
 
     def zero_grad(self) -> None:

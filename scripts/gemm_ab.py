@@ -76,7 +76,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="vit_b16", choices=sorted(SHAPES))
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--ab", default="", help="'tail': split-K tail on / off")
     ap.add_argument("--only", default="", help="comma-separated substrings of case names")
     a = ap.parse_args()
@@ -90,12 +90,18 @@ def main():
         variants = [("tail on ", lambda: ext.set_gemm_tail(True)), ("tail off", lambda: ext.set_gemm_tail(False))]
     cs = [c for c in cases(T, D, M, dev) if not a.only or any(s in c[0] for s in a.only.split(","))]
     res = {}
-    for _ in range(a.rounds):
+    for rnd in range(a.rounds):
         for name, fl, ours, lib in cs:
-            res.setdefault((name, "lib"), []).append(timeit(lib))
-            for vn, setv in variants:
+            # variant order alternates per round (A B lib, then lib B A, ...): a fixed order biased the
+            # comparison by ~10 % on GEMMs the switch does not even touch (clock / power history)
+            order = variants if rnd % 2 == 0 else variants[::-1]
+            if rnd % 2:
+                res.setdefault((name, "lib"), []).append(timeit(lib))
+            for vn, setv in order:
                 setv()
                 res.setdefault((name, vn), []).append(timeit(ours))
+            if rnd % 2 == 0:
+                res.setdefault((name, "lib"), []).append(timeit(lib))
     ext.set_gemm_tail(True)
     print(f"# {a.model} batch {a.batch} (T = {T}), {a.rounds} rounds; median (min) ms, TFLOP/s at the median", flush=True)
     for name, fl, _, _ in cs:

@@ -232,23 +232,32 @@ def check_gemm_tail_split(M=50432, N=768, K=768, kind="resid_drop", p=0.1):
             def run():
                 return (G.linear_fwd(x, w, b, resid=r, drop=drop),)
         refs = None
-    with tile(12):
-        with gemm_tail(False):
-            base = run()
-        a = run()
-        c = run()
+    # dropped elements: 0 without a residual, exactly the residual with one (out = resid + 0)
+    dropped = (lambda t: t == r) if kind == "resid_drop" else (lambda t: t == 0)
+    old_units, G.DGRAD_TAIL_UNITS = G.DGRAD_TAIL_UNITS, 0  # the backward's split-round limit off: split here
+    try:
+        with tile(12):
+            with gemm_tail(False):
+                base = run()
+            a = run()
+            c = run()
+    finally:
+        G.DGRAD_TAIL_UNITS = old_units
     m = worst(*zip(a, base))
     # (the dGELU column sum accumulates with float atomics: its order, hence its last bits, vary run
     # to run with or without the split; determinism is checked on the GEMM outputs)
     m["nondeterministic"] = float(not all(torch.equal(u, v) for u, v in zip(a[:1] if kind == "dgelu" else a, c)))
-    m["mask_differs"] = float(not all(torch.equal(u == 0, v == 0) for u, v in zip(a[:1], base[:1]))) if kind != "dgelu" else 0.0
+    # with a residual, a kept element whose value is below half a bf16 ulp of the residual also reads
+    # as "dropped", and fp32 reassociation can flip such a borderline element: a tiny tolerance there
+    diff = (dropped(a[0]) != dropped(base[0])).float().mean().item() if kind != "dgelu" else 0.0
+    m["mask_differs"] = diff if kind == "resid_drop" else float(diff > 0)
     if refs is not None:
         l2, mx = errs(a[0], refs[0])
         l2c, mxc = errs(a[1], refs[1])
         m.update(ref_l2=l2, ref_max=mx, colsum_l2=l2c)
         lims = lim(1e-3, 8e-3, nondeterministic=0, mask_differs=0, ref_l2=3.5e-3, ref_max=7e-3, colsum_l2=1.5e-6)
     else:
-        lims = lim(1e-3, 8e-3, nondeterministic=0, mask_differs=0)
+        lims = lim(1e-3, 8e-3, nondeterministic=0, mask_differs=2e-6 if kind == "resid_drop" else 0)
     tiles = math.ceil(M / 256) * math.ceil(N / 256)
     S = _ext.ext().gemm_tail_split(M, N, K, 2)
     m["not_split"] = float(S < 2)
