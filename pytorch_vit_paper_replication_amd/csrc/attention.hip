@@ -27,50 +27,59 @@ namespace {
 
 
 // ----------------------------------------------------------------------------------- forward
-template <int DH, bool DROP>
+// QG 16-query groups per wave (workgroup = 4 waves = 64*QG queries). With QG = 2 every K fragment
+// (S^T = K.Q^T) and V^T fragment (O^T += V^T.P^T) read from LDS feeds two MFMAs instead of one, and
+// the per-tile fixed costs (barrier, DMA issue, fragment address math) are shared by 32 queries.
+// KT keys per tile; the dynamic LDS holds two stages of K and V images (4 x KT x 128 x NH bytes).
+template <int DH, bool DROP, int QG, int KT>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
                                                         int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale,
                                                         AttnDrop drop, AttnQ8 q8) {
   using C = Hd<DH>;
-  // keys per tile: 64, or 32 for two-image head rows (dh > 64), so that the two K/V stages stay at
-  // 32 KiB and four workgroups share a CU
-  constexpr int KT = C::NH == 1 ? 64 : 32;
+  static_assert(KT == 32 || KT == 64, "keys per tile");
   constexpr int NFR = KT / 16;                   // 16-key S fragments per tile
-  constexpr int TILE_BYTES = KT * 128 * C::NH;   // one K or V tile image (8 or 16 KiB)
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];  // [stage][K|V]
+  constexpr int TILE_BYTES = KT * 128 * C::NH;   // one K or V tile image
+  constexpr int QW = 16 * QG;                    // queries per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // [stage][K|V]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
   // XCD-aware: the query blocks of one (batch, head) get consecutive logical ids on ONE XCD, so its
   // K/V tiles are fetched into that XCD's L2 once instead of once per query block
-  const int nqb = (N + 63) / 64;
+  const int nqb = (N + 4 * QW - 1) / (4 * QW);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int bh = L / nqb, b = bh / H, h = bh % H;
-  const int q0 = (L % nqb) * 64 + wave * 16;
+  const int q0 = (L % nqb) * 4 * QW + wave * QW;  // group gi: queries q0 + 16 gi ..
 
   const uint16_t* base = qkv + (int64_t)b * N * ld;
   const int64_t extent = ((int64_t)(N - 1) * ld + DH) * 2;
   const __amdgpu_buffer_rsrc_t krs = make_rsrc(base + D + h * DH, clamp_bytes(extent));
   const __amdgpu_buffer_rsrc_t vrs = make_rsrc(base + 2 * D + h * DH, clamp_bytes(extent));
 
-  // Q fragments (B operand): lane holds Q[q0 + li][32ks + 8g + j]
-  v8s qf[C::KS];
-  {
-    const int q = min(q0 + li, N - 1);
+  // Q fragments (B operand): lane holds Q[q0 + 16 gi + li][32ks + 8g + j]
+  v8s qf[QG][C::KS];
 #pragma unroll
-    for (int ks = 0; ks < C::KS; ++ks) qf[ks] = load_frag<DH>(base + (int64_t)q * ld + h * DH, ks * 32 + 8 * g);
+  for (int gi = 0; gi < QG; ++gi) {
+    const int q = min(q0 + 16 * gi + li, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < C::KS; ++ks) qf[gi][ks] = load_frag<DH>(base + (int64_t)q * ld + h * DH, ks * 32 + 8 * g);
   }
 
   const float c = scale * LOG2E;
-  float m_run = -INFINITY, l_run = 0.f;
-  uint32_t dkey = 0, drow = 0;  // dropout: the pair's hash key, this lane's query row start idx
-  if constexpr (DROP) {
-    dkey = attn_drop_key(drop, bh);
-    drow = (uint32_t)min(q0 + li, N - 1) * (uint32_t)((N + 3) & ~3);
-  }
-  v4f o[C::NE];
+  float m_run[QG], l_run[QG];
+  uint32_t dkey = 0, drow[QG];  // dropout: the pair's hash key, this lane's query row start idx
+  if constexpr (DROP) dkey = attn_drop_key(drop, bh);
 #pragma unroll
-  for (int e = 0; e < C::NE; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int gi = 0; gi < QG; ++gi) {
+    m_run[gi] = -INFINITY;
+    l_run[gi] = 0.f;
+    drow[gi] = DROP ? (uint32_t)min(q0 + 16 * gi + li, N - 1) * (uint32_t)((N + 3) & ~3) : 0u;
+  }
+  v4f o[QG][C::NE];
+#pragma unroll
+  for (int gi = 0; gi < QG; ++gi)
+#pragma unroll
+    for (int e = 0; e < C::NE; ++e) o[gi][e] = v4f{0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = (N + KT - 1) / KT;
   dma_rows<C::NH>(krs, smem, KT, ld, 0, wave, 4, lane);
@@ -78,10 +87,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // Waves whose 16 queries all lie past N only help stage K/V (no math); the running max is kept
-  // in scaled log2 units so a score costs max + fma + exp + add; keys past N exist only in the last
-  // tile, whose all-invalid 16-key fragments are skipped outright.
+  // Waves whose queries all lie past N only help stage K/V (no math), as do a wave's groups past N
+  // (QG = 2); the running max is kept in scaled log2 units so a score costs max + fma + exp + add;
+  // keys past N exist only in the last tile, whose all-invalid 16-key fragments are skipped outright.
   const bool active = q0 < N;
+  const bool g1 = QG > 1 && q0 + 16 < N;  // second group holds a valid query (uniform)
   for (int t = 0; t < ntiles; ++t) {
     const char* kimg = smem + (t & 1) * 2 * TILE_BYTES;
     const char* vimg = kimg + TILE_BYTES;
@@ -93,50 +103,60 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     if (active) {
       const int kbase = t * KT;
       const int nf = min(NFR, (N - kbase + 15) >> 4);  // 16-key fragments holding a valid key (uniform)
-      // S^T[key][q] for the key fragments
-      v4f s[NFR];
+      // S^T[key][q] for the key fragments: one K fragment read serves every query group
+      v4f s[QG][NFR];
 #pragma unroll
       for (int f = 0; f < NFR; ++f) {
-        s[f] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int gi = 0; gi < QG; ++gi) s[gi][f] = v4f{0.f, 0.f, 0.f, 0.f};
         if (f < nf) {
 #pragma unroll
-          for (int ks = 0; ks < C::KS; ++ks) s[f] = mfma16(frag_rows(kimg, KT, 16 * f, ks, lane), qf[ks], s[f]);
+          for (int ks = 0; ks < C::KS; ++ks) {
+            const v8s kf = frag_rows(kimg, KT, 16 * f, ks, lane);
+            s[0][f] = mfma16(kf, qf[0][ks], s[0][f]);
+            if (QG > 1 && g1) s[QG - 1][f] = mfma16(kf, qf[QG - 1][ks], s[QG - 1][f]);
+          }
         }
       }
       if (kbase + KT > N) {  // tail tile: mask keys >= N
 #pragma unroll
+        for (int gi = 0; gi < QG; ++gi)
+#pragma unroll
+          for (int f = 0; f < NFR; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (kbase + 16 * f + 4 * g + r >= N) s[gi][f][r] = -INFINITY;
+      }
+#pragma unroll
+      for (int gi = 0; gi < QG; ++gi) {
+        float tmax = s[gi][0][0];
+#pragma unroll
         for (int f = 0; f < NFR; ++f)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (kbase + 16 * f + 4 * g + r >= N) s[f][r] = -INFINITY;
-      }
-      float tmax = s[0][0];
+          for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[gi][f][r]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run[gi], tmax * c);  // scaled log2 units (c > 0)
+        const float alpha = __builtin_amdgcn_exp2f(m_run[gi] - m_new);
+        float psum = 0.f;
 #pragma unroll
-      for (int f = 0; f < NFR; ++f)
+        for (int f = 0; f < NFR; ++f) {
+          bool keep[4] = {true, true, true, true};
+          if constexpr (DROP) rng_keep4_32(dkey, drow[gi] + (uint32_t)(kbase + 16 * f + 4 * g), drop.thr, keep);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[f][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_run, tmax * c);  // scaled log2 units (c > 0)
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      float psum = 0.f;
-#pragma unroll
-      for (int f = 0; f < NFR; ++f) {
-        bool keep[4] = {true, true, true, true};
-        if constexpr (DROP) rng_keep4_32(dkey, drow + (uint32_t)(kbase + 16 * f + 4 * g), drop.thr, keep);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(s[f][r], c, -m_new));
-          psum += pv;  // the normaliser sums the undropped probabilities
-          if constexpr (DROP) s[f][r] = keep[r] ? pv * drop.scale : 0.f;
-          else s[f][r] = pv;
+          for (int r = 0; r < 4; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[gi][f][r], c, -m_new));
+            psum += pv;  // the normaliser sums the undropped probabilities
+            if constexpr (DROP) s[gi][f][r] = keep[r] ? pv * drop.scale : 0.f;
+            else s[gi][f][r] = pv;
+          }
         }
-      }
-      l_run = l_run * alpha + psum;
-      m_run = m_new;
+        l_run[gi] = l_run[gi] * alpha + psum;
+        m_run[gi] = m_new;
 #pragma unroll
-      for (int e = 0; e < C::NE; ++e) o[e] *= alpha;
-      // O^T[d][q] += V^T[d][key] P^T[key][q]
+        for (int e = 0; e < C::NE; ++e) o[gi][e] *= alpha;
+      }
+      // O^T[d][q] += V^T[d][key] P^T[key][q]: one V^T fragment read serves every query group
 #pragma unroll
       for (int kk = 0; kk < NFR / 2; ++kk) {
         if (kk * 2 < nf) {
@@ -144,43 +164,53 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
           v4s vlo[C::NE], vhi[C::NE];
 #pragma unroll
           for (int e = 0; e < C::NE; ++e) frag_tr_async(vimg, KT, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, vlo[e], vhi[e]);
-          const v8s pf = pack_p(s[2 * kk], s[2 * kk + 1]);
+          v8s pf[QG];
+#pragma unroll
+          for (int gi = 0; gi < QG; ++gi) pf[gi] = pack_p(s[gi][2 * kk], s[gi][2 * kk + 1]);
           lds_wait();
 #pragma unroll
-          for (int e = 0; e < C::NE; ++e) o[e] = mfma16(cat44(vlo[e], vhi[e]), pf, o[e]);
+          for (int e = 0; e < C::NE; ++e) {
+            const v8s vf = cat44(vlo[e], vhi[e]);
+            o[0][e] = mfma16(vf, pf[0], o[0][e]);
+            if (QG > 1 && g1) o[QG - 1][e] = mfma16(vf, pf[QG - 1], o[QG - 1][e]);
+          }
         }
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  const int q = q0 + li;
   float qam = 0.f;
-  if (q < N) {
-    const float inv = 1.f / l_run;
-    uint16_t* orow = out + ((int64_t)b * N + q) * ld_o + h * DH;
 #pragma unroll
-    for (int e = 0; e < C::NE; ++e) {
-      uint2 w;
-      w.x = pack2bf(o[e][0] * inv, o[e][1] * inv);
-      w.y = pack2bf(o[e][2] * inv, o[e][3] * inv);
-      *(uint2*)(orow + 16 * e + 4 * g) = w;
-    }
-    if (q8.out) {  // e4m3 copy for the fp8 out-proj GEMM
-      const float qs = *q8.qs;
-      uint8_t* qrow = q8.out + ((int64_t)b * N + q) * q8.ld + h * DH;
+  for (int gi = 0; gi < QG; ++gi) {
+    float l = l_run[gi];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const int q = q0 + 16 * gi + li;
+    if (q < N) {
+      const float inv = 1.f / l;
+      uint16_t* orow = out + ((int64_t)b * N + q) * ld_o + h * DH;
 #pragma unroll
       for (int e = 0; e < C::NE; ++e) {
-        const float v[4] = {o[e][0] * inv, o[e][1] * inv, o[e][2] * inv, o[e][3] * inv};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) qam = nan_max(qam, fabsf(v[r]));
-        *(uint32_t*)(qrow + 16 * e + 4 * g) =
-            (uint32_t)pack2_fp8<0, true>(v[2] * qs, v[3] * qs, pack2_fp8<0, false>(v[0] * qs, v[1] * qs, 0));
+        uint2 w;
+        w.x = pack2bf(o[gi][e][0] * inv, o[gi][e][1] * inv);
+        w.y = pack2bf(o[gi][e][2] * inv, o[gi][e][3] * inv);
+        *(uint2*)(orow + 16 * e + 4 * g) = w;
       }
+      if (q8.out) {  // e4m3 copy for the fp8 out-proj GEMM
+        const float qs = *q8.qs;
+        uint8_t* qrow = q8.out + ((int64_t)b * N + q) * q8.ld + h * DH;
+#pragma unroll
+        for (int e = 0; e < C::NE; ++e) {
+          const float v[4] = {o[gi][e][0] * inv, o[gi][e][1] * inv, o[gi][e][2] * inv, o[gi][e][3] * inv};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qam = nan_max(qam, fabsf(v[r]));
+          *(uint32_t*)(qrow + 16 * e + 4 * g) =
+              (uint32_t)pack2_fp8<0, true>(v[2] * qs, v[3] * qs, pack2_fp8<0, false>(v[0] * qs, v[1] * qs, 0));
+        }
+      }
+      if (g == 0) lse[(int64_t)bh * N + q] = (m_run[gi] + __log2f(l)) * LN2;
     }
-    if (g == 0) lse[(int64_t)bh * N + q] = (m_run + __log2f(l_run)) * LN2;
   }
   if (q8.out) {
     qam = wave_max_nan(qam);
@@ -1275,15 +1305,41 @@ static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t
   return hipGetLastError();
 }
 
+// Tiled forward launch: QG query groups per wave, KT keys per tile, dynamic LDS for two K/V stages.
+// round 3 form: QG 1 (64 queries per workgroup) and 32-key tiles for two-image head rows (dh > 64);
+// round 4: QG 2 (128 queries per workgroup, each K / V fragment read feeds two MFMAs) and 64-key
+// tiles at every head dim (64 KiB of LDS at dh 80: two workgroups per CU).
+int g_attn_fwd_qg = 2;
+template <int DH, bool DROP, int QG, int KT>
+static hipError_t attn_fwd_tiled(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H, int D,
+                                 float scale, const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
+  using namespace pvr;
+  constexpr int SMEM = 4 * KT * 128 * Hd<DH>::NH;
+  auto kern = attn_fwd_kernel<DH, DROP, QG, KT>;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nqb = (N + 64 * QG - 1) / (64 * QG);
+  hipLaunchKernelGGL(kern, dim3(nqb * B * H, 1), dim3(256), SMEM, s, qkv, ld, out, ld_o, lse, N, H, D, scale, drop, q8);
+  return hipGetLastError();
+}
+
+template <int DH, bool DROP>
+static hipError_t attn_fwd_tiled_pick(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
+                                      int D, float scale, const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
+  if (g_attn_fwd_qg == 2) return attn_fwd_tiled<DH, DROP, 2, 64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
+  return attn_fwd_tiled<DH, DROP, 1, (pvr::Hd<DH>::NH == 1 ? 64 : 32)>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
+}
+
 template <int DH>
 static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
                                   int D, float scale, const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
   using namespace pvr;
-  if (drop.seed) {  // attention dropout: the tiled kernel with the in-register keep mask
-    hipLaunchKernelGGL((attn_fwd_kernel<DH, true>), dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D,
-                       scale, drop, q8);
-    return hipGetLastError();
-  }
+  if (drop.seed)  // attention dropout: the tiled kernel with the in-register keep mask
+    return attn_fwd_tiled_pick<DH, true>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
   if (DH == 64 && N <= 256 && !q8.out) {
     // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take
     // up to 128 KiB of LDS), ceil(N/16) waves
@@ -1297,11 +1353,10 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
       default: break;
     }
   }
-  // 1-D grid of (B*H) x query blocks, XCD-remapped in-kernel
-  hipLaunchKernelGGL((attn_fwd_kernel<DH, false>), dim3((N + 63) / 64 * B * H, 1), dim3(256), 0, s, qkv, ld, out, ld_o, lse, N, H, D,
-                     scale, drop, q8);
-  return hipGetLastError();
+  return attn_fwd_tiled_pick<DH, false>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
 }
+
+extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg == 1 ? 1 : 2; }
 
 // seed (optional): attention-probability dropout with keep threshold thr16 (see AttnDrop); the
 // backward must get the same seed / seed_off / thr16

@@ -22,6 +22,7 @@ struct AdamGroup {
 extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
+void pvr_set_attn_fwd_qg(int qg);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
@@ -915,6 +916,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes, (int)max_units); },
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
     "K-parts of the split tail round this GEMM shape gets (0: none)");
+  m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (2 default, 1 = round-3 form; A/B)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

@@ -1,19 +1,17 @@
 #!/bin/bash
-# A/B session (round 4): bench variants interleaved, GEMM table vs hipBLASLt, peak memory.
-# Every GPU step under its own timeout; the first failure ends it.
+# A/B session (round 4): attention forward numerics + A/B, bench variants on one box, H/14 memory,
+# GPU test suite. Every GPU step under its own timeout; the first failure ends it.
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 O=gpurun_out/${1:-ab}; mkdir -p "$O"
-step() { local t=$1 log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "[$log] rc=$rc"; tail -n 1 "$O/$log" | cut -c1-200; [ $rc -eq 0 ] || exit $rc; }
-step 300 tail_check.log python -u scripts/tail_check.py
+step() { local t=$1 log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "[$log] rc=$rc"; tail -n 1 "$O/$log" | cut -c1-120; [ $rc -eq 0 ] || exit $rc; }
+step 300 attn_fwd_checks.log python -u -m pytest tests/test_gpu_kernels.py -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "numerics" -x
+step 300 attn_ab.log python -u scripts/attn_ab.py --ab fwd_qg --bwd
 for r in 1 2; do
-  step 200 b_off_$r.log python bench.py --no-gemm-tail
-  step 200 b_on_$r.log python bench.py
-  step 200 b_ser_on_$r.log python bench.py --serial-wgrad
-  step 200 b_ser_off_$r.log python bench.py --serial-wgrad --no-gemm-tail
-  step 200 b_w8_$r.log python bench.py --no-gemm-tail --side-window 8
-  step 200 b_w0_$r.log python bench.py --no-gemm-tail --side-window 0
+  step 200 b_def_$r.log python bench.py
+  step 200 b_notail_$r.log python bench.py --no-gemm-tail
+  step 200 b_hold0_$r.log python bench.py --side-hold-gb 0
 done
-step 300 h14_w0.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4 --side-window 0
-step 300 h14_w4.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4 --side-window 4
-step 300 h14_w8.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4 --side-window 8
-step 500 gemm_ab_tail.log python -u scripts/gemm_ab.py --ab tail --rounds 4
+step 300 h14_def.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4
+step 300 h14_hold0.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4 --side-hold-gb 0
+step 300 l16_def.log python bench.py --model vit_l16 --image-size 384 --batch 128 --steps 6 --warmup 3
+step 900 pytest_gpu.log python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread
