@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tile_plan.h"
+
 #define PVR_DEV __device__ __forceinline__
 
 typedef short v8s __attribute__((ext_vector_type(8)));
@@ -273,11 +275,8 @@ PVR_DEV float nan_max(float a, float b) { return (a > b || a != a) ? a : b; }
 PVR_DEV float wave_max_nan(float v) { return wave_reduce(v, nan_max); }
 
 // Bijective XCD-aware remap: blocks dealt round-robin over 8 XCDs (b, b+8 share one) are given
-// contiguous logical tile ranges so neighbouring tiles share the XCD's L2.
-PVR_DEV int xcd_remap(int bid, int nblocks) {
-  const int q = nblocks / 8, r = nblocks % 8, x = bid % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-}
+// contiguous logical tile ranges so neighbouring tiles share the XCD's L2 (csrc/tile_plan.h).
+PVR_DEV int xcd_remap(int bid, int nblocks) { return xcd_remap_c(bid, nblocks); }
 
 // Two f32 -> OCP fp8 (FMT 0 e4m3fn, 1 e5m2) into byte pair HI of `old` (v_cvt_pk_fp8 / bf8_f32):
 // finite overflow saturates; a NaN stays a NaN (fminf/fmaxf would turn it into -FMAX and hide it)

@@ -1365,19 +1365,17 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   // one whole tile each; the rest are K-parts of the tail tiles, the parts of one tile on
   // consecutive remapped ids (one XCD, so the last part reads the others' partials from its L2).
   int tt, kbeg, kend, tloc = 0, tpart = -1;
-  if (p.tail_split > 1 && (int)blockIdx.x >= p.tail_from) {
-    const int units = (ntm * ntn - p.tail_from) * p.tail_split;
-    PVR_ASSERT((int)blockIdx.x - p.tail_from < units);
-    const int u = xcd_remap((int)blockIdx.x - p.tail_from, units);
-    tloc = u / p.tail_split;
-    tpart = u % p.tail_split;
-    tt = p.tail_from + tloc;
+  const TailPlan tp{p.tail_from, p.tail_split};
+  PVR_ASSERT((int)blockIdx.x < tail_grid(tp, ntm * ntn));
+  const TailUnit tu = tail_unit_c(tp, ntm * ntn, (int)blockIdx.x);
+  tt = tu.tile;
+  if (tu.part >= 0) {
+    tpart = tu.part;
+    tloc = tt - p.tail_from;
     const int nkt = p.K / BKE;  // k-contiguous operands: K % BKE == 0 (host check)
-    kbeg = (tpart * nkt / p.tail_split) * BKE;
-    kend = ((tpart + 1) * nkt / p.tail_split) * BKE;
+    kbeg = tail_kbeg(tpart, p.tail_split, nkt) * BKE;
+    kend = tail_kbeg(tpart + 1, p.tail_split, nkt) * BKE;
   } else {
-    PVR_ASSERT((int)blockIdx.x < (p.tail_split > 1 ? p.tail_from : ntm * ntn));
-    tt = xcd_remap(blockIdx.x, p.tail_split > 1 ? p.tail_from : ntm * ntn);
     kbeg = blockIdx.z * p.k_split_len;
     kend = min(p.K, kbeg + p.k_split_len);
   }
@@ -1509,21 +1507,9 @@ void plan_tail(GemmParams& q, int ntiles, int bke) {
   q.tail_from = 0;
   q.tail_split = 0;
   if (!q.tail_ws || !q.tail_cnt) return;
-  const int cus = device_cus();
-  const int rem = ntiles % cus;
-  if (ntiles < cus || rem == 0) return;
-  int S = cus / rem;
-  S = S < 4 ? S : 4;
-  const int nkt = q.K / bke;
-  while (S > 1 && nkt / S < 12) --S;
-  if (S < 2) return;
-  if (q.tail_max_units > 0) {
-    while (S > 1 && rem * S > q.tail_max_units) --S;
-    if (S < 2) return;
-  }
-  if ((int64_t)rem * S * 65536 > q.tail_ws_elems || rem > q.tail_cnt_elems) return;
-  q.tail_from = ntiles - rem;
-  q.tail_split = S;
+  const TailPlan t = plan_tail_c(ntiles, q.K / bke, device_cus(), q.tail_ws_elems, q.tail_cnt_elems, q.tail_max_units);
+  q.tail_from = t.from;
+  q.tail_split = t.split;
 }
 
 template <bool AK, bool BKC, bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
@@ -1544,7 +1530,7 @@ hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
   if constexpr (AK && BKC && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
     if (nsplit == 1) {
       plan_tail(q, ntm * ntn, 128 / ES);
-      if (q.tail_split > 1) grid = q.tail_from + (ntm * ntn - q.tail_from) * q.tail_split;
+      grid = tail_grid(TailPlan{q.tail_from, q.tail_split}, ntm * ntn);
     }
   }
   hipLaunchKernelGGL(kern, dim3(grid, 1, nsplit), dim3(512), SMEM, s, q);

@@ -1,0 +1,93 @@
+// Host checks of the GEMM grid planning (csrc/tile_plan.h) that the gfx950 kernels run on the device:
+// the XCD remap is a bijection for every grid size, a split-tail launch covers every output tile
+// exactly once (whole, or as all of its K-parts over disjoint K ranges that cover [0, K)), and the
+// planner respects its rules (parts >= 12 K-tiles, <= 4 parts, the CU / unit / workspace bounds).
+// Built and run by tests/test_tile_plan_cpp.py with -fsanitize=address,undefined.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../pytorch_vit_paper_replication_amd/csrc/tile_plan.h"
+
+using namespace pvr;
+
+static int failures = 0;
+#define CHECK(c)                                                              \
+  do {                                                                        \
+    if (!(c)) {                                                               \
+      std::fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #c); \
+      ++failures;                                                             \
+    }                                                                         \
+  } while (0)
+
+static_assert(xcd_remap_c(0, 1) == 0, "trivial grid");
+static_assert(plan_tail_c(591, 48, 256, 256ll * 65536, 256, 0).split == 3, "ViT-B/16 fc2 forward: 3 K-parts");
+static_assert(plan_tail_c(591, 12, 256, 256ll * 65536, 256, 0).split == 0, "K = 768: no split");
+static_assert(plan_tail_c(591, 48, 256, 256ll * 65536, 256, 64).split == 0, "backward limit: 79 tiles x 2 > 64");
+
+static void check_remap(int n) {
+  std::vector<int> seen(n, 0);
+  for (int b = 0; b < n; ++b) {
+    const int t = xcd_remap_c(b, n);
+    CHECK(t >= 0 && t < n);
+    if (t >= 0 && t < n) ++seen[t];
+  }
+  for (int t = 0; t < n; ++t) CHECK(seen[t] == 1);
+}
+
+static void check_plan(int ntiles, int nkt, int cus, int max_units) {
+  const long long ws = (long long)cus * 65536;
+  const TailPlan p = plan_tail_c(ntiles, nkt, cus, ws, cus, max_units);
+  if (p.split == 0) {
+    CHECK(p.from == 0);
+  } else {
+    const int rem = ntiles - p.from;
+    CHECK(p.split >= 2 && p.split <= 4);
+    CHECK(nkt / p.split >= 12);
+    CHECK(rem > 0 && rem < cus && p.from % cus == 0);
+    CHECK(rem * p.split <= cus);
+    CHECK(max_units <= 0 || rem * p.split <= max_units);
+    CHECK((long long)rem * p.split * 65536 <= ws);
+  }
+  // coverage: every tile whole exactly once, or split into parts that tile [0, nkt) exactly
+  const int grid = tail_grid(p, ntiles);
+  std::vector<int> whole(ntiles, 0);
+  std::vector<std::vector<int>> parts(ntiles);
+  for (int b = 0; b < grid; ++b) {
+    const TailUnit u = tail_unit_c(p, ntiles, b);
+    CHECK(u.tile >= 0 && u.tile < ntiles);
+    if (u.tile < 0 || u.tile >= ntiles) continue;
+    if (u.part < 0) {
+      ++whole[u.tile];
+    } else {
+      CHECK(u.part < p.split);
+      parts[u.tile].push_back(u.part);
+    }
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    if (p.split > 1 && t >= p.from) {
+      CHECK(whole[t] == 0 && (int)parts[t].size() == p.split);
+      std::vector<int> cov(nkt, 0);
+      for (int part : parts[t])
+        for (int k = tail_kbeg(part, p.split, nkt); k < tail_kbeg(part + 1, p.split, nkt); ++k) ++cov[k];
+      for (int k = 0; k < nkt; ++k) CHECK(cov[k] == 1);
+    } else {
+      CHECK(whole[t] == 1 && parts[t].empty());
+    }
+  }
+}
+
+int main() {
+  for (int n = 1; n <= 5000; n += (n < 300 ? 1 : 37)) check_remap(n);
+  const int shapes[][2] = {{591, 48}, {591, 12}, {591, 36}, {2364, 48}, {2364, 12}, {1285, 40}, {1285, 30}, {1773, 12},
+                           {588, 48}, {5140, 10}, {257, 48}, {255, 48}, {512, 48}, {1000, 100}};
+  for (const auto& s : shapes)
+    for (int cus : {256, 304, 80})
+      for (int lim : {0, 64}) check_plan(s[0], s[1], cus, lim);
+  if (failures) {
+    std::fprintf(stderr, "%d failures\n", failures);
+    return 1;
+  }
+  std::printf("tile plan: all checks passed\n");
+  return 0;
+}
