@@ -28,7 +28,8 @@ hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const fl
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, uint8_t*, int64_t, const float*, unsigned*, int, int, hipStream_t);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
-hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, hipStream_t);
+hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, int, int, hipStream_t);
+hipError_t pvr_pad_cols_bf16(const uint16_t*, int, int, uint16_t*, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t,
                       const float*, unsigned*, hipStream_t);
@@ -48,10 +49,11 @@ hipError_t pvr_zero_f32(float*, int64_t, hipStream_t);
 hipError_t pvr_xent(const float*, int64_t, const int64_t*, int, int, float*, float*, int*, float, hipStream_t);
 int pvr_norm_partial_blocks();
 hipError_t pvr_grad_norm(const float*, int64_t, float, float*, float*, hipStream_t);
-hipError_t pvr_adam(float*, const float*, float*, float*, uint16_t*, int64_t, const int64_t*, const int*, int, const pvr::AdamGroup*, const float*, int, hipStream_t);
+hipError_t pvr_adam(float*, const float*, float*, float*, uint16_t*, int64_t, const int64_t*, const int*, int, const pvr::AdamGroup*,
+                    const pvr::AdamGroup*, int, const float*, int, hipStream_t);
 hipError_t pvr_scale_by_clip(float*, int64_t, const float*, hipStream_t);
 hipError_t pvr_adam_t(float*, const float*, float*, float*, uint16_t*, uint16_t*, const int64_t*, int, int, const int64_t*, int, int64_t,
-                      const pvr::AdamGroup*, const float*, int, hipStream_t);
+                      const pvr::AdamGroup*, const pvr::AdamGroup*, int, const float*, int, hipStream_t);
 hipError_t pvr_fp8_quant(const uint16_t*, int64_t, uint8_t*, int64_t, int64_t, int, const float*, unsigned*, int, hipStream_t);
 hipError_t pvr_fp8_dequant(const uint8_t*, float*, int64_t, const float*, int, hipStream_t);
 hipError_t pvr_fp8_scale_update(float*, int, unsigned*, float*, float*, const float*, int, int, float, hipStream_t);
@@ -313,12 +315,27 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
 }
 
 // out (+)= ws.sum(0) for a split-K workspace ws [S, rows, cols] (out: contiguous [rows, cols])
+// out (+)= ws[:S].sum(0) for ws [S, rows, wcols]; out [rows, ocols] contiguous with ocols <= wcols
+// (the leading columns of each workspace row: a K-padded weight gradient reduced into the unpadded one)
 void splitk_reduce(torch::Tensor ws, int64_t S, torch::Tensor out, bool accumulate) {
   TORCH_CHECK(ws.dim() == 3 && ws.size(0) >= S && S >= 1, "splitk_reduce: ws must be [S, rows, cols]");
-  TORCH_CHECK(out.is_contiguous() && ws.stride(2) == 1 && ws.stride(1) == ws.size(2) && out.numel() == ws.size(1) * ws.size(2),
-              "splitk_reduce: layouts");
-  check(pvr_splitk_reduce(f32(ws, "ws"), (int)S, ws.stride(0), f32_mut(out, "out"), out.numel(), accumulate ? 1 : 0, stream()),
+  TORCH_CHECK(out.is_contiguous() && ws.stride(2) == 1 && ws.stride(1) == ws.size(2), "splitk_reduce: layouts");
+  const int64_t rows = ws.size(1), wcols = ws.size(2);
+  TORCH_CHECK(out.numel() % rows == 0, "splitk_reduce: out must hold [rows, ocols]");
+  const int64_t ocols = out.numel() / rows;
+  TORCH_CHECK(ocols <= wcols && ocols % 4 == 0 && wcols % 4 == 0, "splitk_reduce: out columns must be a 4-aligned prefix of ws columns");
+  check(pvr_splitk_reduce(f32(ws, "ws"), (int)S, ws.stride(0), f32_mut(out, "out"), out.numel(), (int)ocols, (int)wcols,
+                          accumulate ? 1 : 0, stream()),
         "splitk_reduce");
+}
+
+// dst [rows, ld] bf16 = src [rows, cols] zero-padded on the right (cols, ld % 4 == 0)
+void pad_cols_bf16(torch::Tensor src, torch::Tensor dst) {
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && src.dim() == 2 && dst.dim() == 2 && src.size(0) == dst.size(0) &&
+                  src.size(1) <= dst.size(1) && src.size(1) % 4 == 0 && dst.size(1) % 4 == 0,
+              "pad_cols_bf16: src [rows, cols], dst [rows, ld >= cols], contiguous, 4-aligned");
+  check(pvr_pad_cols_bf16(bf(src, "src"), (int)src.size(0), (int)src.size(1), bf_mut(dst, "dst"), (int)dst.size(1), stream()),
+        "pad_cols_bf16");
 }
 
 // out = bf16(epilogue(ws.sum(0))) for a split-K workspace ws [S, M, N]: + bias, GELU (inference: no
@@ -458,16 +475,38 @@ void grad_norm(torch::Tensor g, double max_norm, torch::Tensor workspace, torch:
   check(pvr_grad_norm(f32(g, "g"), g.numel(), (float)max_norm, f32_mut(workspace, "ws"), f32_mut(out, "out"), stream()), "grad_norm");
 }
 
+// Param-group table float32 [G][8] (csrc/optim.hip AdamGroup): a CUDA tensor is read by the kernel
+// (graph-captured steps); a CPU tensor is copied into the launch's kernel arguments (G <= 8), so an
+// eager step needs no host-to-device copy of its per-step lr / bias corrections.
+struct GroupTable {
+  const pvr::AdamGroup* dev = nullptr;
+  const pvr::AdamGroup* host = nullptr;
+  int n = 0;
+};
+GroupTable group_table(const torch::Tensor& groups, const char* who) {
+  TORCH_CHECK(groups.scalar_type() == torch::kFloat32 && groups.dim() == 2 && groups.size(1) == 8 && groups.is_contiguous(), who,
+              ": groups must be contiguous float32 [G, 8]");
+  GroupTable t;
+  t.n = (int)groups.size(0);
+  auto* ptr = reinterpret_cast<const pvr::AdamGroup*>(groups.data_ptr<float>());
+  if (groups.is_cuda()) {
+    t.dev = ptr;
+  } else {
+    TORCH_CHECK(t.n >= 1 && t.n <= 8, who, ": a host group table holds 1..8 groups (pass a device table for more)");
+    t.host = ptr;
+  }
+  return t;
+}
+
 void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> shadow, torch::Tensor seg_start,
           torch::Tensor seg_group, torch::Tensor groups, c10::optional<torch::Tensor> clip, bool skip_nonfinite) {
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam: size mismatch");
-  TORCH_CHECK(groups.scalar_type() == torch::kFloat32 && groups.size(-1) == 8, "adam: groups must be float32 [G, 8]");
+  const GroupTable gt = group_table(groups, "adam");
   TORCH_CHECK(seg_start.scalar_type() == torch::kInt64 && seg_group.scalar_type() == torch::kInt32, "adam: segment table dtypes");
   uint16_t* sh = nullptr;
   if (shadow.has_value() && shadow->defined()) sh = const_cast<uint16_t*>(bf(*shadow, "shadow"));
   check(pvr_adam(f32_mut(p, "p"), f32(g, "g"), f32_mut(m, "m"), f32_mut(v, "v"), sh, p.numel(), seg_start.data_ptr<int64_t>(),
-                 seg_group.data_ptr<int>(), (int)seg_start.numel(), reinterpret_cast<const pvr::AdamGroup*>(groups.data_ptr<float>()),
-                 opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0, stream()),
+                 seg_group.data_ptr<int>(), (int)seg_start.numel(), gt.dev, gt.host, gt.n, opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0, stream()),
         "adam");
 }
 
@@ -479,7 +518,7 @@ void adam_t(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, 
             c10::optional<torch::Tensor> clip, bool skip_nonfinite) {
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel() && shadow.numel() == p.numel(),
               "adam_t: size mismatch");
-  TORCH_CHECK(groups.scalar_type() == torch::kFloat32 && groups.size(-1) == 8, "adam_t: groups must be float32 [G, 8]");
+  const GroupTable gt = group_table(groups, "adam_t");
   TORCH_CHECK(tmeta.is_cuda() && tmeta.scalar_type() == torch::kInt64 && tmeta.dim() == 2 && tmeta.size(1) == 6 && tmeta.is_contiguous(),
               "adam_t: tmeta int64 [n][6]");
   TORCH_CHECK(fmeta.is_cuda() && fmeta.scalar_type() == torch::kInt64 && fmeta.dim() == 2 && fmeta.size(1) == 4 && fmeta.is_contiguous(),
@@ -489,7 +528,7 @@ void adam_t(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, 
               "adam_t: contiguous buffers");
   check(pvr_adam_t(f32_mut(p, "p"), f32(g, "g"), f32_mut(m, "m"), f32_mut(v, "v"), bf_mut(shadow, "shadow"), bf_mut(shadow_t, "shadow_t"),
                    tmeta.data_ptr<int64_t>(), (int)tmeta.size(0), (int)ntiles, fmeta.data_ptr<int64_t>(), (int)fmeta.size(0), flat4,
-                   reinterpret_cast<const pvr::AdamGroup*>(groups.data_ptr<float>()), opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0,
+                   gt.dev, gt.host, gt.n, opt_ptr<const float>(clip), skip_nonfinite ? 1 : 0,
                    stream()),
         "adam_t");
 }
@@ -916,7 +955,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes, (int)max_units); },
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
     "K-parts of the split tail round this GEMM shape gets (0: none)");
-  m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (2 default, 1 = round-3 form; A/B)");
+  m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),
@@ -938,6 +977,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd_bias_rows", &attn_bwd_bias_rows, py::arg("B"), py::arg("N"), py::arg("H"), py::arg("D"), py::arg("drop") = false);
   m.def("attn_dbias_reduce", &attn_dbias_reduce);
   m.def("splitk_reduce", &splitk_reduce);
+  m.def("pad_cols_bf16", &pad_cols_bf16);
   m.def("transpose_batched", &transpose_batched);
   m.def("colsum", &colsum, py::arg("dy"), py::arg("rows"), py::arg("N"), py::arg("db"), py::arg("dz"), py::arg("seed"),
         py::arg("seed_offset"), py::arg("drop_p"), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),

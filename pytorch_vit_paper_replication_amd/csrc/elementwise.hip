@@ -335,13 +335,18 @@ __global__ void __launch_bounds__(256) transpose_batched_kernel(const uint16_t* 
   }
 }
 
-// out (+)= sum over S split-K partial slices ws[s][i] (i < n, n % 4 == 0): the second half of the
-// store-then-reduce wgrad (tile 14); fixed slice order, so the result is deterministic
+// out (+)= sum over S split-K partial slices ws[s] (the second half of the store-then-reduce wgrad,
+// tile 14); fixed slice order, so the result is deterministic. ws rows hold wcols floats, out rows
+// the first ocols of them (ocols <= wcols, both % 4 == 0): a GEMM over a K padded to the tile width
+// reduces straight into the unpadded weight gradient.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int S, int64_t stride,
-                                                            float* __restrict__ out, int64_t n4, int accumulate) {
+                                                            float* __restrict__ out, int64_t n4, int ocols, int wcols,
+                                                            int accumulate) {
+  const int oc4 = ocols / 4;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 a = accumulate ? ((const float4*)out)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* src = ws + 4 * i;
+    const int64_t row = i / oc4;
+    const float* src = ws + row * wcols + 4 * (i - row * oc4);
     int s = 0;
     for (; s + 4 <= S; s += 4) {  // 4 independent loads in flight per trip
       const float4 b0 = *(const float4*)(src + (int64_t)s * stride);
@@ -361,16 +366,43 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// dst[r][c] = c < cols ? src[r][c] : 0 for c < ld_dst (bf16; cols, ld_dst % 4 == 0): the patch
+// embedding's conv weight [D][C*P*P] zero-padded to the GEMM's K tile
+__global__ void __launch_bounds__(256) pad_cols_bf16_kernel(const uint16_t* __restrict__ src, int rows, int cols,
+                                                            uint16_t* __restrict__ dst, int ld_dst) {
+  const int q = ld_dst / 4;
+  const int64_t n4 = (int64_t)rows * q;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / q;
+    const int c = 4 * (int)(i - r * q);
+    uint2 v = make_uint2(0u, 0u);
+    if (c < cols) v = *(const uint2*)(src + r * cols + c);
+    *(uint2*)(dst + r * ld_dst + c) = v;
+  }
+}
+
 }  // namespace
 }  // namespace pvr
 
-extern "C" hipError_t pvr_splitk_reduce(const float* ws, int S, int64_t stride, float* out, int64_t n, int accumulate, hipStream_t s) {
+extern "C" hipError_t pvr_splitk_reduce(const float* ws, int S, int64_t stride, float* out, int64_t n, int ocols, int wcols,
+                                        int accumulate, hipStream_t s) {
   using namespace pvr;
   if (n <= 0) return hipSuccess;
-  if (n % 4 || stride % 4) return hipErrorInvalidValue;
+  if (n % 4 || stride % 4 || ocols <= 0 || ocols % 4 || wcols % 4 || ocols > wcols || n % ocols) return hipErrorInvalidValue;
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, S, stride, out, n / 4, accumulate);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, S, stride, out, n / 4, ocols, wcols,
+                     accumulate);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pvr_pad_cols_bf16(const uint16_t* src, int rows, int cols, uint16_t* dst, int ld_dst, hipStream_t s) {
+  using namespace pvr;
+  if (rows <= 0) return hipSuccess;
+  if (cols % 4 || ld_dst % 4 || cols > ld_dst) return hipErrorInvalidValue;
+  int64_t blocks = ((int64_t)rows * (ld_dst / 4) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(pad_cols_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, cols, dst, ld_dst);
   return hipGetLastError();
 }
 

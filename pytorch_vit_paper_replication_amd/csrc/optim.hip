@@ -16,6 +16,13 @@ struct AdamGroup {
   int decoupled;
 };
 
+// Group table passed by value in the kernel arguments (eager stepping: no per-step host-to-device
+// copy); graph-captured steps pass a device table instead (kernel arguments are frozen at capture).
+constexpr int MAX_ARG_GROUPS = 8;
+struct AdamGroupArgs {
+  AdamGroup g[MAX_ARG_GROUPS];
+};
+
 namespace {
 
 constexpr int NORM_BLOCKS = 1024;
@@ -62,8 +69,8 @@ __global__ void __launch_bounds__(256) norm_finalize_kernel(const float* __restr
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                                     float* __restrict__ v, uint16_t* __restrict__ shadow, int64_t n,
                                                     const int64_t* __restrict__ seg_start, const int* __restrict__ seg_group, int nseg,
-                                                    const AdamGroup* __restrict__ groups, const float* __restrict__ clip,
-                                                    int skip_nonfinite) {
+                                                    const AdamGroup* __restrict__ groups, AdamGroupArgs garg,
+                                                    const float* __restrict__ clip, int skip_nonfinite) {
   const float gscale = clip ? clip[1] : 1.f;
   if (clip && skip_nonfinite && clip[2] != 0.f) return;
   const int64_t n4 = n / 4;
@@ -77,7 +84,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
     }
     const int gi = seg_group[lo];
     if (gi < 0) continue;  // frozen / padding
-    const AdamGroup G = groups[gi];
+    const AdamGroup G = groups ? groups[gi] : garg.g[gi];
     float4 pp = ((float4*)p)[i];
     const float4 gg4 = ((const float4*)g)[i];
     float4 mm = ((float4*)m)[i];
@@ -139,8 +146,8 @@ __global__ void __launch_bounds__(256) adam_t_kernel(float* __restrict__ p, cons
                                                       float* __restrict__ v, uint16_t* __restrict__ shadow, uint16_t* __restrict__ shadow_t,
                                                       const int64_t* __restrict__ tmeta, int nmat, int ntiles,
                                                       const int64_t* __restrict__ fmeta, int nflat, int64_t flat4,
-                                                      const AdamGroup* __restrict__ groups, const float* __restrict__ clip,
-                                                      int skip_nonfinite) {
+                                                      const AdamGroup* __restrict__ groups, AdamGroupArgs garg,
+                                                      const float* __restrict__ clip, int skip_nonfinite) {
   const float gscale = clip ? clip[1] : 1.f;
   if (clip && skip_nonfinite && clip[2] != 0.f) return;
   const int tid = threadIdx.x;
@@ -159,7 +166,7 @@ __global__ void __launch_bounds__(256) adam_t_kernel(float* __restrict__ p, cons
     const int tc = C / 64;
     const int r0 = (local / tc) * 64, c0 = (local % tc) * 64;
     if (gi < 0) return;  // frozen: master, shadow and W^T unchanged
-    const AdamGroup G = groups[gi];
+    const AdamGroup G = groups ? groups[gi] : garg.g[gi];
     const int cq = (tid & 15) * 4;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -202,7 +209,7 @@ __global__ void __launch_bounds__(256) adam_t_kernel(float* __restrict__ p, cons
     const int gi = (int)fmeta[lo * 4 + 2];
     if (gi < 0) continue;
     const int64_t e = fmeta[lo * 4 + 0] + (i - fmeta[lo * 4 + 3]) * 4;
-    const AdamGroup G = groups[gi];
+    const AdamGroup G = groups ? groups[gi] : garg.g[gi];
     float4 pp = *(float4*)(p + e);
     const float4 gg4 = *(const float4*)(g + e);
     float4 mm = *(float4*)(m + e);
@@ -220,6 +227,13 @@ __global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ g, int64
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) g[i] *= c;
 }
 
+// host: copy a [ngroups] table into the by-value kernel argument (false: too many groups)
+bool adam_group_args(const AdamGroup* host, int ngroups, AdamGroupArgs& out) {
+  if (!host || ngroups <= 0 || ngroups > MAX_ARG_GROUPS) return false;
+  for (int i = 0; i < ngroups; ++i) out.g[i] = host[i];
+  return true;
+}
+
 }  // namespace
 }  // namespace pvr
 
@@ -235,14 +249,17 @@ extern "C" hipError_t pvr_grad_norm(const float* g, int64_t n, float max_norm, f
 
 extern "C" hipError_t pvr_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, int64_t n,
                                const int64_t* seg_start, const int* seg_group, int nseg, const pvr::AdamGroup* groups,
-                               const float* clip, int skip_nonfinite, hipStream_t s) {
+                               const pvr::AdamGroup* host_groups, int ngroups, const float* clip, int skip_nonfinite,
+                               hipStream_t s) {
   using namespace pvr;
   if (n <= 0) return hipSuccess;
   if (n % 4 != 0) return hipErrorInvalidValue;
+  AdamGroupArgs ga{};
+  if (!groups && !adam_group_args(host_groups, ngroups, ga)) return hipErrorInvalidValue;
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, shadow, n, seg_start, seg_group, nseg,
-                     groups, clip, skip_nonfinite);
+                     groups, ga, clip, skip_nonfinite);
   return hipGetLastError();
 }
 
@@ -259,13 +276,16 @@ extern "C" hipError_t pvr_scale_by_clip(float* g, int64_t n, const float* clip, 
 // (see the kernel), flat4 = float4s covered by fmeta.
 extern "C" hipError_t pvr_adam_t(float* p, const float* g, float* m, float* v, uint16_t* shadow, uint16_t* shadow_t,
                                  const int64_t* tmeta, int nmat, int ntiles, const int64_t* fmeta, int nflat, int64_t flat4,
-                                 const pvr::AdamGroup* groups, const float* clip, int skip_nonfinite, hipStream_t s) {
+                                 const pvr::AdamGroup* groups, const pvr::AdamGroup* host_groups, int ngroups,
+                                 const float* clip, int skip_nonfinite, hipStream_t s) {
   using namespace pvr;
   if (nmat <= 0 || ntiles <= 0 || nflat <= 0) return hipErrorInvalidValue;
+  AdamGroupArgs ga{};
+  if (!groups && !adam_group_args(host_groups, ngroups, ga)) return hipErrorInvalidValue;
   int64_t fb = (flat4 + 255) / 256;
   if (fb > 1024) fb = 1024;
   if (fb < 1) fb = 1;
   hipLaunchKernelGGL(adam_t_kernel, dim3((unsigned)(ntiles + fb)), dim3(256), 0, s, p, g, m, v, shadow, shadow_t, tmeta, nmat,
-                     ntiles, fmeta, nflat, flat4, groups, clip, skip_nonfinite);
+                     ntiles, fmeta, nflat, flat4, groups, ga, clip, skip_nonfinite);
   return hipGetLastError();
 }

@@ -53,7 +53,9 @@ class PatchEmbedFn(torch.autograd.Function):
         ext.im2col(img, patches, patch, kp)
         w16 = store.bf16(conv_w).reshape(D, kc)
         if kp != kc:
-            w16 = F.pad(w16, (0, kp - kc))
+            w16p = torch.empty(D, kp, dtype=torch.bfloat16, device=img.device)
+            ext.pad_cols_bf16(w16, w16p)
+            w16 = w16p
         tokens = torch.empty(B * ntok, D, dtype=torch.bfloat16, device=img.device)
         drop = site_drop(seed, 0, p_drop, training)
         gemm.linear_fwd(patches, w16, conv_b, addend=pos.reshape(ntok, D), addend_period=ntok,
@@ -78,13 +80,8 @@ class PatchEmbedFn(torch.autograd.Function):
         dseed, doff, dp = gemm._drop_args(drop)
         ext.patch_bwd(dtokens, B, ntok, D, None if gpos is None else gpos.view(-1),
                       None if gcls is None else gcls.view(-1), dconv, gb, dseed, doff, dp)
-        if gw is not None:
-            if kp == kc:
-                gemm.linear_wgrad(dconv, patches, gw.view(D, kc))
-            else:
-                tmp = torch.zeros(D, kp, dtype=torch.float32, device=dtokens.device)
-                gemm.linear_wgrad(dconv, patches, tmp)
-                gw.view(D, kc).add_(tmp[:, :kc])
+        if gw is not None:  # K padded to kp in patches; the reduction writes the first kc columns
+            gemm.linear_wgrad(dconv, patches, gw.view(D, kc))
         store.grad_ready([conv_w, conv_b, cls, pos])
         return (None,) * 10
 
@@ -297,13 +294,18 @@ class EncoderBlockFn(torch.autograd.Function):
                 if f8d is not None:
                     pre_q[0] = own.dz2_q
                 own.dz2_q = None
-        elif drop2 is not None:
-            dz2 = torch.empty_like(dx2)
-            gemm.bias_grad(dx2, g(b2), drop=drop2, dz=dz2)
         else:
-            dz2 = dx2
-            if b2.requires_grad:
-                gemm.bias_grad(dx2, g(b2))
+            # last block: the column-sum pass that reduces d(b2) (and applies the fc2 dropout) also
+            # writes dz2's e5m2 copy for the fp8 fc2 dgrad once that slot is calibrated
+            prod = f8d[0].grad_producer(f8d[1], 0) if f8d is not None and store.bf16_t(w2) is not None else None
+            if drop2 is not None:
+                dz2 = torch.empty_like(dx2)
+                r = gemm.bias_grad(dx2, g(b2), drop=drop2, dz=dz2, quant=prod)
+            else:
+                dz2 = dx2
+                r = gemm.bias_grad(dx2, g(b2), quant=prod) if (b2.requires_grad or prod is not None) else None
+            if prod is not None:
+                pre_q[0] = r
         # dU = (dz2 . W2) * mask*scale*gelu'(u), with d(b1) = colsum(dU) reduced in the same epilogue
         gb1 = g(b1)
         gw2, gw1 = g(w2), g(w1)

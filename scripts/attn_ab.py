@@ -61,7 +61,7 @@ def main():
                 res.setdefault((name, "fwd", vn), []).append(timeit(lambda: ext.attn_fwd(qkv, B, N, H, dh ** -0.5)))
             if a.bwd:
                 res.setdefault((name, "bwd", ""), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
-    ext.set_attn_fwd_qg(2)
+    ext.set_attn_fwd_qg(0)
     for name in a.shapes.split(","):
         B, N, H, dh = SHAPES[name]
         fl = 4.0 * B * H * N * N * dh

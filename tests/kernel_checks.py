@@ -368,6 +368,27 @@ def check_patch_bwd(B, ntok, D, p=0.1):
     return (f"patch_bwd B{B} ntok{ntok} D{D} p{p}", m, {"sums_l2": 5e-6, "sums_max": 2e-5, "dconv_l2": 3.5e-3, "dconv_max": 7e-3})
 
 
+def check_patch_wgrad_narrow(T, D=1280, kc=588):
+    """Patch-embedding weight gradient with K padded to the tile (kc = C*P*P -> kp): the split-K
+    reduction writes the first kc columns straight into the [D, kc] gradient (accumulating), and
+    pad_cols_bf16 builds the zero-padded bf16 weight the forward GEMM reads."""
+    ext = _ext.ext()
+    kp = (kc + 63) // 64 * 64
+    dy = bf(rnd(T, D))
+    x = bf(F.pad(rnd(T, kc), (0, kp - kc)))
+    g0 = rnd(D, kc)
+    gw = g0.clone()
+    G.linear_wgrad(dy, x, gw)
+    ref = g0 + dy.float().t() @ x[:, :kc].float()
+    w = bf(rnd(D, kc))
+    wp = torch.full((D, kp), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ext.pad_cols_bf16(w, wp)
+    pad_ok = torch.equal(wp[:, :kc], w) and bool((wp[:, kc:] == 0).all())
+    m = worst((gw, ref))
+    m["pad_wrong"] = float(not pad_ok)
+    return (f"patch wgrad narrow T{T} D{D} kc{kc}->kp{kp}", m, lim(1e-6, 4e-6, pad_wrong=0))
+
+
 def check_transpose_batched():
     ext = _ext.ext()
     shapes = [(128, 192), (100, 70), (768, 2304)]
@@ -1355,6 +1376,8 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_im2col(2, 3, 56, 14),
         lambda: check_patch_bwd(37, 197, 768),
         lambda: check_patch_bwd(5, 17, 1280, 0.0),
+        lambda: check_patch_wgrad_narrow(8192),  # tile-12 split-K store + narrow reduction
+        lambda: check_patch_wgrad_narrow(512, 256, 300),  # atomic path (temporary + narrow add)
         check_transpose_batched,
         lambda: check_layernorm(394, 768),
         lambda: check_layernorm(100, 1024),
