@@ -32,7 +32,7 @@ namespace {
 // the per-tile fixed costs (barrier, DMA issue, fragment address math) are shared by 32 queries.
 // KT keys per tile; the dynamic LDS holds two stages of K and V images (4 x KT x 128 x NH bytes).
 template <int DH, bool DROP, int QG, int KT>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) attn_fwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld, uint16_t* __restrict__ out,
                                                         int64_t ld_o, float* __restrict__ lse, int N, int H, int D, float scale,
                                                         AttnDrop drop, AttnQ8 q8) {
   using C = Hd<DH>;
@@ -70,26 +70,50 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
   uint32_t dkey = 0, drow[QG];  // dropout: the pair's hash key, this lane's query row start idx
   if constexpr (DROP) dkey = attn_drop_key(drop, bh);
 #pragma unroll
-  for (int gi = 0; gi < QG; ++gi) {
-    m_run[gi] = -INFINITY;
-    l_run[gi] = 0.f;
-    drow[gi] = DROP ? (uint32_t)min(q0 + 16 * gi + li, N - 1) * (uint32_t)((N + 3) & ~3) : 0u;
-  }
+  for (int gi = 0; gi < QG; ++gi) drow[gi] = DROP ? (uint32_t)min(q0 + 16 * gi + li, N - 1) * (uint32_t)((N + 3) & ~3) : 0u;
+  // The LAST key (N - 1) starts the online softmax instead of running through the tiles: ViT's
+  // N = 64k + 1 (the CLS token: 257 at 224/14, 577 at 384/16) then streams exactly k full 64-key
+  // tiles (no masked tail tile, no 1-key tile). Per query: s = q . k_last from the Q fragments
+  // (8 dims per lane, reduced over the 4 lane groups), m = s * c, l = 1 (counted on lane group 0),
+  // O^T = v_last (times the keep mask / scale with dropout).
+  const int NL = N - 1;  // keys through the tiles
+  const uint16_t* klast = base + (int64_t)NL * ld + D + h * DH;
   v4f o[QG][C::NE];
+  {
+    v8s kl[C::KS];
 #pragma unroll
-  for (int gi = 0; gi < QG; ++gi)
+    for (int ks = 0; ks < C::KS; ++ks) kl[ks] = load_frag<DH>(klast, ks * 32 + 8 * g);
+    uint2 vl[C::NE];
 #pragma unroll
-    for (int e = 0; e < C::NE; ++e) o[gi][e] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < C::NE; ++e) vl[e] = *(const uint2*)(klast + D + 16 * e + 4 * g);
+#pragma unroll
+    for (int gi = 0; gi < QG; ++gi) {
+      float sl = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < C::KS; ++ks) sl = dot8_bf16(qf[gi][ks], kl[ks], sl);
+      sl += __shfl_xor(sl, 16, 64);
+      sl += __shfl_xor(sl, 32, 64);
+      m_run[gi] = sl * c;
+      l_run[gi] = g == 0 ? 1.f : 0.f;
+      float pk = 1.f;
+      if constexpr (DROP) pk = attn_keep1(dkey, drow[gi] + (uint32_t)NL, drop.thr) ? drop.scale : 0.f;
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e)
+        o[gi][e] = v4f{bf2f(vl[e].x & 0xFFFF) * pk, bf2f(vl[e].x >> 16) * pk, bf2f(vl[e].y & 0xFFFF) * pk, bf2f(vl[e].y >> 16) * pk};
+    }
+  }
 
-  const int ntiles = (N + KT - 1) / KT;
-  dma_rows<C::NH>(krs, smem, KT, ld, 0, wave, 4, lane);
-  dma_rows<C::NH>(vrs, smem + TILE_BYTES, KT, ld, 0, wave, 4, lane);
+  const int ntiles = (NL + KT - 1) / KT;
+  if (ntiles > 0) {
+    dma_rows<C::NH>(krs, smem, KT, ld, 0, wave, 4, lane);
+    dma_rows<C::NH>(vrs, smem + TILE_BYTES, KT, ld, 0, wave, 4, lane);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // Waves whose queries all lie past N only help stage K/V (no math), as do a wave's groups past N
   // (QG = 2); the running max is kept in scaled log2 units so a score costs max + fma + exp + add;
-  // keys past N exist only in the last tile, whose all-invalid 16-key fragments are skipped outright.
+  // keys past NL exist only in the last tile, whose all-invalid 16-key fragments are skipped outright.
   const bool active = q0 < N;
   const bool g1 = QG > 1 && q0 + 16 < N;  // second group holds a valid query (uniform)
   for (int t = 0; t < ntiles; ++t) {
@@ -102,7 +126,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
     }
     if (active) {
       const int kbase = t * KT;
-      const int nf = min(NFR, (N - kbase + 15) >> 4);  // 16-key fragments holding a valid key (uniform)
+      const int nf = min(NFR, (NL - kbase + 15) >> 4);  // 16-key fragments holding a tile key (uniform)
       // S^T[key][q] for the key fragments: one K fragment read serves every query group
       v4f s[QG][NFR];
 #pragma unroll
@@ -118,14 +142,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const uint16_t* __restric
           }
         }
       }
-      if (kbase + KT > N) {  // tail tile: mask keys >= N
+      if (kbase + KT > NL) {  // tail tile: mask keys >= NL
 #pragma unroll
         for (int gi = 0; gi < QG; ++gi)
 #pragma unroll
           for (int f = 0; f < NFR; ++f)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              if (kbase + 16 * f + 4 * g + r >= N) s[gi][f][r] = -INFINITY;
+              if (kbase + 16 * f + 4 * g + r >= NL) s[gi][f][r] = -INFINITY;
       }
 #pragma unroll
       for (int gi = 0; gi < QG; ++gi) {

@@ -1432,6 +1432,8 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd(2, 577, 3, 80),
         lambda: check_attn_fwd(2, 257, 3, 80),
         lambda: check_attn_fwd(1, 33, 2, 80),
+        lambda: check_attn_fwd(3, 1, 2, 80),    # tiled forward with no tile: the last key alone
+        lambda: check_attn_fwd(2, 65, 2, 80),   # one full 64-key tile + the last key
         lambda: check_attn_bwd(2, 257, 3, 80),
         lambda: check_attn_bwd(3, 257, 4, 64),    # N = 256 + 1: key-block body + last-key kernel
         lambda: check_attn_bwd(2, 257, 2, 128),
