@@ -160,8 +160,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
           for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[gi][f][r]);
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float m_new = fmaxf(m_run[gi], tmax * c);  // scaled log2 units (c > 0)
-        const float alpha = __builtin_amdgcn_exp2f(m_run[gi] - m_new);
+        // lazy rescale: the running max (scaled log2 units, c > 0) moves only when some query of the
+        // wave sees a score above it by more than 2^8; otherwise P is taken against the stale max
+        // (values <= 256, exact in fp32 and bf16 range) and O / l skip the alpha multiply
+        const bool grow = __builtin_amdgcn_ballot_w64(tmax * c > m_run[gi] + 8.f) != 0;
+        const float m_new = grow ? fmaxf(m_run[gi], tmax * c) : m_run[gi];
         float psum = 0.f;
 #pragma unroll
         for (int f = 0; f < NFR; ++f) {
@@ -175,10 +178,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
             else s[gi][f][r] = pv;
           }
         }
-        l_run[gi] = l_run[gi] * alpha + psum;
-        m_run[gi] = m_new;
+        if (grow) {
+          const float alpha = __builtin_amdgcn_exp2f(m_run[gi] - m_new);
+          l_run[gi] *= alpha;
 #pragma unroll
-        for (int e = 0; e < C::NE; ++e) o[gi][e] *= alpha;
+          for (int e = 0; e < C::NE; ++e) o[gi][e] *= alpha;
+          m_run[gi] = m_new;
+        }
+        l_run[gi] += psum;
       }
       // O^T[d][q] += V^T[d][key] P^T[key][q]: one V^T fragment read serves every query group
 #pragma unroll
@@ -403,11 +410,12 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
 template <int DH, bool DROP>
 __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                         const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                        const uint16_t* __restrict__ o, int64_t ld_o,
-                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ lse, const float* __restrict__ dlt,
+                                                        const float* __restrict__ dsl,
                                                         uint16_t* __restrict__ dqkv, int64_t ld_dq, float* __restrict__ dq_acc,
-                                                        float* __restrict__ dbias, int N, int H, int D, float scale,
-                                                        int key_off, int key_end, int dq_mode, AttnDrop drop) {
+                                                        float* __restrict__ dbias, float* __restrict__ bpart, int N, int H,
+                                                        int D, float scale, int key_off, int key_end, int dq_mode,
+                                                        int64_t slab_stride, int nslab, AttnDrop drop, AttnQ8 q8) {
   using C = Hd<DH>;
   constexpr int QB = 32;
   constexpr int RB = 128 * C::NH;  // LDS bytes per staged head row
@@ -425,11 +433,13 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int kw0 = kb0 + wave * 32;
   PVR_ASSERT(kb0 < N && L < (int)gridDim.x && (KB & (KB - 1)) == 0);
 
-  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh] | O blk [32][dh]) | dS [32][KB] | 2 x lse [256]
-  // Q / dO / O / lse of query block qb+1 are staged while block qb is processed.
+  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh]) | dS [32][KB] | 2 x (lse | delta | ds_last) [3][256]
+  // Q / dO rows and the per-query constants of query block qb+1 are staged while block qb is processed.
+  // delta = rowsum(dO * O) comes from attn_bwd_prep_kernel (one pass over dO and O instead of every
+  // wave dotting staged O rows per block); ds_last (lastkey path): dS of key N - 1 per query.
   char* kimg = smem;
   char* qdo = kimg + KB * RB;
-  char* dsimg = qdo + 6 * QB * RB;
+  char* dsimg = qdo + 4 * QB * RB;
   float* s_ld = (float*)(dsimg + QB * KB * 2);
   typedef uint32_t v2u __attribute__((ext_vector_type(2)));
   // dS^T image [key_local][32 queries]: 64-B rows of 8-B units (4 queries), unit XOR (key>>1)&7
@@ -443,11 +453,22 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const __amdgpu_buffer_rsrc_t krs = make_rsrc(base + D + h * DH, clamp_bytes(extent));
   const uint16_t* dobase = dout + (int64_t)b * N * ld_do;
   const __amdgpu_buffer_rsrc_t dors = make_rsrc(dobase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2));
-  const uint16_t* obase = o + (int64_t)b * N * ld_o;
-  const __amdgpu_buffer_rsrc_t ors = make_rsrc(obase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_o + DH) * 2));
-  // dQ destination of this batch: the f32 accumulator [N][D] or the bf16 gradient rows directly
-  const __amdgpu_buffer_rsrc_t dqrs = dq_acc ? make_rsrc(dq_acc + (int64_t)b * N * D, clamp_bytes((int64_t)N * D * 4))
-                                             : make_rsrc(dqkv + (int64_t)b * N * ld_dq, clamp_bytes(((int64_t)(N - 1) * ld_dq + D) * 2));
+  // dQ destination of this batch. dq_mode 0-2 with dq_acc: f32 atomics into the accumulator [N][D];
+  // dq_mode 3 (key-block body of a multi-block head): plain f32 stores of this key block's partial
+  // dQ into slab (L % nkb) of dq_acc [slabs][B*N][D] (6 TB/s stores instead of 1.3 TB/s atomics);
+  // dq_mode 4 (the tail launch after a mode-3 body): bf16 dQ = own partial + the nslab slabs;
+  // otherwise the bf16 gradient rows directly.
+  const bool slab_w = dq_mode == 3, slab_r = dq_mode == 4;
+  // optional e5m2 copy of dQKV (the fp8 recipe's grad slot: dgrad and weight-gradient operand) with
+  // the slot's delayed scale, written next to every final bf16 value, amax recorded per wave
+  const bool q8kv = q8.out != nullptr;  // dK / dV: every launch writes final values
+  const bool q8on = q8kv && !slab_w;     // dQ: only the launch that writes the final dQ
+  float q8am = 0.f;
+  const float q8s = q8kv ? *q8.qs : 1.f;
+  const __amdgpu_buffer_rsrc_t q8rs = make_rsrc(q8.out + (int64_t)b * N * q8.ld, q8on ? clamp_bytes((int64_t)(N - 1) * q8.ld + D) : 0u);
+  float* dq_dst = dq_acc && slab_w ? dq_acc + (L % nkb) * slab_stride : dq_acc;
+  const __amdgpu_buffer_rsrc_t dqrs = dq_acc && !slab_r ? make_rsrc(dq_dst + (int64_t)b * N * D, clamp_bytes((int64_t)N * D * 4))
+                                                        : make_rsrc(dqkv + (int64_t)b * N * ld_dq, clamp_bytes(((int64_t)(N - 1) * ld_dq + D) * 2));
 
   // own keys' K and V fragments (B operands): lane holds X[kw0 + 16f + li][32ks + 8g + j]
   v8s kf[2][C::KS], vf[2][C::KS];
@@ -480,19 +501,30 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const float c = scale * LOG2E;
   const int nqb = (N + QB - 1) / QB;
   const uint32_t dkey = DROP ? attn_drop_key(drop, bh) : 0u, npad = (uint32_t)((N + 3) & ~3);
-  auto stage = [&](int qb) {  // Q / dO / O rows and the lse of query block qb into slot qb & 1
+  auto stage = [&](int qb) {  // Q / dO rows and lse / delta (/ ds_last) of query block qb into slot qb & 1
     // everything by LDS-DMA: a plain load of lse here would make hipcc wait vmcnt(0) at its first
-    // use, draining these DMAs right after issuing them. lse of queries past N reads as 0; their
-    // Q and dO rows are zero, so their P = 1 meets dO = 0 and dS = 0 and contributes nothing.
-    char* qi = qdo + (qb & 1) * 3 * QB * RB;
+    // use, draining these DMAs right after issuing them. lse / delta of queries past N read as 0;
+    // their Q and dO rows are zero, so their P = 1 meets dO = 0 and dS = 0 and contributes nothing.
+    char* qi = qdo + (qb & 1) * 2 * QB * RB;
     dma_rows<C::NH>(qrs, qi, QB, ld, qb * QB, wave, NW, lane);
     dma_rows<C::NH>(dors, qi + QB * RB, QB, ld_do, qb * QB, wave, NW, lane);
-    dma_rows<C::NH>(ors, qi + 2 * QB * RB, QB, ld_o, qb * QB, wave, NW, lane);
-    if (wave == NW - 1) {
-      const __amdgpu_buffer_rsrc_t lrs = make_rsrc(lse + (int64_t)bh * N + qb * QB, (uint32_t)(N - qb * QB) * 4);
-      dma16(lrs, to_lds(s_ld + (qb & 1) * 256), (uint32_t)lane * 16);  // 1 KiB slot, first QB floats used
+    if (wave == NW - 1) {  // 1 KiB slots, first QB floats used
+      const int64_t r0 = (int64_t)bh * N + qb * QB;
+      const uint32_t nb = (uint32_t)(N - qb * QB) * 4;
+      dma16(make_rsrc(lse + r0, nb), to_lds(s_ld + (qb & 1) * 768), (uint32_t)lane * 16);
+      dma16(make_rsrc(dlt + r0, nb), to_lds(s_ld + (qb & 1) * 768 + 256), (uint32_t)lane * 16);
+      if (dsl) dma16(make_rsrc(dsl + r0, nb), to_lds(s_ld + (qb & 1) * 768 + 512), (uint32_t)lane * 16);
     }
   };
+  // lastkey path: K[N - 1] at this lane's dQ columns (16e + li of the wave's dQ fragments)
+  float kl_dq[2] = {0.f, 0.f};
+  if (dsl) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int fr = wave + j * NW;
+      if (fr < 2 * C::NE) kl_dq[j] = bf2f(base[(int64_t)(N - 1) * ld + D + h * DH + 16 * (fr % C::NE) + li]);
+    }
+  }
   stage(0);
   float dqb0 = 0.f, dqb1 = 0.f;  // q-bias gradient partials (column sums of this wave's dQ fragments)
   // dQ stores this wave issues per query block (younger than the next block's staging DMAs)
@@ -512,28 +544,30 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (qb + 1 < nqb) stage(qb + 1);
-    const char* qimg = qdo + (qb & 1) * 3 * QB * RB;
+    const char* qimg = qdo + (qb & 1) * 2 * QB * RB;
     const char* doimg = qimg + QB * RB;
-    const char* oimg = doimg + QB * RB;
-    const float* s_lse = s_ld + (qb & 1) * 256;
+    const float* s_lse = s_ld + (qb & 1) * 768;
+    const float* s_dl = s_lse + 256;
 
     if (active) {
-    // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]
+    // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]; dP starts from
+    // -delta of its row, so dS = P * dP' needs no subtraction
     v4f s[2][2], dp[2][2];
-    float dsum[2] = {0.f, 0.f};  // delta partials: query 16a + li, head dims 32ks + 8g .. +7
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a) {
+      const v4f nd = DROP ? v4f{0.f, 0.f, 0.f, 0.f} : -*(const v4f*)(s_dl + 16 * a + 4 * g);
 #pragma unroll
-      for (int f = 0; f < 2; ++f) s[a][f] = dp[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int f = 0; f < 2; ++f) {
+        s[a][f] = v4f{0.f, 0.f, 0.f, 0.f};
+        dp[a][f] = nd;
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < C::KS; ++ks) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         const v8s qa = frag_rows(qimg, QB, 16 * a, ks, lane);
         const v8s da = frag_rows(doimg, QB, 16 * a, ks, lane);
-        if (DH % 32 == 0 || 32 * ks + 8 * g < DH) {  // staged dims past dh belong to the next head
-          dsum[a] = dot8_bf16(da, frag_rows(oimg, QB, 16 * a, ks, lane), dsum[a]);
-        }
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           s[a][f] = mfma16(qa, kf[f][ks], s[a][f]);
@@ -541,18 +575,13 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         }
       }
     }
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      dsum[a] += __shfl_xor(dsum[a], 16, 64);
-      dsum[a] += __shfl_xor(dsum[a], 32, 64);  // every lane li: delta of query 16a + li
-    }
     // P and dS
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * a + 4 * g + r;
-        const float l2 = s_lse[ql] * LOG2E, dl = __shfl(dsum[a], 4 * g + r, 64);
+        const float l2 = s_lse[ql] * LOG2E;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const float pv = __builtin_amdgcn_exp2f(fmaf(s[a][f][r], c, -l2));
@@ -563,10 +592,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
             const uint32_t qi = (uint32_t)min(q0 + ql, N - 1);
             const float m = attn_keep1(dkey, qi * npad + (uint32_t)min(key, N - 1), drop.thr) ? drop.scale : 0.f;
             s[a][f][r] = pv * m;
-            dp[a][f][r] = pv * (m * dp[a][f][r] - dl);
+            dp[a][f][r] = pv * (m * dp[a][f][r] - s_dl[ql]);
           } else {
             s[a][f][r] = pv;
-            dp[a][f][r] = pv * (dp[a][f][r] - dl);
+            dp[a][f][r] = pv * dp[a][f][r];
           }
         }
       }
@@ -638,17 +667,50 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       if (nks_dq > 4) batch(std::integral_constant<int, 4>{});
       const uint32_t vq = (uint32_t)(q0 + 16 * a + 4 * g), col = (uint32_t)(h * DH + 16 * e + li);
       float cs = 0.f;  // queries past N have dS = 0, so their dQ is exactly 0
+      if (dsl) {  // + dS[q][N - 1] K[N - 1] (lastkey path: key N - 1 is not in any key block)
+        const v4f sl = *(const v4f*)(s_ld + (qb & 1) * 768 + 512 + 16 * a + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(sl[r], kl_dq[kfr], acc[r]);
+      }
+      float sadd[4] = {0.f, 0.f, 0.f, 0.f};
+      if (slab_r) {  // the body launch's partial slabs, summed in slab order (deterministic)
+        const uint32_t nbytes = clamp_bytes((int64_t)N * D * 4);
+        for (int sl = 0; sl < nslab; ++sl) {
+          const __amdgpu_buffer_rsrc_t srs = make_rsrc(dq_acc + sl * slab_stride + (int64_t)b * N * D, nbytes);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sadd[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0));
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float val = acc[r] * scale;
+        const float val = acc[r] * scale + sadd[r];
         cs += val;
-        if (dq_acc)
+        if (dq_acc && slab_w)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
+        else if (dq_acc && !slab_r)
           __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
-        else
+        else if (!q8.only)
           __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dqrs, ((vq + r) * (uint32_t)ld_dq + col) * 2, 0, 0);
+        if (q8on) {
+          q8am = nan_max(q8am, fabsf(val));
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pack2_fp8<1, false>(val * q8s, 0.f, 0) & 0xFF), q8rs,
+                                               (vq + r) * (uint32_t)q8.ld + col, 0, 0);
+        }
       }
       if (kfr == 0) dqb0 += cs;  // q-bias gradient: this fragment's column sums across query blocks
       else dqb1 += cs;           // (at most two fragments per wave: host guarantees 2*NE <= 2*NW)
+    }
+  }
+  // bpart (the launch that writes the final dQ): this pair's q-bias partials, the column sums of the
+  // wave's dQ fragments over all query blocks -> [bh][a][16e + li] (the pre-pass adds the v sums)
+  if (bpart) {
+    int kfr = 0;
+    for (int fr = wave; fr < 2 * C::NE && kfr < 2; fr += NW, ++kfr) {
+      float cs = kfr == 0 ? dqb0 : dqb1;
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (g == 0) bpart[((int64_t)bh * 3 + fr / C::NE) * DH + 16 * (fr % C::NE) + li] = cs;
     }
   }
   // in_proj bias gradient partials of this (batch, key block, head): column sums of dQ | dK | dV,
@@ -714,15 +776,34 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       wk.y = pack2bf(dk[e][f][2] * scale, dk[e][f][3] * scale);
       wv.x = pack2bf(dv[e][f][0], dv[e][f][1]);
       wv.y = pack2bf(dv[e][f][2], dv[e][f][3]);
-      *(uint2*)(row + D + h * DH + 16 * e + 4 * g) = wk;
-      *(uint2*)(row + 2 * D + h * DH + 16 * e + 4 * g) = wv;
+      if (!q8.only) {
+        *(uint2*)(row + D + h * DH + 16 * e + 4 * g) = wk;
+        *(uint2*)(row + 2 * D + h * DH + 16 * e + 4 * g) = wv;
+      }
+      if (q8kv) {
+        float k4[4], v4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          k4[r] = dk[e][f][r] * scale;
+          v4[r] = dv[e][f][r];
+          q8am = nan_max(q8am, nan_max(fabsf(k4[r]), fabsf(v4[r])));
+        }
+        uint8_t* qrow = q8.out + ((int64_t)b * N + key) * q8.ld + h * DH + 16 * e + 4 * g;
+        *(uint32_t*)(qrow + D) = (uint32_t)pack2_fp8<1, true>(k4[2] * q8s, k4[3] * q8s, pack2_fp8<1, false>(k4[0] * q8s, k4[1] * q8s, 0));
+        *(uint32_t*)(qrow + 2 * D) =
+            (uint32_t)pack2_fp8<1, true>(v4[2] * q8s, v4[3] * q8s, pack2_fp8<1, false>(v4[0] * q8s, v4[1] * q8s, 0));
+      }
     }
+  }
+  if (q8kv) {
+    q8am = wave_max_nan(q8am);
+    if (lane == 0) amax_record(q8.amax, q8am);
   }
   // dq_mode 1 / 2 (the last launch, one workgroup per (batch, head)): the other key blocks' dQ
   // atomics landed before this launch started and this workgroup's own are acknowledged after the
   // wait below, so it converts the pair's accumulated dQ rows to bf16 (no separate pass over the
   // whole accumulator) and, in mode 2, zeroes them again for the next use of a persistent workspace
-  if (dq_mode && dq_acc) {
+  if ((dq_mode == 1 || dq_mode == 2) && dq_acc) {
     // (no agent-scope fence: it would write back the whole L2. This workgroup's atomics performed in
     // its XCD's L2, which its loads below go through; the CU's L1 holds no line of these rows.)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -754,25 +835,27 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   }
 }
 
-// Backward contribution of ONE key (index kt = N - 1) of every (batch, head) pair, after the main
-// kernel has covered keys [0, N - 1) and written dQ directly (bf16). For ViT's N = 256 + 1 (the CLS
-// token of 224/14) the main kernel's key blocks are then exactly full: a 512-thread workgroup per
-// pair for the one remaining key doubled the whole backward (918 vs 451 us at H/14 b128).
+// Backward pre-pass, one workgroup per (batch, head) pair, streaming the pair's rows once:
+//   delta[q] = rowsum(dO[q] * O[q]) for every query (the main kernel then stages no O rows);
+//   LAST = true (the lastkey path: the main kernel covers keys [0, N - 1)): the contribution of key
+//   kt = N - 1 as well: s = Q.K[kt], dp = dO.V[kt], p = exp(s*scale - lse), ds = p (dp - delta),
+//   written per query (ds_last, added to dQ by the main kernel's dQ epilogue), and dV[kt] = sum p dO,
+//   dK[kt] = scale * sum ds Q reduced here. For ViT's N = 256 + 1 (the CLS token of 224/14) the main
+//   kernel's key blocks are then exactly full.
 // Thread = (row slot, 16-B head-dim chunk): 16 lanes share one query row (coalesced 16-B chunks),
-// 16 row slots per workgroup walk the queries. Per query: s = Q.K, dp = dO.V, delta = dO.O reduced
-// over the row's lanes, p = exp(s*scale - lse), ds = p (dp - delta); dQ += scale * ds * K in place
-// (bf16 read-modify-write of the main kernel's row); dV += p dO and dK += ds Q accumulate per lane
-// and are reduced over the row slots in LDS at the end. Memory-bound, no MFMA.
-template <int DH>
-__global__ void __launch_bounds__(256) attn_bwd_lastkey_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
-                                                                const uint16_t* __restrict__ dout, int64_t ld_do,
-                                                                const uint16_t* __restrict__ o, int64_t ld_o,
-                                                                const float* __restrict__ lse, uint16_t* __restrict__ dqkv,
-                                                                int64_t ld_dq, int N, int H, int D, float scale) {
+// 16 row slots per workgroup walk the queries; memory-bound, no MFMA.
+template <int DH, bool LAST>
+__global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                             const uint16_t* __restrict__ dout, int64_t ld_do,
+                                                             const uint16_t* __restrict__ o, int64_t ld_o,
+                                                             const float* __restrict__ lse, float* __restrict__ dlt,
+                                                             float* __restrict__ dsl, float* __restrict__ bpart,
+                                                             uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H, int D,
+                                                             float scale, AttnQ8 q8) {
   constexpr int NCH = DH / 8;  // 16-B chunks per head row (<= 16)
   constexpr int RS = 16;       // row slots
   static_assert(NCH <= 16, "head dim <= 128");
-  __shared__ float red[2][RS][DH];
+  __shared__ float red[3][RS][DH];
   const int pr = blockIdx.x;
   const int b = pr / H, h = pr % H;
   const int tid = threadIdx.x;
@@ -781,79 +864,91 @@ __global__ void __launch_bounds__(256) attn_bwd_lastkey_kernel(const uint16_t* _
   const int cc = act ? ch : 0;
   const int kt = N - 1;
   const uint16_t* qbase = qkv + (int64_t)b * N * ld + h * DH + cc * 8;
-  // this lane's chunk of K and V of key kt
-  float kf[8], vf[8];
-  {
-    const uint4 kq = *(const uint4*)(qbase + (int64_t)kt * ld + D);
-    const uint4 vq = *(const uint4*)(qbase + (int64_t)kt * ld + 2 * D);
-    const uint32_t uk[4] = {kq.x, kq.y, kq.z, kq.w}, uv[4] = {vq.x, vq.y, vq.z, vq.w};
+  auto unpack = [](const uint4& w, float (&x)[8]) {
+    const uint32_t u[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      kf[j] = act ? bf2f(j & 1 ? uk[j >> 1] >> 16 : uk[j >> 1] & 0xFFFF) : 0.f;
-      vf[j] = act ? bf2f(j & 1 ? uv[j >> 1] >> 16 : uv[j >> 1] & 0xFFFF) : 0.f;
-    }
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(j & 1 ? u[j >> 1] >> 16 : u[j >> 1] & 0xFFFF);
+  };
+  float kf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, vf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (LAST && act) {  // this lane's chunk of K and V of key kt
+    unpack(*(const uint4*)(qbase + (int64_t)kt * ld + D), kf);
+    unpack(*(const uint4*)(qbase + (int64_t)kt * ld + 2 * D), vf);
   }
   const float c = scale * LOG2E;
   float av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float ov_sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of dO (the v-bias gradient)
   for (int q = rs; q < N; q += RS) {
     const int64_t row = (int64_t)b * N + q;
-    const uint4 qq = *(const uint4*)(qbase + (int64_t)q * ld);
-    const uint4 dd = *(const uint4*)(dout + row * ld_do + h * DH + cc * 8);
-    const uint4 oo = *(const uint4*)(o + row * ld_o + h * DH + cc * 8);
-    uint4* dqp = (uint4*)(dqkv + row * ld_dq + h * DH + cc * 8);
-    const uint4 dq = *dqp;
-    const float l2 = lse[(int64_t)pr * N + q] * LOG2E;
-    const uint32_t uq[4] = {qq.x, qq.y, qq.z, qq.w}, ud[4] = {dd.x, dd.y, dd.z, dd.w}, uo[4] = {oo.x, oo.y, oo.z, oo.w};
-    float qv[8], dv[8];
-    float sdot = 0.f, dpdot = 0.f, dl = 0.f;
+    float dv[8], ov[8];
+    unpack(*(const uint4*)(dout + row * ld_do + h * DH + cc * 8), dv);
+    unpack(*(const uint4*)(o + row * ld_o + h * DH + cc * 8), ov);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      qv[j] = bf2f(j & 1 ? uq[j >> 1] >> 16 : uq[j >> 1] & 0xFFFF);
-      dv[j] = bf2f(j & 1 ? ud[j >> 1] >> 16 : ud[j >> 1] & 0xFFFF);
-      const float ov = bf2f(j & 1 ? uo[j >> 1] >> 16 : uo[j >> 1] & 0xFFFF);
-      sdot = fmaf(qv[j], kf[j], sdot);
-      dpdot = fmaf(dv[j], vf[j], dpdot);
-      dl = act ? fmaf(dv[j], ov, dl) : dl;
+    for (int j = 0; j < 8; ++j) ov_sum[j] += dv[j];
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl = fmaf(dv[j], ov[j], dl);
+    if (!act) dl = 0.f;
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) dl += __shfl_xor(dl, off, 16);  // the row's 16 lanes
+    if constexpr (LAST) {
+      float qv[8];
+      unpack(*(const uint4*)(qbase + (int64_t)q * ld), qv);
+      float sdot = 0.f, dpdot = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sdot = fmaf(qv[j], kf[j], sdot);
+        dpdot = fmaf(dv[j], vf[j], dpdot);
+      }
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) {
+        sdot += __shfl_xor(sdot, off, 16);
+        dpdot += __shfl_xor(dpdot, off, 16);
+      }
+      const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -lse[(int64_t)pr * N + q] * LOG2E));
+      const float ds = p * (dpdot - dl);
+      if (ch == 0) dsl[(int64_t)pr * N + q] = ds;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        av[j] = fmaf(p, dv[j], av[j]);
+        ak[j] = fmaf(ds, qv[j], ak[j]);
+      }
     }
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {  // the row's 16 lanes
-      sdot += __shfl_xor(sdot, off, 16);
-      dpdot += __shfl_xor(dpdot, off, 16);
-      dl += __shfl_xor(dl, off, 16);
-    }
-    const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -l2));
-    const float ds = p * (dpdot - dl);
-    const float f = ds * scale;
-    const uint32_t u[4] = {dq.x, dq.y, dq.z, dq.w};
-    uint32_t w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      w[j] = pack2bf(fmaf(f, kf[2 * j], bf2f(u[j] & 0xFFFF)), fmaf(f, kf[2 * j + 1], bf2f(u[j] >> 16)));
-    if (act) *dqp = make_uint4(w[0], w[1], w[2], w[3]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      av[j] = fmaf(p, dv[j], av[j]);
-      ak[j] = fmaf(ds, qv[j], ak[j]);
-    }
+    if (ch == 0) dlt[(int64_t)pr * N + q] = dl;
   }
+  if (!LAST && !bpart) return;
   if (act) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[0][rs][cc * 8 + j] = av[j];
       red[1][rs][cc * 8 + j] = ak[j];
+      red[2][rs][cc * 8 + j] = ov_sum[j];
     }
   }
   __syncthreads();
   if (tid < DH) {
-    float sv = 0.f, sk = 0.f;
+    float sv = 0.f, sk = 0.f, so = 0.f;
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
       sv += red[0][r][tid];
       sk += red[1][r][tid];
+      so += red[2][r][tid];
     }
-    uint16_t* krow = dqkv + ((int64_t)b * N + kt) * ld_dq + h * DH;
-    krow[D + tid] = f2bf(sk * scale);
-    krow[2 * D + tid] = f2bf(sv);
+    if constexpr (LAST) {
+      uint16_t* krow = dqkv + ((int64_t)b * N + kt) * ld_dq + h * DH;
+      if (!q8.only) {
+        krow[D + tid] = f2bf(sk * scale);
+        krow[2 * D + tid] = f2bf(sv);
+      }
+      if (q8.out) {  // e5m2 copy of key kt's dK / dV (amax of the two values: the rest come from the main kernel)
+        const float qs = *q8.qs;
+        uint8_t* qrow = q8.out + ((int64_t)b * N + kt) * q8.ld + h * DH;
+        qrow[D + tid] = (uint8_t)(pack2_fp8<1, false>(sk * scale * qs, 0.f, 0) & 0xFF);
+        qrow[2 * D + tid] = (uint8_t)(pack2_fp8<1, false>(sv * qs, 0.f, 0) & 0xFF);
+        amax_record(q8.amax, nan_max(fabsf(sk * scale), fabsf(sv)));
+      }
+    }
+    // v-bias partial: sum_k dV[k] = sum_q dO[q] (softmax rows sum to 1, no attention dropout)
+    if (bpart) bpart[((int64_t)pr * 3 + 2) * DH + tid] = so;
   }
 }
 
@@ -1247,26 +1342,28 @@ __global__ void __launch_bounds__(256) dq_convert_kernel(float* __restrict__ acc
 // part[(b*H + h)*NQ + nq][192] (q sums of the two 16-query halves | v sums), deterministic in two
 // passes: (1) grid (H, S): rows s*R .. of head h's B*NQ partial rows -> ws[s][h][128] (q | v);
 // (2) grid H: dbias[q slice of h] += sum_s, dbias[v slice of h] += sum_s (the k bias gradient is 0).
-__global__ void __launch_bounds__(128) dbias_part_kernel(const float* __restrict__ part, float* __restrict__ ws, int B, int H,
-                                                         int NQ, int R) {
+// partial rows of 3 * DH floats: q sums of the two 16-query halves | v sums; block = 2 * DH threads
+__global__ void __launch_bounds__(256) dbias_part_kernel(const float* __restrict__ part, float* __restrict__ ws, int B, int H,
+                                                         int NQ, int R, int DH) {
   const int h = blockIdx.x, sidx = blockIdx.y, t = threadIdx.x;
   const int rows = B * NQ, r0 = sidx * R, r1 = min(rows, r0 + R);
   float a = 0.f;
 #pragma unroll 8
   for (int r = r0; r < r1; ++r) {  // unrolled: eight rows' loads in flight, not one dependent load per row
     const int b = r / NQ, nq = r - b * NQ;
-    const float* row = part + ((int64_t)(b * H + h) * NQ + nq) * 192;
-    a += t < 64 ? row[t] + row[64 + t] : row[64 + t];
+    const float* row = part + ((int64_t)(b * H + h) * NQ + nq) * 3 * DH;
+    a += t < DH ? row[t] + row[DH + t] : row[DH + t];
   }
-  ws[((int64_t)sidx * H + h) * 128 + t] = a;
+  ws[((int64_t)sidx * H + h) * 2 * DH + t] = a;
 }
 
-__global__ void __launch_bounds__(128) dbias_final_kernel(const float* __restrict__ ws, float* __restrict__ dbias, int H, int D, int S) {
+__global__ void __launch_bounds__(256) dbias_final_kernel(const float* __restrict__ ws, float* __restrict__ dbias, int H, int D, int S,
+                                                          int DH) {
   const int h = blockIdx.x, t = threadIdx.x;
   // four independent partial sums, 16 loads in flight per thread: the one-accumulator loop waited one
   // memory latency per split (32 us for 128 splits at ViT-B/16 b256); fixed order, so deterministic
-  const float* col = ws + (int64_t)h * 128 + t;
-  const int64_t step = (int64_t)H * 128;
+  const float* col = ws + (int64_t)h * 2 * DH + t;
+  const int64_t step = (int64_t)H * 2 * DH;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int sidx = 0;
 #pragma unroll 4
@@ -1278,25 +1375,27 @@ __global__ void __launch_bounds__(128) dbias_final_kernel(const float* __restric
   }
   for (; sidx < S; ++sidx) a0 += col[sidx * step];
   const float a = (a0 + a1) + (a2 + a3);
-  if (t < 64)
-    dbias[h * 64 + t] += a;
+  if (t < DH)
+    dbias[h * DH + t] += a;
   else
-    dbias[2 * D + h * 64 + (t - 64)] += a;
+    dbias[2 * D + h * DH + (t - DH)] += a;
 }
 
 }  // namespace
 }  // namespace pvr
 
-// ws: f32 [S][H][128] scratch, S = pvr_attn_dbias_splits(B, NQ)
+// ws: f32 [S][H][2 * DH] scratch, S = pvr_attn_dbias_splits(B, NQ); part f32 [B*H][NQ][3 * DH]
 extern "C" int pvr_attn_dbias_splits(int B, int NQ) { return B * NQ < 128 ? B * NQ : 128; }
 
 extern "C" hipError_t pvr_attn_dbias_reduce(const float* part, float* ws, float* dbias, int B, int H, int NQ, int D, hipStream_t s) {
   using namespace pvr;
   const int S = pvr_attn_dbias_splits(B, NQ);
   if (S <= 0) return hipSuccess;
+  const int DH = D / H;
+  if (D % H != 0 || 2 * DH > 256) return hipErrorInvalidValue;
   const int R = (B * NQ + S - 1) / S;
-  hipLaunchKernelGGL(dbias_part_kernel, dim3(H, S), dim3(128), 0, s, part, ws, B, H, NQ, R);
-  hipLaunchKernelGGL(dbias_final_kernel, dim3(H), dim3(128), 0, s, ws, dbias, H, D, S);
+  hipLaunchKernelGGL(dbias_part_kernel, dim3(H, S), dim3(2 * DH), 0, s, part, ws, B, H, NQ, R, DH);
+  hipLaunchKernelGGL(dbias_final_kernel, dim3(H), dim3(2 * DH), 0, s, ws, dbias, H, D, S, DH);
   return hipGetLastError();
 }
 
@@ -1422,17 +1521,42 @@ extern "C" int pvr_attn_bwd_waves(int N) {
   return need >= 8 ? 8 : (need > 4 ? 8 : (need > 2 ? 4 : (need > 1 ? 2 : 1)));
 }
 
-// N = (full key blocks) + 1 key: main kernel + last-key kernel, dQ written directly (no dq_acc);
-// not with attention dropout (the last-key kernel has no mask)
+// N = (full key blocks) + 1 key: main kernel + the pre-pass's last key, dQ written directly (no
+// dq_acc); not with attention dropout (the pre-pass has no mask)
 static bool attn_bwd_lastkey_path(int N, bool dbias, bool drop) {
   const int KB = 32 * pvr_attn_bwd_waves(N);
   return (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && !drop && N <= 512;
 }
 
+// key-block body + short tail with dQ through f32 slabs (see attn_bwd_generic)
+static bool attn_bwd_slab_path(int N, bool dbias, bool drop) {
+  const int KB = 32 * pvr_attn_bwd_waves(N);
+  const int rem = N % KB;
+  return !attn_bwd_lastkey_path(N, dbias, drop) && (N + KB - 1) / KB > 1 && rem >= 16 && rem <= 128 && !dbias;
+}
+
+// the generic backward's kernels write every final dQ value (no f32 atomics + conversion pass)
+static bool attn_bwd_final_dq_in_kernel(int N, bool dbias, bool drop) {
+  const int KB = 32 * pvr_attn_bwd_waves(N);
+  return attn_bwd_lastkey_path(N, dbias, drop) || attn_bwd_slab_path(N, dbias, drop) || (N + KB - 1) / KB == 1;
+}
+
+// the generic backward can emit the in_proj bias gradient as [B*H][1][3*dh] partials (q sums of
+// the two 16-query fragment rows | v sums = dO column sums): the launch that writes the final dQ
+// holds every dQ fragment of a pair, at most two per wave (no attention dropout: its rows of P do
+// not sum to 1, so sum_k dV != sum_q dO)
+static bool attn_bwd_bpart_ok(int N, int DH) {
+  const int NE = DH / 16;
+  const int KB = 32 * pvr_attn_bwd_waves(N);
+  if (attn_bwd_lastkey_path(N, false, false)) return NE <= pvr_attn_bwd_waves(N);
+  if (attn_bwd_slab_path(N, false, false)) return NE <= pvr_attn_bwd_waves(N % KB);
+  return (N + KB - 1) / KB == 1 && NE <= pvr_attn_bwd_waves(N);
+}
+
 // 1 if pvr_attn_bwd needs the zero-initialised f32 dQ workspace for this shape
 extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias, int drop) {
   if (pvr_attn_bwd_key_blocks(N) <= 1) return 0;
-  return attn_bwd_lastkey_path(N, dbias != 0, drop != 0) ? 0 : 1;
+  return attn_bwd_lastkey_path(N, dbias != 0, drop != 0) || attn_bwd_slab_path(N, dbias != 0, drop != 0) ? 0 : 1;
 }
 
 template <int NQ>
@@ -1466,55 +1590,70 @@ static bool attn_bwd_pipe_ok(int B, int N, int H, int D, int64_t ld, int64_t ld_
 template <int DH, bool DROP>
 static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                    int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, const pvr::AttnDrop& drop,
-                                   hipStream_t s) {
+                                   int dq_rezero, float* dbias, float* bpart, float* ws, int B, int N, int H, int D, float scale,
+                                   const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
   using namespace pvr;
+  if (bpart && (DROP || dbias || !attn_bwd_bpart_ok(N, DH))) return hipErrorInvalidValue;
+  if (q8.out && !attn_bwd_final_dq_in_kernel(N, dbias != nullptr, DROP)) return hipErrorInvalidValue;
   const int NW = pvr_attn_bwd_waves(N);
   const int KB = NW * 32;
   const int nkb = (N + KB - 1) / KB;
-  if (nkb > 1 && !dq_acc && !attn_bwd_lastkey_path(N, dbias != nullptr, DROP)) return hipErrorInvalidValue;
+  const bool lastkey = attn_bwd_lastkey_path(N, dbias != nullptr, DROP);
+  const int rem_ = N % KB;
+  const bool slab_path = !lastkey && nkb > 1 && rem_ >= 16 && rem_ <= 128 && !dbias;
+  if (nkb > 1 && !dq_acc && !lastkey && !slab_path) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
+  if (!ws) return hipErrorInvalidValue;
   const int RB = 128 * Hd<DH>::NH;
+  // K image | 2 x (Q | dO) blocks | dS | 2 x (lse | delta | ds_last) 1 KiB DMA slots
+  auto smem_of = [&](int kb) { return (size_t)kb * RB + 4 * 32 * RB + 32 * kb * 2 + 6 * 1024; };
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)(8 * 32 * RB + 6 * 32 * RB + 32 * 8 * 32 * 2 + 2 * 1024));
+                                             (int)smem_of(8 * 32));
     if (e != hipSuccess) return e;
     attr = true;
   }
-  // K image | 2 x (Q | dO | O) blocks | dS | 2 x 1 KiB lse DMA slots
-  auto launch = [&](int nw, int k0, int k1, int dq_mode) {
+  // pre-pass: delta (and, on the lastkey path, key N - 1's dS / dK / dV)
+  float* dlt = ws;
+  float* dsl = lastkey ? ws + (int64_t)B * H * N : nullptr;
+  float* slab = slab_path ? ws + 2 * (int64_t)B * H * N : nullptr;  // [N / KB][B*N][D] f32 partial dQ
+  if (lastkey)
+    hipLaunchKernelGGL((attn_bwd_prep_kernel<DH, true>), dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dlt, dsl,
+                       bpart, dqkv, ld_dq, N, H, D, scale, q8);
+  else
+    hipLaunchKernelGGL((attn_bwd_prep_kernel<DH, false>), dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dlt,
+                       nullptr, bpart, dqkv, ld_dq, N, H, D, scale, q8);
+  // bp: q-bias partials, passed only to the launch that writes the final dQ
+  auto launch = [&](int nw, int k0, int k1, int dq_mode, float* dqa, int64_t sstride, int nslab, float* bp) {
     const int kb = nw * 32;
-    const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
-    hipLaunchKernelGGL((attn_bwd_kernel<DH, DROP>), dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem, s, qkv, ld, dout,
-                       ld_do, out, ld_o, lse, dqkv, ld_dq, nkb > 1 ? dq_acc : nullptr, dbias, N, H, D, scale, k0, k1, dq_mode, drop);
+    hipLaunchKernelGGL((attn_bwd_kernel<DH, DROP>), dim3((k1 - k0 + kb - 1) / kb * B * H), dim3(nw * 64), smem_of(kb), s, qkv, ld,
+                       dout, ld_do, lse, dlt, dsl, dqkv, ld_dq, dqa, dbias, bp, N, H, D, scale, k0, k1, dq_mode, sstride, nslab, drop,
+                       q8);
   };
-  const int rem = N % KB;
-  if (attn_bwd_lastkey_path(N, dbias != nullptr, DROP)) {
-    // one key past a full key block: the main kernel over keys [0, N - 1) writes dQ directly, the
-    // last key's dK / dV and dQ contribution come from the streaming kernel above
-    const int kb = NW * 32, k1 = N - 1;
-    const size_t smem = (size_t)kb * RB + 6 * 32 * RB + 32 * kb * 2 + 2 * 1024;
-    hipLaunchKernelGGL((attn_bwd_kernel<DH, DROP>), dim3((k1 + kb - 1) / kb * B * H), dim3(NW * 64), smem, s, qkv, ld, dout, ld_do,
-                       out, ld_o, lse, dqkv, ld_dq, nullptr, nullptr, N, H, D, scale, 0, k1, 0, drop);
-    hipLaunchKernelGGL(attn_bwd_lastkey_kernel<DH>, dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dqkv, ld_dq,
-                       N, H, D, scale);
+  if (lastkey) {
+    // one key past a full key block: the main kernel over keys [0, N - 1) writes dQ directly (adding
+    // the pre-pass's dS of key N - 1 times K[N - 1]); that key's dK / dV come from the pre-pass
+    launch(NW, 0, N - 1, 0, nullptr, 0, 0, bpart);
     return hipGetLastError();
   }
-  if (nkb > 1 && rem >= 16 && rem <= 128 && !dbias) {
+  const int rem = N % KB;
+  if (slab_path) {
     // N = a multiple of KB plus a short tail (ViT-L/16@384: 577 = 2 x 256 + 65): the KB-aligned body
     // in full-size workgroups, the tail in workgroups sized for it, instead of 8-wave workgroups with
     // 3 live waves holding a CU each (818 vs 862 us at B64 H16). A 1-key tail (257 = 256 + 1, the
-    // CLS token of 224/14) is cheaper left interleaved in the one grid: as its own launch of 1-wave
-    // workgroups it serialises 9 query-block staging round trips per pair (975 vs 915 us at H/14
-    // b128; scripts/attn_shape_probe.py)
-    // the tail launch has one workgroup per (batch, head) and runs after the body: it also turns
-    // the pair's accumulated dQ into bf16 (and re-zeroes a persistent accumulator)
-    launch(NW, 0, N - rem, 0);
-    launch(pvr_attn_bwd_waves(rem), N - rem, N, dq_rezero ? 2 : 1);
+    // CLS token of 224/14) takes the lastkey path above instead.
+    // The body's key blocks store their partial dQ as f32 slabs (plain stores); the tail launch,
+    // one workgroup per (batch, head) running after the body, adds them to its own partial and
+    // writes bf16 dQ: no atomics, no zeroed accumulator, no conversion pass
+    // (ViT-L/16@384 b128: 1.16 ms per layer with f32 atomics, profiles/r4/attn_ab*).
+    const int nslab = (N - rem) / KB;
+    const int64_t sstride = (int64_t)B * N * D;
+    launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
+    launch(pvr_attn_bwd_waves(rem), N - rem, N, 4, slab, sstride, nslab, bpart);
     return hipGetLastError();
   }
-  launch(NW, 0, N, 0);
+  launch(NW, 0, N, 0, nkb > 1 ? dq_acc : nullptr, 0, 0, nkb > 1 ? nullptr : bpart);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
     int64_t blocks = (rows * D + 255) / 256;
@@ -1527,16 +1666,27 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
 template <int DH>
 static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                   int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                  int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, const pvr::AttnDrop& drop,
-                                  hipStream_t s) {
+                                  int dq_rezero, float* dbias, float* bpart, float* ws, int B, int N, int H, int D, float scale,
+                                  const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
   if (drop.seed)  // attention dropout: the generic kernel regenerates the forward's keep mask
-    return attn_bwd_generic<DH, true>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale,
-                                      drop, s);
-  if (DH == 64 && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][192] partials
+    return attn_bwd_generic<DH, true>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, bpart, ws, B, N, H, D, scale,
+                                      drop, q8, s);
+  if (DH == 64 && !q8.out && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq))  // dbias: [B*H][NQ][192] partials
     return attn_bwd_pipe8_launch<7>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dbias, B, N, H, D, scale, s);
-  return attn_bwd_generic<DH, false>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale,
-                                     drop, s);
+  return attn_bwd_generic<DH, false>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, bpart, ws, B, N, H, D, scale,
+                                     drop, q8, s);
 }
+
+// floats of the f32 scratch pvr_attn_bwd needs (per-query delta and, on the lastkey path, ds_last)
+extern "C" int64_t pvr_attn_bwd_ws_floats(int B, int N, int H, int D, int dbias, int drop) {
+  int64_t n = 2 * (int64_t)B * H * N;
+  if (attn_bwd_slab_path(N, dbias != 0, drop != 0)) n += (int64_t)(N / (32 * pvr_attn_bwd_waves(N))) * B * N * D;
+  return n;
+}
+
+// 1 if pvr_attn_bwd can write dQKV's e5m2 copy (q8_out) for this shape: the generic kernels must
+// write every final dQ value
+extern "C" int pvr_attn_bwd_q8_ok(int N, int drop) { return attn_bwd_final_dq_in_kernel(N, false, drop != 0) ? 1 : 0; }
 
 // 1 if pvr_attn_bwd takes the pipelined whole-head backward for this shape and these layouts; its
 // dbias is then f32 [B*H][ceil(N/32)][192] partials instead: per (batch, head, 32-query block) the
@@ -1547,11 +1697,13 @@ extern "C" int pvr_attn_bwd_uses_pipe(int B, int N, int H, int D, int64_t ld, in
   return !drop && attn_bwd_pipe_ok(B, N, H, D, ld, ld_do, ld_o, ld_dq) ? 1 : 0;
 }
 
-// Rows R of the f32 [B*H][R][192] bias-gradient partials (q half 0 | q half 1 | v) that pvr_attn_bwd
-// writes into `dbias` for this shape (pipelined kernel: R = 32-query blocks), or 0 when `dbias`
-// means the generic kernel's [B * key blocks][3D] layout.
+// Rows R of the f32 [B*H][R][3*dh] bias-gradient partials (q half 0 | q half 1 | v) that pvr_attn_bwd
+// writes for this shape: pipelined kernel (into `dbias`): R = 32-query blocks; generic kernel (into
+// `bpart`): R = 1 where attn_bwd_bpart_ok; 0: none (`dbias` then means the generic kernel's
+// [B * key blocks][3D] layout).
 extern "C" int pvr_attn_bwd_part_rows(int B, int N, int H, int D, int64_t ld, int64_t ld_do, int64_t ld_o, int64_t ld_dq, int drop) {
-  return pvr_attn_bwd_uses_pipe(B, N, H, D, ld, ld_do, ld_o, ld_dq, drop) ? (N + 31) / 32 : 0;
+  if (pvr_attn_bwd_uses_pipe(B, N, H, D, ld, ld_do, ld_o, ld_dq, drop)) return (N + 31) / 32;
+  return !drop && H > 0 && D % H == 0 && pvr_attn_head_dim_supported(D / H) && attn_bwd_bpart_ok(N, D / H) ? 1 : 0;
 }
 
 // dq_acc: f32 [B*N][D] zero-initialised workspace, required iff N > 256 (several key blocks per head);
@@ -1559,16 +1711,22 @@ extern "C" int pvr_attn_bwd_part_rows(int B, int N, int H, int D, int64_t ld, in
 // dbias: optional f32 [B * nkb][3D] partial column sums of dQ | dK | dV (nkb = pvr_attn_bwd_key_blocks;
 // every element is written), whose row sum is the in_proj bias gradient; on the pipelined path
 // (pvr_attn_bwd_uses_pipe) the per-block partials described there.
+// ws: f32 scratch of pvr_attn_bwd_ws_floats(B, N, H) floats (the generic path's pre-pass outputs).
 extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ld_o, const uint16_t* dout,
                                    int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
-                                   int dq_rezero, float* dbias, int B, int N, int H, int D, float scale, const uint64_t* seed,
-                                   uint64_t seed_off, uint32_t thr16, float keep_scale, hipStream_t s) {
+                                   int dq_rezero, float* dbias, float* bpart, float* ws, int B, int N, int H, int D, float scale,
+                                   const uint64_t* seed, uint64_t seed_off, uint32_t thr16, float keep_scale, uint8_t* q8_out,
+                                   int64_t q8_ld, const float* q8_qs, unsigned* q8_amax, int q8_only, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
+  if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
   const pvr::AttnDrop drop{seed, seed_off, thr16, keep_scale};
+  if (q8_only && (!q8_out || dq_acc)) return hipErrorInvalidValue;  // atomics-path dQ needs the bf16 conversion
+  const pvr::AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, q8_only};
   switch (D / H) {
 #define PVR_BWD_DH(DH) \
   case DH:             \
-    return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, B, N, H, D, scale, drop, s);
+    return attn_bwd_launch<DH>(qkv, ld, out, ld_o, dout, ld_do, lse, dqkv, ld_dq, dq_acc, dq_rezero, dbias, bpart, ws, B, N, H, D, scale, \
+                               drop, q8, s);
     PVR_BWD_DH(64) PVR_BWD_DH(80) PVR_BWD_DH(96) PVR_BWD_DH(128)
 #undef PVR_BWD_DH
     default: return hipErrorInvalidValue;

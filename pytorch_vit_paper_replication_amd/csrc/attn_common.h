@@ -117,6 +117,7 @@ struct AttnQ8 {
   int64_t ld;
   const float* qs;
   unsigned* amax;
+  int only;  // backward: store only the fp8 copy, not the bf16 gradient (every reader takes the copy)
 };
 // max|x| record with few same-address atomics: most waves find the running amax already larger
 PVR_DEV void amax_record(unsigned* amax, float m) {

@@ -71,8 +71,11 @@ int pvr_attn_dbias_splits(int, int);
 hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float*, const uint16_t*, int64_t, int, uint16_t*, int64_t,
                                hipStream_t);
 hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, int, hipStream_t);
-hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, int, int, int, int, float,
-                        const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
+hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, float*, float*, int, int, int, int, float,
+                        const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t, const float*, unsigned*,
+                        int, hipStream_t);
+int64_t pvr_attn_bwd_ws_floats(int, int, int, int, int, int);
+int pvr_attn_bwd_q8_ok(int, int);
 }
 
 namespace {
@@ -848,14 +851,15 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int
 // dbias[3D] += the in_proj bias gradient from the pipelined backward's [B*H][NQ][192] partials
 // (per query block: dQ column sums of two query halves | dO column sums; the k slice gets none)
 void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor dbias) {
-  TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32 && part.is_contiguous() && part.numel() % (B * H * 192) == 0,
-              "attn_dbias_reduce: f32 [B*H][NQ][192] partials");
-  TORCH_CHECK(dbias.is_cuda() && dbias.scalar_type() == torch::kFloat32 && dbias.is_contiguous() && dbias.numel() == 3 * H * 64,
-              "attn_dbias_reduce: f32 [3D] bias gradient, D = 64 H");
-  const int64_t NQ = part.numel() / (B * H * 192);
-  auto ws = torch::empty({(int64_t)pvr_attn_dbias_splits((int)B, (int)NQ) * H * 128}, part.options());
+  TORCH_CHECK(dbias.is_cuda() && dbias.scalar_type() == torch::kFloat32 && dbias.is_contiguous() && dbias.numel() % (3 * H) == 0,
+              "attn_dbias_reduce: f32 [3D] bias gradient");
+  const int64_t DH = dbias.numel() / (3 * H);
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32 && part.is_contiguous() && part.numel() % (B * H * 3 * DH) == 0,
+              "attn_dbias_reduce: f32 [B*H][R][3 * head dim] partials");
+  const int64_t NQ = part.numel() / (B * H * 3 * DH);
+  auto ws = torch::empty({(int64_t)pvr_attn_dbias_splits((int)B, (int)NQ) * H * 2 * DH}, part.options());
   check(pvr_attn_dbias_reduce(part.data_ptr<float>(), ws.data_ptr<float>(), dbias.data_ptr<float>(), (int)B, (int)H, (int)NQ,
-                              (int)(64 * H), stream()),
+                              (int)(DH * H), stream()),
         "attn_dbias_reduce");
 }
 
@@ -887,60 +891,93 @@ int64_t attn_bwd_bias_rows(int64_t B, int64_t N, int64_t H, int64_t D, bool drop
   return pvr_attn_bwd_part_rows((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D, drop ? 1 : 0);
 }
 
+// 1 if attn_bwd can write dQKV's e5m2 copy (q_out) for this shape with the standard layouts (the
+// generic kernels write every final dQ value; not the pipelined ViT-B/16 kernel)
+bool attn_bwd_q8_ok(int64_t B, int64_t N, int64_t H, int64_t D, bool drop) {
+  return pvr_attn_bwd_q8_ok((int)N, drop ? 1 : 0) && !pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, 3 * D, D, D, 3 * D, drop ? 1 : 0);
+}
+
 // dbias: [3D] f32 accumulated with the in_proj bias gradient. dbias_part (pipelined path only,
 // [B*H][ceil(N/32)][192] f32): receives the kernel's per-block partials instead, left unreduced (the
 // caller reduces them, e.g. on the weight-gradient side stream: attn_dbias_reduce).
 torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
                        double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out,
-                       c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p) {
+                       c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
+                       c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool q_only) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
   torch::Tensor dq_acc;
   int dq_rezero = 0;
-  const bool has_db = dbias.has_value() && dbias->defined();
   const DropArgs drop = drop_args(seed, drop_p, "attn_bwd");
   const int has_drop = drop.seed ? 1 : 0;
-  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)(D / H), has_db ? 1 : 0, has_drop)) {
-    dq_acc = dq_workspace(B * N * D, qkv.options());
-    dq_rezero = dq_acc.defined() ? 1 : 0;
-    if (!dq_acc.defined()) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
-  }
-  // fused in_proj bias gradient: per-(batch, key block) partial sums (no atomics), reduced below
-  torch::Tensor dbias_part;
+  const int64_t dh = D / H;
+  // fused in_proj bias gradient: per-(batch, head, row) partials written by the kernels (no atomics;
+  // pipelined kernel: per 32-query block, generic kernel: one row per pair), reduced below
+  torch::Tensor dbias_part, old_part;
   const bool want_db = dbias.has_value() && dbias->defined();
-  const int prow = pvr_attn_bwd_part_rows((int)B, (int)N, (int)H, (int)D, ld_of(qkv, "qkv"), ld_of(dout, "dout"), ld_of(out, "out"),
-                                          ld_of(dqkv, "dqkv"), has_drop);
-  const bool pipe = prow > 0;  // the kernel writes [B*H][prow][192] partials
+  const int64_t lds[4] = {ld_of(qkv, "qkv"), ld_of(dout, "dout"), ld_of(out, "out"), ld_of(dqkv, "dqkv")};
+  const int prow = pvr_attn_bwd_part_rows((int)B, (int)N, (int)H, (int)D, lds[0], lds[1], lds[2], lds[3], has_drop);
+  const bool parts = prow > 0;  // the kernels write [B*H][prow][3*dh] partials
+  const bool pipe = pvr_attn_bwd_uses_pipe((int)B, (int)N, (int)H, (int)D, lds[0], lds[1], lds[2], lds[3], has_drop) != 0;
   const bool part_out = dbias_part_out.has_value() && dbias_part_out->defined();
   if (part_out) {
-    TORCH_CHECK(pipe && !want_db, "dbias_part: pipelined / chunked backward only, and not together with dbias");
+    TORCH_CHECK(parts && !want_db, "dbias_part: shapes with attn_bwd_bias_rows > 0 only, and not together with dbias");
     TORCH_CHECK(dbias_part_out->is_cuda() && dbias_part_out->scalar_type() == torch::kFloat32 && dbias_part_out->is_contiguous() &&
-                    dbias_part_out->numel() == B * H * prow * 192,
-                "dbias_part [B*H][attn_bwd_bias_rows][192] f32");
+                    dbias_part_out->numel() == B * H * prow * 3 * dh,
+                "dbias_part [B*H][attn_bwd_bias_rows][3 * head dim] f32");
     dbias_part = *dbias_part_out;
   }
   if (want_db) {
     TORCH_CHECK(dbias->numel() == 3 * D && dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous(), "dbias [3D] f32");
-    const int dh = (int)(D / H);
-    if (pipe)  // per-(batch, head, block or chunk) partials written by the kernel: q 2 x 64 | v 64
-      dbias_part = torch::empty({B * H, (int64_t)prow, 192}, qkv.options().dtype(torch::kFloat32));
+    if (parts)  // q sums of the two 16-query fragment rows | v sums, per (batch, head, row)
+      dbias_part = torch::empty({B * H, (int64_t)prow, 3 * dh}, qkv.options().dtype(torch::kFloat32));
     else if (2 * (dh / 16) <= 2 * pvr_attn_bwd_waves((int)N))
-      dbias_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
+      old_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
-  const hipError_t err = pvr_attn_bwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf(out, "out"), ld_of(out, "out"), bf(dout, "dout"),
-                                      ld_of(dout, "dout"), f32(lse, "lse"), bf_mut(dqkv, "dqkv"),
-                                      ld_of(dqkv, "dqkv"), dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
-                                      dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr, (int)B, (int)N, (int)H, (int)D,
-                                      (float)scale, drop.seed, (uint64_t)seed_offset, drop.thr, drop.scale, stream());
+  const int old_db = old_part.defined() ? 1 : 0;
+  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)dh, old_db, has_drop)) {
+    dq_acc = dq_workspace(B * N * D, qkv.options());
+    dq_rezero = dq_acc.defined() ? 1 : 0;
+    if (!dq_acc.defined()) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
+  }
+  // optional e5m2 copy of dQKV + amax record (the fp8 recipe's dgrad / weight-gradient operand)
+  uint8_t* qp = nullptr;
+  int64_t ldq = 0;
+  const float* qs = nullptr;
+  unsigned* qa = nullptr;
+  if (q_out.has_value() && q_out->defined()) {
+    TORCH_CHECK(pvr_attn_bwd_q8_ok((int)N, has_drop) && !old_db && !pipe, "attn_bwd: no e5m2 dQKV copy for this shape (see attn_bwd_q8_ok)");
+    TORCH_CHECK(q_out->is_cuda() && q_out->scalar_type() == torch::kUInt8 && q_out->dim() == 2 && q_out->stride(1) == 1 &&
+                    q_out->size(0) >= B * N && q_out->size(1) >= 3 * D && q_out->stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(q_out->data_ptr()) % 4 == 0,
+                "attn_bwd: q_out uint8 [B*N][>= 3D], row stride a multiple of 4");
+    TORCH_CHECK(q_scale.has_value() && q_scale->defined() && q_amax.has_value() && q_amax->defined() && q_amax->is_cuda() &&
+                    q_amax->scalar_type() == torch::kInt32,
+                "attn_bwd: q_out needs q_scale (f32) and q_amax (int32)");
+    qp = q_out->data_ptr<uint8_t>();
+    ldq = q_out->stride(0);
+    qs = f32(*q_scale, "q_scale");
+    qa = reinterpret_cast<unsigned*>(q_amax->data_ptr());
+  }
+  float* dbias_arg = pipe && dbias_part.defined() ? dbias_part.data_ptr<float>() : old_db ? old_part.data_ptr<float>() : nullptr;
+  float* bpart_arg = !pipe && dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr;
+  // pre-pass outputs of the generic backward (per-query delta, lastkey path: ds_last; slab path: dQ slabs)
+  auto ws = torch::empty({pvr_attn_bwd_ws_floats((int)B, (int)N, (int)H, (int)D, old_db, has_drop)},
+                          qkv.options().dtype(torch::kFloat32));
+  const hipError_t err = pvr_attn_bwd(bf(qkv, "qkv"), lds[0], bf(out, "out"), lds[2], bf(dout, "dout"), lds[1], f32(lse, "lse"),
+                                      bf_mut(dqkv, "dqkv"), lds[3], dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
+                                      dbias_arg, bpart_arg, ws.data_ptr<float>(), (int)B, (int)N, (int)H, (int)D, (float)scale,
+                                      drop.seed, (uint64_t)seed_offset, drop.thr, drop.scale, qp, ldq, qs, qa, q_only && qp ? 1 : 0,
+                                      stream());
   // a persistent accumulator is re-zeroed only by a completed backward: after a failed launch it
   // may hold stale partial sums, so it is dropped (re-created zeroed by the next call)
   if (err != hipSuccess && dq_rezero) dq_workspace(0, qkv.options(), true);
   check(err, "attn_bwd");
   if (want_db) {
-    if (pipe)
+    if (parts)
       attn_dbias_reduce(dbias_part, B, H, *dbias);
-    else if (dbias_part.defined())
-      dbias->add_(dbias_part.sum(0));
+    else if (old_db)
+      dbias->add_(old_part.sum(0));
     else
       dbias->add_(dqkv.sum(0, false, torch::kFloat32));
   }
@@ -1019,6 +1056,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
         py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none(),
-        py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0);
+        py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0, py::arg("q_out") = py::none(),
+        py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none(), py::arg("q_only") = false);
+  m.def("attn_bwd_q8_ok", &attn_bwd_q8_ok, "attn_bwd can write dQKV's e5m2 copy for this shape");
   m.def("arch", []() { return std::string("gfx950"); });
 }

@@ -87,6 +87,7 @@ class PatchEmbedFn(torch.autograd.Function):
 
 
 LN_BWD_FP8_COPY = True  # the LayerNorm backward writes dx1 / dz2's e5m2 copies (False: quantize passes, A/B)
+ATTN_BWD_FP8_COPY = True  # the attention backward writes dQKV's e5m2 copy (False: a quantize pass, A/B)
 # test hook: bf16 outputs left unwritten on the fp8 path (only their fp8 copies are consumed) are
 # filled with NaN, so any reader of one would poison the loss / gradients (tests/kernel_checks.py)
 POISON_SKIPPED = False
@@ -338,15 +339,30 @@ class EncoderBlockFn(torch.autograd.Function):
         side_db = False
         db_part = None
         prow = ext.attn_bwd_bias_rows(B, N, H, D, aseed is not None) if gbqkv is not None else 0
+        fp8_qkv = f8d is not None and f8d[0].wgrad_ready(f8d[1], 3, 0) and store.bf16_t(wqkv) is not None
+        # fp8: dQKV's e5m2 copy (grad slot 3: the qkv dgrad and weight-gradient operand) written by the
+        # attention backward's own stores once the slot is calibrated (generic kernels)
+        q8kw, q8res = {}, None
+        if fp8_qkv and ATTN_BWD_FP8_COPY:
+            prod = f8d[0].grad_producer(f8d[1], 3)
+            if prod is not None and ext.attn_bwd_q8_ok(B, N, H, D, aseed is not None):
+                meta, slot = prod
+                q8 = torch.empty(T, 3 * D, dtype=torch.uint8, device=do.device)
+                # dQKV's bf16 copy is not stored when every reader takes the e5m2 copy: the qkv dgrad
+                # and weight gradient (fp8_qkv) and the bias gradient (kernel partials, prow > 0)
+                q8_only = prow > 0 and DGRAD_TAP is None and T >= 256
+                q8kw = dict(q_out=q8, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1], q_only=q8_only)
+                q8res = (q8, meta.dscale[slot:slot + 1])
         if prow > 0:
-            # the pipelined / chunked attention backward emits per-(image, head, query block or key
-            # chunk) column sums of dQ and dV (the v-bias gradient; the k bias has none); only their
-            # small reduction remains (side stream), no pass over dQKV
-            db_part = torch.empty(B * H, prow, 192, dtype=torch.float32, device=do.device)
-            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part)
+            # the attention backward emits per-(image, head, query block) column sums of dQ and dO
+            # (= sum_k dV: the v-bias gradient; the k bias has none); only their small reduction
+            # remains (side stream), no pass over dQKV
+            db_part = torch.empty(B * H, prow, 3 * (D // H), dtype=torch.float32, device=do.device)
+            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, db_part, **q8kw)
+            _poison(dqkv, q8kw.get("q_only", False))
         else:
             # other shapes: the in_proj bias gradient is a column sum of dQKV on the side stream
-            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, None, aseed, aoff, ap)
+            dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, scale, None, None, aseed, aoff, ap, **q8kw)
             side_db = gbqkv is not None
 
         def attn_wgrads():
@@ -367,7 +383,9 @@ class EncoderBlockFn(torch.autograd.Function):
             if gwqkv is not None:
                 wgrad(dqkv, xn1, gwqkv, 3, 0)
 
-        if f8d is not None and f8d[0].wgrad_ready(f8d[1], 3, 0) and store.bf16_t(wqkv) is not None:
+        if q8res is not None:
+            pre_q[3] = q8res
+        elif fp8_qkv:
             # dQKV's e5m2 copy now, so the side-stream qkv weight gradient transposes it (the dgrad uses it too).
             # With a column-sum in_proj bias gradient (generic attention path) and a calibrated slot, ONE
             # pass over dQKV writes both: the bias gradient (all three slices, exact with or without

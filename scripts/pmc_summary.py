@@ -12,8 +12,8 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    name = re.sub(r"\(.*", "", name)
-    return name.replace("pvr::(anonymous namespace)::", "").replace("void ", "")[:70]
+    name = name.replace("pvr::(anonymous namespace)::", "").replace("void ", "")
+    return re.sub(r"\(.*", "", name)[:70]
 
 
 def main():

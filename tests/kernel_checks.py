@@ -538,6 +538,32 @@ def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
             lim(5e-3, 1e-2, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
 
 
+def check_attn_bwd_q8(B, N, H, dh=64, p=0.0):
+    """The attention backward's own e5m2 copy of dQKV (fp8 recipe, grad slot 3) vs quantizing its bf16
+    dQKV: same bytes up to the double rounding bf16 -> e5m2 (the kernel rounds the fp32 value once),
+    i.e. at most one e5m2 step apart on a tiny fraction of elements; the amax record is max |dQKV|."""
+    ext = _ext.ext()
+    D = H * dh
+    sc = 1.0 / math.sqrt(dh)
+    qkv = bf(rnd(B * N, 3 * D))
+    seed = torch.tensor([4321], dtype=torch.int64, device=DEV) if p > 0 else None
+    o, lse = ext.attn_fwd(qkv, B, N, H, sc, seed, 5 << 32, p)
+    do = bf(rnd(B * N, D))
+    qs = torch.tensor([3000.0], device=DEV)
+    amax = torch.zeros(1, dtype=torch.int32, device=DEV)
+    q8 = torch.full((B * N, 3 * D), 0xAB, dtype=torch.uint8, device=DEV)
+    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, sc, None, None, seed, 5 << 32, p, q_out=q8, q_scale=qs, q_amax=amax)
+    got = q8.view(torch.float8_e5m2).float()
+    ref = (dqkv.float() * qs).clamp(-57344, 57344).to(torch.float8_e5m2).float()
+    step = ref.abs() * 0.25 + 1e-30  # one e5m2 step (2 mantissa bits) at the reference magnitude
+    far = ((got - ref).abs() > step * 1.01).float().mean().item()
+    diff = (got != ref).float().mean().item()
+    am = amax.view(torch.float32).item()
+    am_ref = dqkv.float().abs().max().item()
+    m = {"beyond_one_step": far, "differ_frac": diff, "amax_rel": abs(am - am_ref) / am_ref}
+    return (f"attn_bwd e5m2 dQKV copy B{B} N{N} H{H} dh{dh} p{p}", m, {"beyond_one_step": 0, "differ_frac": 2e-3, "amax_rel": 8e-3})
+
+
 def check_attn_dropout(B, N, H, dh=64, p=0.1):
     """Attention-probability dropout: the forward's mask is the counter hash regenerated in PyTorch
     (rate ~ p), O and dQ|dK|dV match the fp32 reference under THAT mask (so forward and backward
@@ -949,7 +975,7 @@ def check_vit_fp8(B=4):
     return (f"vit fp8 fwd vs fp32, loss {losses[0]:.3f}->{losses[-1]:.3f}", m, lim(8.5e-2, 1e-1, loss_not_falling=0))
 
 
-def check_vit_fp8_bf16_skip(B=4, steps=4):
+def check_vit_fp8_bf16_skip(B=4, steps=4, image=64, images=None):
     """fp8 training with the bf16 copies that only fp8 consumers read left unwritten (xn1, xn2, h in
     the forward, dU and the linked dz in the backward, once their weight gradients run in fp8 from
     the e4m3 / e5m2 copies). Those unwritten tensors are filled with NaN (POISON_SKIPPED), so a
@@ -966,10 +992,11 @@ def check_vit_fp8_bf16_skip(B=4, steps=4):
     res = []
     for skip in (True, False):
         torch.manual_seed(0)
-        m = ViT(**dict(_FP8_CFG, mlp_dropout=0.1)).to(DEV).enable_fp8()
+        m = ViT(**dict(_FP8_CFG, mlp_dropout=0.1, image_size=image)).to(DEV).enable_fp8()
         opt = FusedAdam(m.parameters(), lr=1e-3)
-        x = torch.rand(B * 64, 3, 64, 64, device=DEV)
-        y = torch.randint(0, 10, (B * 64,), device=DEV)
+        nimg = images or B * 64
+        x = torch.rand(nimg, 3, image, image, device=DEV)
+        y = torch.randint(0, 10, (nimg,), device=DEV)
         fused_vit.DGRAD_TAP = None if skip else (lambda which, t: None)
         fused_vit.POISON_SKIPPED = skip
         try:
@@ -990,7 +1017,7 @@ def check_vit_fp8_bf16_skip(B=4, steps=4):
     m = {"grad_l2": errs(g0, g1)[0], "nonfinite": float(not (torch.isfinite(g0).all().item() and torch.isfinite(p0).all().item()
                                                           and all(math.isfinite(v) for v in l0))),
          "loss_diff": max(abs(a - b) for a, b in zip(l0, l1)), "param_l2": errs(p0, p1)[0]}
-    return (f"vit fp8 bf16-copy skips (NaN-poisoned) vs all copies written, {steps} steps (loss {l0[0]:.3f}->{l0[-1]:.3f})", m,
+    return (f"vit fp8 bf16-copy skips (NaN-poisoned) vs all copies written, {image} px, {steps} steps (loss {l0[0]:.3f}->{l0[-1]:.3f})", m,
             {"grad_l2": 1e-6, "nonfinite": 0, "loss_diff": 2e-3, "param_l2": 1e-3})  # measured grad_l2 2.9e-8
 
 
@@ -1435,6 +1462,11 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_fwd(3, 1, 2, 80),    # tiled forward with no tile: the last key alone
         lambda: check_attn_fwd(2, 65, 2, 80),   # one full 64-key tile + the last key
         lambda: check_attn_bwd(2, 257, 3, 80),
+        lambda: check_attn_bwd(2, 257, 3, 80, True),  # lastkey path + in-kernel bias partials (dh 80)
+        lambda: check_attn_bwd(2, 577, 2, 64, True),  # slab path + bias partials from the tail launch
+        lambda: check_attn_bwd_q8(2, 257, 3, 80),    # e5m2 dQKV copy: lastkey path (pre-pass writes key N - 1)
+        lambda: check_attn_bwd_q8(2, 577, 2, 64),    # slab path (body dK/dV, tail dQ)
+        lambda: check_attn_bwd_q8(3, 197, 2, 80, 0.1),  # one key block, attention dropout
         lambda: check_attn_bwd(3, 257, 4, 64),    # N = 256 + 1: key-block body + last-key kernel
         lambda: check_attn_bwd(2, 257, 2, 128),
         lambda: check_attn_bwd(1, 40, 2, 80),
@@ -1479,6 +1511,9 @@ def all_checks() -> List[Callable[[], Result]]:
         check_vit_fp8_dgrad,
         check_vit_fp8_wgrad,
         check_vit_fp8_bf16_skip,
+        # 257 tokens: the attention backward's lastkey path writes dQKV's e5m2 copy and the in_proj bias
+        # partials itself and stores no bf16 dQKV (poisoned here)
+        lambda: check_vit_fp8_bf16_skip(steps=4, image=256, images=8),
         check_fp8_nonfinite_recovery,
         lambda: check_xent(8, 1000),
         lambda: check_xent(3, 3),
