@@ -1434,7 +1434,8 @@ static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t
 // tiles at every head dim (64 KiB of LDS at dh 80: two workgroups per CU). QG 2 pads the query
 // count to 128 instead of 64: it is chosen only when that padding costs < 10 % more query rows
 // (L/16-384, N = 577: 640 either way, QG 2 0.399 vs 0.440 ms; H/14, N = 257: 384 vs 320 rows, QG 2
-// 0.376 vs 0.319 ms, scripts/attn_ab.py). g_attn_fwd_qg: 0 = that rule, 1 / 2 = forced (A/B).
+// 0.376 vs 0.319 ms, scripts/attn_ab.py). g_attn_fwd_qg: 0 = that rule, 1 / 2 = forced, 3 = QG 1 with
+// 64-key tiles at every head dim (A/B).
 int g_attn_fwd_qg = 0;
 static bool attn_fwd_use_qg2(int N) {
   if (g_attn_fwd_qg) return g_attn_fwd_qg == 2;
@@ -1461,6 +1462,7 @@ static hipError_t attn_fwd_tiled(const uint16_t* qkv, int64_t ld, uint16_t* out,
 template <int DH, bool DROP>
 static hipError_t attn_fwd_tiled_pick(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
                                       int D, float scale, const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
+  if (g_attn_fwd_qg == 3) return attn_fwd_tiled<DH, DROP, 1, 64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);  // A/B
   if (attn_fwd_use_qg2(N)) return attn_fwd_tiled<DH, DROP, 2, 64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
   return attn_fwd_tiled<DH, DROP, 1, (pvr::Hd<DH>::NH == 1 ? 64 : 32)>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
 }
@@ -1487,7 +1489,7 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
   return attn_fwd_tiled_pick<DH, false>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
 }
 
-extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg == 1 || qg == 2 ? qg : 0; }
+extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg >= 1 && qg <= 3 ? qg : 0; }
 
 // seed (optional): attention-probability dropout with keep threshold thr16 (see AttnDrop); the
 // backward must get the same seed / seed_off / thr16

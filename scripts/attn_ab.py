@@ -36,14 +36,15 @@ def timeit(fn, iters=10, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="l16_384,h14,b16")
-    ap.add_argument("--ab", default="", help="'fwd_qg': tiled forward with 2 vs 1 query groups per wave")
+    ap.add_argument("--ab", default="", help="'fwd_qg': tiled forward with 2 vs 1 query groups per wave vs 1 with 64-key tiles")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--bwd", action="store_true", help="also time the backward")
     a = ap.parse_args()
     ext = _ext.ext()
     variants = [("", lambda: None)]
     if a.ab == "fwd_qg":
-        variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1))]
+        variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1)),
+                    ("kt64", lambda: ext.set_attn_fwd_qg(3))]
     res = {}
     data = {}
     for name in a.shapes.split(","):
