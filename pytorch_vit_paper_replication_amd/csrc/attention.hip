@@ -456,19 +456,20 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   // dQ destination of this batch. dq_mode 0-2 with dq_acc: f32 atomics into the accumulator [N][D];
   // dq_mode 3 (key-block body of a multi-block head): plain f32 stores of this key block's partial
   // dQ into slab (L % nkb) of dq_acc [slabs][B*N][D] (6 TB/s stores instead of 1.3 TB/s atomics);
-  // dq_mode 4 (the tail launch after a mode-3 body): bf16 dQ = own partial + the nslab slabs;
+  // dq_mode 4 (the tail launch after a mode-3 body): its own partial into slab nslab, then the
+  // final pass at the end sums the nslab + 1 slabs of the pair in fixed order into bf16 dQ;
   // otherwise the bf16 gradient rows directly.
-  const bool slab_w = dq_mode == 3, slab_r = dq_mode == 4;
+  const bool slab_w = dq_mode == 3 || dq_mode == 4;
   // optional e5m2 copy of dQKV (the fp8 recipe's grad slot: dgrad and weight-gradient operand) with
   // the slot's delayed scale, written next to every final bf16 value, amax recorded per wave
   const bool q8kv = q8.out != nullptr;  // dK / dV: every launch writes final values
-  const bool q8on = q8kv && !slab_w;     // dQ: only the launch that writes the final dQ
+  const bool q8on = q8kv && !slab_w;     // dQ here: only a launch whose fragments are the final dQ
   float q8am = 0.f;
   const float q8s = q8kv ? *q8.qs : 1.f;
   const __amdgpu_buffer_rsrc_t q8rs = make_rsrc(q8.out + (int64_t)b * N * q8.ld, q8on ? clamp_bytes((int64_t)(N - 1) * q8.ld + D) : 0u);
-  float* dq_dst = dq_acc && slab_w ? dq_acc + (L % nkb) * slab_stride : dq_acc;
-  const __amdgpu_buffer_rsrc_t dqrs = dq_acc && !slab_r ? make_rsrc(dq_dst + (int64_t)b * N * D, clamp_bytes((int64_t)N * D * 4))
-                                                        : make_rsrc(dqkv + (int64_t)b * N * ld_dq, clamp_bytes(((int64_t)(N - 1) * ld_dq + D) * 2));
+  float* dq_dst = dq_acc && slab_w ? dq_acc + (dq_mode == 3 ? (L % nkb) : nslab) * slab_stride : dq_acc;
+  const __amdgpu_buffer_rsrc_t dqrs = dq_acc ? make_rsrc(dq_dst + (int64_t)b * N * D, clamp_bytes((int64_t)N * D * 4))
+                                             : make_rsrc(dqkv + (int64_t)b * N * ld_dq, clamp_bytes(((int64_t)(N - 1) * ld_dq + D) * 2));
 
   // own keys' K and V fragments (B operands): lane holds X[kw0 + 16f + li][32ks + 8g + j]
   v8s kf[2][C::KS], vf[2][C::KS];
@@ -672,23 +673,13 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] = fmaf(sl[r], kl_dq[kfr], acc[r]);
       }
-      float sadd[4] = {0.f, 0.f, 0.f, 0.f};
-      if (slab_r) {  // the body launch's partial slabs, summed in slab order (deterministic)
-        const uint32_t nbytes = clamp_bytes((int64_t)N * D * 4);
-        for (int sl = 0; sl < nslab; ++sl) {
-          const __amdgpu_buffer_rsrc_t srs = make_rsrc(dq_acc + sl * slab_stride + (int64_t)b * N * D, nbytes);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            sadd[r] += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(srs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0));
-        }
-      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float val = acc[r] * scale + sadd[r];
+        const float val = acc[r] * scale;
         cs += val;
         if (dq_acc && slab_w)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
-        else if (dq_acc && !slab_r)
+        else if (dq_acc)
           __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
         else if (!q8.only)
           __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dqrs, ((vq + r) * (uint32_t)ld_dq + col) * 2, 0, 0);
@@ -704,7 +695,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   }
   // bpart (the launch that writes the final dQ): this pair's q-bias partials, the column sums of the
   // wave's dQ fragments over all query blocks -> [bh][a][16e + li] (the pre-pass adds the v sums)
-  if (bpart) {
+  if (bpart && dq_mode != 4) {  // (mode 4: the final slab pass below writes them)
     int kfr = 0;
     for (int fr = wave; fr < 2 * C::NE && kfr < 2; fr += NW, ++kfr) {
       float cs = kfr == 0 ? dqb0 : dqb1;
@@ -830,6 +821,78 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         const v4f f = __builtin_bit_cast(v4f, v[u]);
         __builtin_amdgcn_raw_buffer_store_b64(v2u_{pack2bf(f[0], f[1]), pack2bf(f[2], f[3])}, ors_q, oo[u], 0, 0);
         if (dq_mode == 2) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, dqrs, ao[u], 0, 0);
+      }
+    }
+  }
+  // dq_mode 4: every key block of this pair stored its partial dQ as an f32 slab (the body launch
+  // before this one, this workgroup's own just now); sum the nslab + 1 slabs in slab order
+  // (deterministic) with coalesced 16-B loads and write the final dQ: bf16 (unless only the fp8 copy
+  // is wanted), its e5m2 copy, and the q-bias partials (column sums in a fixed order).
+  // (no agent-scope fence: the body launch completed before this one started, and this workgroup's
+  // own slab stores are acknowledged by the wait below; the loads go through this XCD's L2.)
+  if (dq_mode == 4 && dq_acc) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    constexpr int C4 = DH / 4, U = 4;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef uint32_t v2u_ __attribute__((ext_vector_type(2)));
+    const int RG = (int)blockDim.x / C4;  // row groups; thread = (row group, fixed 4-column chunk)
+    const int chunk = (int)threadIdx.x % C4, rg = (int)threadIdx.x / C4;
+    const bool tact = rg < RG;
+    const uint32_t sbytes = clamp_bytes((int64_t)N * D * 4);
+    const __amdgpu_buffer_rsrc_t ors_q = make_rsrc(dqkv + (int64_t)b * N * ld_dq + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_dq + DH) * 2));
+    float csum[4] = {0.f, 0.f, 0.f, 0.f};
+    float am = 0.f;
+    for (int r0 = rg; r0 < N; r0 += RG * U) {
+      v4f sum[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum[u] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl <= nslab; ++sl) {
+        const __amdgpu_buffer_rsrc_t srs = make_rsrc(dq_acc + sl * slab_stride + (int64_t)b * N * D, sbytes);
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // rows past N (and idle threads) read as zero
+          const int qrow = tact ? r0 + u * RG : N;
+          v[u] = __builtin_amdgcn_raw_buffer_load_b128(srs, ((uint32_t)qrow * (uint32_t)D + (uint32_t)(h * DH + 4 * chunk)) * 4, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) sum[u] += __builtin_bit_cast(v4f, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int qrow = r0 + u * RG;
+        if (!tact || qrow >= N) continue;
+        const v4f sv = sum[u];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          csum[j] += sv[j];
+          am = nan_max(am, fabsf(sv[j]));
+        }
+        if (!q8.only)
+          __builtin_amdgcn_raw_buffer_store_b64(v2u_{pack2bf(sv[0], sv[1]), pack2bf(sv[2], sv[3])}, ors_q,
+                                                ((uint32_t)qrow * (uint32_t)ld_dq + 4 * chunk) * 2, 0, 0);
+        if (q8kv)
+          *(uint32_t*)(q8.out + ((int64_t)b * N + qrow) * q8.ld + h * DH + 4 * chunk) =
+              (uint32_t)pack2_fp8<1, true>(sv[2] * q8s, sv[3] * q8s, pack2_fp8<1, false>(sv[0] * q8s, sv[1] * q8s, 0));
+      }
+    }
+    if (q8kv) {
+      am = wave_max_nan(am);
+      if (lane == 0) amax_record(q8.amax, am);
+    }
+    if (bpart) {  // q-bias partials: the row groups' column sums reduced in a fixed order
+      float* red = (float*)smem;
+      __syncthreads();  // every wave is past its LDS use
+      if (tact) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[rg * DH + 4 * chunk + j] = csum[j];
+      }
+      __syncthreads();
+      for (int d = (int)threadIdx.x; d < DH; d += (int)blockDim.x) {
+        float t = 0.f;
+        for (int g2 = 0; g2 < RG; ++g2) t += red[g2 * DH + d];
+        bpart[((int64_t)bh * 3 + 0) * DH + d] = t;
+        bpart[((int64_t)bh * 3 + 1) * DH + d] = 0.f;
       }
     }
   }
@@ -1619,7 +1682,7 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
   // pre-pass: delta (and, on the lastkey path, key N - 1's dS / dK / dV)
   float* dlt = ws;
   float* dsl = lastkey ? ws + (int64_t)B * H * N : nullptr;
-  float* slab = slab_path ? ws + 2 * (int64_t)B * H * N : nullptr;  // [N / KB][B*N][D] f32 partial dQ
+  float* slab = slab_path ? ws + 2 * (int64_t)B * H * N : nullptr;  // [N / KB + 1][B*N][D] f32 partial dQ
   if (lastkey)
     hipLaunchKernelGGL((attn_bwd_prep_kernel<DH, true>), dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dlt, dsl,
                        bpart, dqkv, ld_dq, N, H, D, scale, q8);
@@ -1645,10 +1708,11 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
     // in full-size workgroups, the tail in workgroups sized for it, instead of 8-wave workgroups with
     // 3 live waves holding a CU each (818 vs 862 us at B64 H16). A 1-key tail (257 = 256 + 1, the
     // CLS token of 224/14) takes the lastkey path above instead.
-    // The body's key blocks store their partial dQ as f32 slabs (plain stores); the tail launch,
-    // one workgroup per (batch, head) running after the body, adds them to its own partial and
-    // writes bf16 dQ: no atomics, no zeroed accumulator, no conversion pass
-    // (ViT-L/16@384 b128: 1.16 ms per layer with f32 atomics, profiles/r4/attn_ab*).
+    // Every key block stores its partial dQ as an f32 slab (plain stores); the tail launch, one
+    // workgroup per (batch, head) running after the body, then sums the pair's slabs in a coalesced
+    // final pass into bf16 dQ: no atomics, no zeroed accumulator, no separate conversion pass
+    // (ViT-L/16@384 b128: 1.16 ms per layer with f32 atomics, profiles/r4/attn_ab*; summing the
+    // slabs per dQ fragment inside the tail's block loop instead: 1.21 ms).
     const int nslab = (N - rem) / KB;
     const int64_t sstride = (int64_t)B * N * D;
     launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
@@ -1682,7 +1746,7 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
 // floats of the f32 scratch pvr_attn_bwd needs (per-query delta and, on the lastkey path, ds_last)
 extern "C" int64_t pvr_attn_bwd_ws_floats(int B, int N, int H, int D, int dbias, int drop) {
   int64_t n = 2 * (int64_t)B * H * N;
-  if (attn_bwd_slab_path(N, dbias != 0, drop != 0)) n += (int64_t)(N / (32 * pvr_attn_bwd_waves(N))) * B * N * D;
+  if (attn_bwd_slab_path(N, dbias != 0, drop != 0)) n += (int64_t)(N / (32 * pvr_attn_bwd_waves(N)) + 1) * B * N * D;
   return n;
 }
 
