@@ -433,14 +433,14 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const int kw0 = kb0 + wave * 32;
   PVR_ASSERT(kb0 < N && L < (int)gridDim.x && (KB & (KB - 1)) == 0);
 
-  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh]) | dS [32][KB] | 2 x (lse | delta | ds_last) [3][256]
+  // LDS carve: K image [KB][dh] | 2 x (Q blk [32][dh] | dO blk [32][dh]) | 2 x dS [32][KB] | 2 x (lse | delta | ds_last) [3][256]
   // Q / dO rows and the per-query constants of query block qb+1 are staged while block qb is processed.
   // delta = rowsum(dO * O) comes from attn_bwd_prep_kernel (one pass over dO and O instead of every
   // wave dotting staged O rows per block); ds_last (lastkey path): dS of key N - 1 per query.
   char* kimg = smem;
   char* qdo = kimg + KB * RB;
-  char* dsimg = qdo + 4 * QB * RB;
-  float* s_ld = (float*)(dsimg + QB * KB * 2);
+  char* dsimg = qdo + 4 * QB * RB;  // two dS^T buffers (software pipelining over query blocks)
+  float* s_ld = (float*)(dsimg + 2 * QB * KB * 2);
   typedef uint32_t v2u __attribute__((ext_vector_type(2)));
   // dS^T image [key_local][32 queries]: 64-B rows of 8-B units (4 queries), unit XOR (key>>1)&7
   auto ds_off = [](int key, int u) { return key * 64 + ((u ^ ((key >> 1) & 7)) << 3); };
@@ -530,11 +530,77 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   float dqb0 = 0.f, dqb1 = 0.f;  // q-bias gradient partials (column sums of this wave's dQ fragments)
   // dQ stores this wave issues per query block (younger than the next block's staging DMAs)
   const int nst = wave < 2 * C::NE ? 4 * ((2 * C::NE - 1 - wave) / NW + 1) : 0;
+  constexpr int DS_BYTES = QB * 32 * 2;  // per 32 keys of one dS^T buffer
+  const int ds_buf = KB / 32 * DS_BYTES;
+  // dQ of query block qbp = sum_key dS[q][key] K[key][d] from dS^T buffer (qbp & 1); 2*NE output
+  // fragments split over the waves. Both operands by transposed reads (dS^T rows 32ks + 8g + q4 (+4),
+  // queries 16a + 4p4; K rows the same keys, dims 16e + 4p4), four key slices per LDS wait; the
+  // stores are buffer ops, so queries past N drop in the range check and every wave issues exactly 4
+  // per fragment. slq: the block's dS of key N - 1 at this lane's fragment rows (lastkey path).
+  auto dq_block = [&](int qbp, const v4f (&slq)[2]) {
+    const char* dsb = dsimg + (qbp & 1) * ds_buf;
+    int kfr = 0;
+    for (int fr = wave; fr < 2 * C::NE; fr += NW, ++kfr) {
+      const int a = fr / C::NE, e = fr % C::NE;
+      v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
+      const char* kt0 = kimg + lds_off(KB, 8 * g + q4, 2 * e + (p4 >> 1)) + 8 * (p4 & 1);
+      const char* kt1 = kimg + lds_off(KB, 8 * g + q4 + 4, 2 * e + (p4 >> 1)) + 8 * (p4 & 1);
+      const char* dt0 = dsb + ds_off(8 * g + q4, 4 * a + p4);
+      const char* dt1 = dsb + ds_off(8 * g + q4 + 4, 4 * a + p4);
+      auto batch = [&](auto k0c) {
+        constexpr int k0 = decltype(k0c)::value;
+        v4s klo[4], khi[4], slo[4], shi[4];
+        static_for<0, 4>([&](auto jc) {
+          constexpr int ks = k0 + decltype(jc)::value;
+          klo[ks - k0] = ds_read_tr_async_at<4096 * ks>(kt0);
+          khi[ks - k0] = ds_read_tr_async_at<4096 * ks>(kt1);
+          slo[ks - k0] = ds_read_tr_async_at<2048 * ks>(dt0);
+          shi[ks - k0] = ds_read_tr_async_at<2048 * ks>(dt1);
+        });
+        lds_wait();
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (k0 + jj < nks_dq) acc = mfma16(cat44(slo[jj], shi[jj]), cat44(klo[jj], khi[jj]), acc);
+      };
+      batch(std::integral_constant<int, 0>{});
+      if (nks_dq > 4) batch(std::integral_constant<int, 4>{});
+      const uint32_t vq = (uint32_t)(qbp * QB + 16 * a + 4 * g), col = (uint32_t)(h * DH + 16 * e + li);
+      float cs = 0.f;  // queries past N have dS = 0, so their dQ is exactly 0
+      if (dsl) {  // + dS[q][N - 1] K[N - 1] (lastkey path: key N - 1 is not in any key block)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(slq[kfr & 1][r], kl_dq[kfr & 1], acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float val = acc[r] * scale;
+        cs += val;
+        if (dq_acc && slab_w)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
+        else if (dq_acc)
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
+        else if (!q8.only)
+          __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dqrs, ((vq + r) * (uint32_t)ld_dq + col) * 2, 0, 0);
+        if (q8on) {
+          q8am = nan_max(q8am, fabsf(val));
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pack2_fp8<1, false>(val * q8s, 0.f, 0) & 0xFF), q8rs,
+                                               (vq + r) * (uint32_t)q8.ld + col, 0, 0);
+        }
+      }
+      if (kfr == 0) dqb0 += cs;  // q-bias gradient: this fragment's column sums across query blocks
+      else dqb1 += cs;           // (at most two fragments per wave: host guarantees 2*NE <= 2*NW)
+    }
+  };
+  // Software-pipelined over query blocks, one barrier per block: block qb's S / dP / dV / dK and its
+  // dS^T write (buffer qb & 1) run in the same interval as the dQ of block qb - 1 (buffer (qb-1) & 1,
+  // written before this block's barrier), so the dQ product's LDS reads and MFMAs interleave with
+  // the next block's instead of waiting behind a second barrier.
+  v4f slq_prev[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
   for (int qb = 0; qb < nqb; ++qb) {
     const int q0 = qb * QB;
-    // block qb landed (issued one iteration ago; the previous block's dQ stores may stay in
-    // flight); every wave is done with slot (qb+1)&1 and with dS
-    if (qb == 0 || nst < 4)
+    // block qb landed (issued one iteration ago, before the dQ stores of block qb - 2, which may
+    // stay in flight); every wave is done with slot (qb+1)&1, with dS buffer qb&1 (block qb - 2's)
+    // and has written dS buffer (qb-1)&1
+    if (qb < 2 || nst < 4)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (nst < 8)
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -549,6 +615,17 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     const char* doimg = qimg + QB * RB;
     const float* s_lse = s_ld + (qb & 1) * 768;
     const float* s_dl = s_lse + 256;
+    char* dsw = dsimg + (qb & 1) * ds_buf;
+    // this block's dS of key N - 1 at the rows of this wave's dQ fragments: its constants slot is
+    // restaged (block qb + 2) before the dQ of this block runs (next iteration)
+    v4f slq_cur[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+    if (dsl) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int fr = wave + j * NW;
+        if (fr < 2 * C::NE) slq_cur[j] = *(const v4f*)(s_lse + 512 + 16 * (fr / C::NE) + 4 * g);
+      }
+    }
 
     if (active) {
     // S[q][key], dP[q][key]: lane holds [q = 16a + 4g + r][key = kw0 + 16f + li]; dP starts from
@@ -628,74 +705,23 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         const v4u w = __builtin_bit_cast(v4u, sf[f]);
-        *(__attribute__((address_space(3))) v2u*)(dsimg + dsw0 + 1024 * f) = v2u{w[0], w[1]};
-        *(__attribute__((address_space(3))) v2u*)(dsimg + dsw1 + 1024 * f) = v2u{w[2], w[3]};
+        *(__attribute__((address_space(3))) v2u*)(dsw + dsw0 + 1024 * f) = v2u{w[0], w[1]};
+        *(__attribute__((address_space(3))) v2u*)(dsw + dsw1 + 1024 * f) = v2u{w[2], w[3]};
       }
     }
     }  // active
-    // dS visible to every wave; a raw barrier, so the next block's DMAs stay in flight
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // dQ[q][d] = scale * sum_key dS[q][key] K[key][d]; 2*NE output fragments split over the waves.
-    // Both operands by transposed reads (dS^T rows 32ks + 8g + q4 (+4), queries 16a + 4p4; K rows
-    // the same keys, dims 16e + 4p4), four key slices per LDS wait; the stores are buffer ops, so
-    // queries past N drop in the range check and every wave issues exactly 4 per fragment.
-    int kfr = 0;
-    for (int fr = wave; fr < 2 * C::NE; fr += NW, ++kfr) {
-      const int a = fr / C::NE, e = fr % C::NE;
-      v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-      const char* kt0 = kimg + lds_off(KB, 8 * g + q4, 2 * e + (p4 >> 1)) + 8 * (p4 & 1);
-      const char* kt1 = kimg + lds_off(KB, 8 * g + q4 + 4, 2 * e + (p4 >> 1)) + 8 * (p4 & 1);
-      const char* dt0 = dsimg + ds_off(8 * g + q4, 4 * a + p4);
-      const char* dt1 = dsimg + ds_off(8 * g + q4 + 4, 4 * a + p4);
-      auto batch = [&](auto k0c) {
-        constexpr int k0 = decltype(k0c)::value;
-        v4s klo[4], khi[4], slo[4], shi[4];
-        static_for<0, 4>([&](auto jc) {
-          constexpr int ks = k0 + decltype(jc)::value;
-          klo[ks - k0] = ds_read_tr_async_at<4096 * ks>(kt0);
-          khi[ks - k0] = ds_read_tr_async_at<4096 * ks>(kt1);
-          slo[ks - k0] = ds_read_tr_async_at<2048 * ks>(dt0);
-          shi[ks - k0] = ds_read_tr_async_at<2048 * ks>(dt1);
-        });
-        lds_wait();
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (k0 + j < nks_dq) acc = mfma16(cat44(slo[j], shi[j]), cat44(klo[j], khi[j]), acc);
-      };
-      batch(std::integral_constant<int, 0>{});
-      if (nks_dq > 4) batch(std::integral_constant<int, 4>{});
-      const uint32_t vq = (uint32_t)(q0 + 16 * a + 4 * g), col = (uint32_t)(h * DH + 16 * e + li);
-      float cs = 0.f;  // queries past N have dS = 0, so their dQ is exactly 0
-      if (dsl) {  // + dS[q][N - 1] K[N - 1] (lastkey path: key N - 1 is not in any key block)
-        const v4f sl = *(const v4f*)(s_ld + (qb & 1) * 768 + 512 + 16 * a + 4 * g);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = fmaf(sl[r], kl_dq[kfr], acc[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float val = acc[r] * scale;
-        cs += val;
-        if (dq_acc && slab_w)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
-        else if (dq_acc)
-          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, dqrs, ((vq + r) * (uint32_t)D + col) * 4, 0, 0);
-        else if (!q8.only)
-          __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dqrs, ((vq + r) * (uint32_t)ld_dq + col) * 2, 0, 0);
-        if (q8on) {
-          q8am = nan_max(q8am, fabsf(val));
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pack2_fp8<1, false>(val * q8s, 0.f, 0) & 0xFF), q8rs,
-                                               (vq + r) * (uint32_t)q8.ld + col, 0, 0);
-        }
-      }
-      if (kfr == 0) dqb0 += cs;  // q-bias gradient: this fragment's column sums across query blocks
-      else dqb1 += cs;           // (at most two fragments per wave: host guarantees 2*NE <= 2*NW)
-    }
+    if (qb > 0) dq_block(qb - 1, slq_prev);
+    slq_prev[0] = slq_cur[0];
+    slq_prev[1] = slq_cur[1];
   }
+  // the last block's dQ, once every wave's dS^T of it is written
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  dq_block(nqb - 1, slq_prev);
   // bpart (the launch that writes the final dQ): this pair's q-bias partials, the column sums of the
   // wave's dQ fragments over all query blocks -> [bh][a][16e + li] (the pre-pass adds the v sums)
-  if (bpart && dq_mode != 4) {  // (mode 4: the final slab pass below writes them)
+  if (bpart && dq_mode == 0) {  // (modes 1, 2, 4: the final pass below writes them)
     int kfr = 0;
     for (int fr = wave; fr < 2 * C::NE && kfr < 2; fr += NW, ++kfr) {
       float cs = kfr == 0 ? dqb0 : dqb1;
@@ -790,47 +816,18 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     q8am = wave_max_nan(q8am);
     if (lane == 0) amax_record(q8.amax, q8am);
   }
-  // dq_mode 1 / 2 (the last launch, one workgroup per (batch, head)): the other key blocks' dQ
-  // atomics landed before this launch started and this workgroup's own are acknowledged after the
-  // wait below, so it converts the pair's accumulated dQ rows to bf16 (no separate pass over the
-  // whole accumulator) and, in mode 2, zeroes them again for the next use of a persistent workspace
-  if ((dq_mode == 1 || dq_mode == 2) && dq_acc) {
-    // (no agent-scope fence: it would write back the whole L2. This workgroup's atomics performed in
-    // its XCD's L2, which its loads below go through; the CU's L1 holds no line of these rows.)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // 8 independent 16-B loads in flight per thread, then their stores (buffer ops: rows past N drop)
-    constexpr int C4 = DH / 4, U = 8;
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    typedef uint32_t v2u_ __attribute__((ext_vector_type(2)));
-    const __amdgpu_buffer_rsrc_t ors_q = make_rsrc(dqkv + (int64_t)b * N * ld_dq + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_dq + DH) * 2));
-    const int n4 = N * C4;
-    for (int i0 = 0; i0 < n4; i0 += U * (int)blockDim.x) {
-      v4u v[U];
-      uint32_t ao[U], oo[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * (int)blockDim.x + (int)threadIdx.x;
-        const int qrow = i < n4 ? i / C4 : N, col = 4 * (i - (i / C4) * C4);
-        ao[u] = ((uint32_t)qrow * (uint32_t)D + (uint32_t)(h * DH + col)) * 4;
-        oo[u] = ((uint32_t)qrow * (uint32_t)ld_dq + (uint32_t)col) * 2;
-        v[u] = __builtin_amdgcn_raw_buffer_load_b128(dqrs, ao[u], 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const v4f f = __builtin_bit_cast(v4f, v[u]);
-        __builtin_amdgcn_raw_buffer_store_b64(v2u_{pack2bf(f[0], f[1]), pack2bf(f[2], f[3])}, ors_q, oo[u], 0, 0);
-        if (dq_mode == 2) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, dqrs, ao[u], 0, 0);
-      }
-    }
-  }
-  // dq_mode 4: every key block of this pair stored its partial dQ as an f32 slab (the body launch
-  // before this one, this workgroup's own just now); sum the nslab + 1 slabs in slab order
-  // (deterministic) with coalesced 16-B loads and write the final dQ: bf16 (unless only the fp8 copy
-  // is wanted), its e5m2 copy, and the q-bias partials (column sums in a fixed order).
-  // (no agent-scope fence: the body launch completed before this one started, and this workgroup's
-  // own slab stores are acknowledged by the wait below; the loads go through this XCD's L2.)
-  if (dq_mode == 4 && dq_acc) {
+  // Final dQ pass of the last launch of a multi-block head (one workgroup per (batch, head)):
+  //   dq_mode 1 / 2: the other key blocks' f32 atomics landed before this launch started and this
+  //     workgroup's own are acknowledged after the wait below: convert the pair's accumulated rows
+  //     (and, in mode 2, zero them again for the next use of a persistent workspace);
+  //   dq_mode 4: every key block stored its partial dQ as an f32 slab (the body launch before this
+  //     one, this workgroup's own just now): sum the nslab + 1 slabs in slab order (deterministic).
+  // Coalesced 16-B loads; writes the final dQ: bf16 (unless only the fp8 copy is wanted), its e5m2
+  // copy, and the q-bias partials (column sums in a fixed order).
+  // (no agent-scope fence: it would write back the whole L2. The body launch completed before this
+  // one started; this workgroup's own stores / atomics performed in its XCD's L2, which the loads
+  // below go through; the CU's L1 holds no line of these rows.)
+  if ((dq_mode == 1 || dq_mode == 2 || dq_mode == 4) && dq_acc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     constexpr int C4 = DH / 4, U = 4;
@@ -847,16 +844,22 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       v4f sum[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) sum[u] = v4f{0.f, 0.f, 0.f, 0.f};
-      for (int sl = 0; sl <= nslab; ++sl) {
+      const int nsrc = dq_mode == 4 ? nslab + 1 : 1;
+      for (int sl = 0; sl < nsrc; ++sl) {
         const __amdgpu_buffer_rsrc_t srs = make_rsrc(dq_acc + sl * slab_stride + (int64_t)b * N * D, sbytes);
         v4u v[U];
+        uint32_t off[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {  // rows past N (and idle threads) read as zero
           const int qrow = tact ? r0 + u * RG : N;
-          v[u] = __builtin_amdgcn_raw_buffer_load_b128(srs, ((uint32_t)qrow * (uint32_t)D + (uint32_t)(h * DH + 4 * chunk)) * 4, 0, 0);
+          off[u] = ((uint32_t)qrow * (uint32_t)D + (uint32_t)(h * DH + 4 * chunk)) * 4;
+          v[u] = __builtin_amdgcn_raw_buffer_load_b128(srs, off[u], 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) sum[u] += __builtin_bit_cast(v4f, v[u]);
+        for (int u = 0; u < U; ++u) {
+          sum[u] += __builtin_bit_cast(v4f, v[u]);
+          if (dq_mode == 2) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, srs, off[u], 0, 0);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1593,17 +1596,22 @@ static bool attn_bwd_lastkey_path(int N, bool dbias, bool drop) {
   return (N + KB - 1) / KB == 2 && N % KB == 1 && !dbias && !drop && N <= 512;
 }
 
-// key-block body + short tail with dQ through f32 slabs (see attn_bwd_generic)
-static bool attn_bwd_slab_path(int N, bool dbias, bool drop) {
+// key-block body + a short tail launch (ViT-L/16@384: 577 = 2 x 256 + 65; see attn_bwd_generic)
+static bool attn_bwd_tail_split(int N, bool dbias, bool drop) {
   const int KB = 32 * pvr_attn_bwd_waves(N);
   const int rem = N % KB;
   return !attn_bwd_lastkey_path(N, dbias, drop) && (N + KB - 1) / KB > 1 && rem >= 16 && rem <= 128 && !dbias;
 }
+// dQ of the tail-split path through f32 slabs summed by the tail (1) or f32 atomics converted by
+// the tail (0, default: 1.15 vs 1.22 ms per ViT-L/16@384 b128 layer, profiles/r4/ab8, ab9)
+int g_attn_bwd_slab = 0;
+static bool attn_bwd_slab_path(int N, bool dbias, bool drop) { return g_attn_bwd_slab && attn_bwd_tail_split(N, dbias, drop); }
+extern "C" void pvr_set_attn_bwd_slab(int on) { g_attn_bwd_slab = on ? 1 : 0; }
 
 // the generic backward's kernels write every final dQ value (no f32 atomics + conversion pass)
 static bool attn_bwd_final_dq_in_kernel(int N, bool dbias, bool drop) {
   const int KB = 32 * pvr_attn_bwd_waves(N);
-  return attn_bwd_lastkey_path(N, dbias, drop) || attn_bwd_slab_path(N, dbias, drop) || (N + KB - 1) / KB == 1;
+  return attn_bwd_lastkey_path(N, dbias, drop) || attn_bwd_tail_split(N, dbias, drop) || (N + KB - 1) / KB == 1;
 }
 
 // the generic backward can emit the in_proj bias gradient as [B*H][1][3*dh] partials (q sums of
@@ -1614,7 +1622,7 @@ static bool attn_bwd_bpart_ok(int N, int DH) {
   const int NE = DH / 16;
   const int KB = 32 * pvr_attn_bwd_waves(N);
   if (attn_bwd_lastkey_path(N, false, false)) return NE <= pvr_attn_bwd_waves(N);
-  if (attn_bwd_slab_path(N, false, false)) return NE <= pvr_attn_bwd_waves(N % KB);
+  if (attn_bwd_tail_split(N, false, false)) return true;  // the tail's final dQ pass writes them
   return (N + KB - 1) / KB == 1 && NE <= pvr_attn_bwd_waves(N);
 }
 
@@ -1665,13 +1673,14 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
   const int nkb = (N + KB - 1) / KB;
   const bool lastkey = attn_bwd_lastkey_path(N, dbias != nullptr, DROP);
   const int rem_ = N % KB;
-  const bool slab_path = !lastkey && nkb > 1 && rem_ >= 16 && rem_ <= 128 && !dbias;
+  const bool tail_split = !lastkey && nkb > 1 && rem_ >= 16 && rem_ <= 128 && !dbias;
+  const bool slab_path = tail_split && g_attn_bwd_slab;
   if (nkb > 1 && !dq_acc && !lastkey && !slab_path) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   if (!ws) return hipErrorInvalidValue;
   const int RB = 128 * Hd<DH>::NH;
   // K image | 2 x (Q | dO) blocks | dS | 2 x (lse | delta | ds_last) 1 KiB DMA slots
-  auto smem_of = [&](int kb) { return (size_t)kb * RB + 4 * 32 * RB + 32 * kb * 2 + 6 * 1024; };
+  auto smem_of = [&](int kb) { return (size_t)kb * RB + 4 * 32 * RB + 2 * 32 * kb * 2 + 6 * 1024; };
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)attn_bwd_kernel<DH, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1703,20 +1712,24 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
     return hipGetLastError();
   }
   const int rem = N % KB;
-  if (slab_path) {
+  if (tail_split) {
     // N = a multiple of KB plus a short tail (ViT-L/16@384: 577 = 2 x 256 + 65): the KB-aligned body
     // in full-size workgroups, the tail in workgroups sized for it, instead of 8-wave workgroups with
     // 3 live waves holding a CU each (818 vs 862 us at B64 H16). A 1-key tail (257 = 256 + 1, the
     // CLS token of 224/14) takes the lastkey path above instead.
-    // Every key block stores its partial dQ as an f32 slab (plain stores); the tail launch, one
-    // workgroup per (batch, head) running after the body, then sums the pair's slabs in a coalesced
-    // final pass into bf16 dQ: no atomics, no zeroed accumulator, no separate conversion pass
-    // (ViT-L/16@384 b128: 1.16 ms per layer with f32 atomics, profiles/r4/attn_ab*; summing the
-    // slabs per dQ fragment inside the tail's block loop instead: 1.21 ms).
-    const int nslab = (N - rem) / KB;
-    const int64_t sstride = (int64_t)B * N * D;
-    launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
-    launch(pvr_attn_bwd_waves(rem), N - rem, N, 4, slab, sstride, nslab, bpart);
+    // The tail launch, one workgroup per (batch, head) running after the body, ends with a final
+    // dQ pass over the pair's rows: f32 atomics of every key block into dq_acc, converted there
+    // (default), or (g_attn_bwd_slab) plain f32 slabs per key block summed there. Either way the
+    // final pass also writes the e5m2 copy and the q-bias partials.
+    if (slab_path) {
+      const int nslab = (N - rem) / KB;
+      const int64_t sstride = (int64_t)B * N * D;
+      launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
+      launch(pvr_attn_bwd_waves(rem), N - rem, N, 4, slab, sstride, nslab, bpart);
+    } else {
+      launch(NW, 0, N - rem, 0, dq_acc, 0, 0, nullptr);
+      launch(pvr_attn_bwd_waves(rem), N - rem, N, dq_rezero ? 2 : 1, dq_acc, 0, 0, bpart);
+    }
     return hipGetLastError();
   }
   launch(NW, 0, N, 0, nkb > 1 ? dq_acc : nullptr, 0, 0, nkb > 1 ? nullptr : bpart);

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU session: kernel checks, attention backward dQ A/B (atomics vs slabs), BASELINE benches (round 4)
+R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
+O=gpurun_out/${1:-ab}; mkdir -p "$O"
+step() { local t=$1 log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "[$log] rc=$rc"; tail -n 1 "$O/$log" | cut -c1-160; [ $rc -eq 0 ] || exit $rc; }
+step 600 kernel_checks.log python -u -m pytest tests/test_gpu_kernels.py -q -p no:cacheprovider --timeout 120 --timeout-method thread -x
+step 300 attn_ab.log python -u scripts/attn_ab.py --ab bwd_slab --bwd --shapes l16_384,h14
+step 300 l16_def.log python bench.py --model vit_l16 --image-size 384 --batch 128 --steps 6 --warmup 3
+step 300 h14_def.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4
+step 200 b_def.log python bench.py

@@ -42,6 +42,8 @@ def main():
     a = ap.parse_args()
     ext = _ext.ext()
     variants = [("", lambda: None)]
+    if a.ab == "bwd_slab":
+        variants = [("atom", lambda: ext.set_attn_bwd_slab(0)), ("slab", lambda: ext.set_attn_bwd_slab(1))]
     if a.ab == "fwd_qg":
         variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1)),
                     ("kt64", lambda: ext.set_attn_fwd_qg(3))]
@@ -61,8 +63,11 @@ def main():
                 setv()
                 res.setdefault((name, "fwd", vn), []).append(timeit(lambda: ext.attn_fwd(qkv, B, N, H, dh ** -0.5)))
             if a.bwd:
-                res.setdefault((name, "bwd", ""), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
+                for vn, setv in (order if a.ab == "bwd_slab" else [("", lambda: None)]):
+                    setv()
+                    res.setdefault((name, "bwd", vn), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
     ext.set_attn_fwd_qg(0)
+    ext.set_attn_bwd_slab(0)
     for name in a.shapes.split(","):
         B, N, H, dh = SHAPES[name]
         fl = 4.0 * B * H * N * N * dh
@@ -71,8 +76,9 @@ def main():
             t = statistics.median(v)
             print(f"attn fwd {name:8s} B{B} N{N} H{H} dh{dh} {vn:4s} {t:7.3f} ms (min {min(v):.3f}) {fl / t / 1e9:6.1f} TF", flush=True)
         if a.bwd:
-            t = statistics.median(res[(name, "bwd", "")])
-            print(f"attn bwd {name:8s} B{B} N{N} H{H} dh{dh}      {t:7.3f} ms {2.5 * fl / t / 1e9:6.1f} TF", flush=True)
+            for vn in sorted({k[2] for k in res if k[0] == name and k[1] == "bwd"}):
+                t = statistics.median(res[(name, "bwd", vn)])
+                print(f"attn bwd {name:8s} B{B} N{N} H{H} dh{dh} {vn:4s} {t:7.3f} ms {2.5 * fl / t / 1e9:6.1f} TF", flush=True)
 
 
 if __name__ == "__main__":

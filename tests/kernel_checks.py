@@ -519,22 +519,27 @@ def check_attn_fwd(B, N, H, dh=64):
     return (f"attn_fwd B{B} N{N} H{H} dh{dh}", m, lim(4.5e-3, 6e-3, lse_l2=1.5e-7, lse_max=3e-7))
 
 
-def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
-    """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference."""
+def check_attn_bwd(B, N, H, dh=64, fused_bias=False, slab=False):
+    """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference. slab: the
+    multi-block path's dQ through f32 slabs instead of f32 atomics (set_attn_bwd_slab, A/B)."""
     ext = _ext.ext()
     D = H * dh
     qkv = bf(rnd(B * N, 3 * D))
     o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / math.sqrt(dh))
     do = bf(rnd(B * N, D))
     dbias = torch.zeros(3 * D, device=DEV) if fused_bias else None
-    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
+    ext.set_attn_bwd_slab(1 if slab else 0)
+    try:
+        dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
+    finally:
+        ext.set_attn_bwd_slab(0)
     qr = qkv.float().requires_grad_(True)
     oref, _ = _attn_ref(qr, B, N, H)
     oref.backward(do.float())
     m = worst((dqkv, qr.grad))
     if fused_bias:
         m["dbias_l2"], m["dbias_max"] = errs(dbias, qr.grad.sum(0))
-    return (f"attn_bwd B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}", m,
+    return (f"attn_bwd B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}{' slab' if slab else ''}", m,
             lim(5e-3, 1e-2, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
 
 
@@ -1465,9 +1470,11 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_fwd(2, 65, 2, 80),   # one full 64-key tile + the last key
         lambda: check_attn_bwd(2, 257, 3, 80),
         lambda: check_attn_bwd(2, 257, 3, 80, True),  # lastkey path + in-kernel bias partials (dh 80)
-        lambda: check_attn_bwd(2, 577, 2, 64, True),  # slab path + bias partials from the tail launch
+        lambda: check_attn_bwd(2, 577, 2, 64, True),  # tail split + bias partials from the tail's final dQ pass
+        lambda: check_attn_bwd(2, 577, 2, 64, True, slab=True),  # same with the f32-slab dQ (A/B variant)
+        lambda: check_attn_bwd(2, 577, 3, 80, False, slab=True),
         lambda: check_attn_bwd_q8(2, 257, 3, 80),    # e5m2 dQKV copy: lastkey path (pre-pass writes key N - 1)
-        lambda: check_attn_bwd_q8(2, 577, 2, 64),    # slab path (body dK/dV, tail dQ)
+        lambda: check_attn_bwd_q8(2, 577, 2, 64),    # tail split (body dK/dV, tail's final dQ pass)
         lambda: check_attn_bwd_q8(3, 197, 2, 80, 0.1),  # one key block, attention dropout
         lambda: check_attn_bwd(3, 257, 4, 64),    # N = 256 + 1: key-block body + last-key kernel
         lambda: check_attn_bwd(2, 257, 2, 128),
