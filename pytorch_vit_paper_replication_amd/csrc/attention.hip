@@ -463,7 +463,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   // optional e5m2 copy of dQKV (the fp8 recipe's grad slot: dgrad and weight-gradient operand) with
   // the slot's delayed scale, written next to every final bf16 value, amax recorded per wave
   const bool q8kv = q8.out != nullptr;  // dK / dV: every launch writes final values
-  const bool q8on = q8kv && !slab_w;     // dQ here: only a launch whose fragments are the final dQ
+  const bool q8on = q8kv && !dq_acc;     // dQ here: only a launch whose fragments are the final dQ
   float q8am = 0.f;
   const float q8s = q8kv ? *q8.qs : 1.f;
   const __amdgpu_buffer_rsrc_t q8rs = make_rsrc(q8.out + (int64_t)b * N * q8.ld, q8on ? clamp_bytes((int64_t)(N - 1) * q8.ld + D) : 0u);
@@ -1602,9 +1602,10 @@ static bool attn_bwd_tail_split(int N, bool dbias, bool drop) {
   const int rem = N % KB;
   return !attn_bwd_lastkey_path(N, dbias, drop) && (N + KB - 1) / KB > 1 && rem >= 16 && rem <= 128 && !dbias;
 }
-// dQ of the tail-split path through f32 slabs summed by the tail (1) or f32 atomics converted by
-// the tail (0, default: 1.15 vs 1.22 ms per ViT-L/16@384 b128 layer, profiles/r4/ab8, ab9)
-int g_attn_bwd_slab = 0;
+// dQ of the tail-split path through f32 slabs summed by the tail (1, default) or f32 atomics
+// converted by the tail (0): 1.215 vs 1.260 ms per ViT-L/16@384 b128 layer, same process
+// (profiles/r4/ab10/attn_ab.log)
+int g_attn_bwd_slab = 1;
 static bool attn_bwd_slab_path(int N, bool dbias, bool drop) { return g_attn_bwd_slab && attn_bwd_tail_split(N, dbias, drop); }
 extern "C" void pvr_set_attn_bwd_slab(int on) { g_attn_bwd_slab = on ? 1 : 0; }
 

@@ -994,7 +994,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
     "K-parts of the split tail round this GEMM shape gets (0: none)");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
-  m.def("set_attn_bwd_slab", &pvr_set_attn_bwd_slab, "multi-block attention backward: dQ through f32 slabs (1) or f32 atomics (0, default; A/B)");
+  m.def("set_attn_bwd_slab", &pvr_set_attn_bwd_slab, "multi-block attention backward: dQ through f32 slabs (1, default) or f32 atomics (0; A/B)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

@@ -67,7 +67,7 @@ def main():
                     setv()
                     res.setdefault((name, "bwd", vn), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
     ext.set_attn_fwd_qg(0)
-    ext.set_attn_bwd_slab(0)
+    ext.set_attn_bwd_slab(1)
     for name in a.shapes.split(","):
         B, N, H, dh = SHAPES[name]
         fl = 4.0 * B * H * N * N * dh

@@ -519,9 +519,9 @@ def check_attn_fwd(B, N, H, dh=64):
     return (f"attn_fwd B{B} N{N} H{H} dh{dh}", m, lim(4.5e-3, 6e-3, lse_l2=1.5e-7, lse_max=3e-7))
 
 
-def check_attn_bwd(B, N, H, dh=64, fused_bias=False, slab=False):
-    """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference. slab: the
-    multi-block path's dQ through f32 slabs instead of f32 atomics (set_attn_bwd_slab, A/B)."""
+def check_attn_bwd(B, N, H, dh=64, fused_bias=False, slab=True):
+    """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference. slab=False:
+    the multi-block path's dQ through f32 atomics instead of f32 slabs (set_attn_bwd_slab, A/B)."""
     ext = _ext.ext()
     D = H * dh
     qkv = bf(rnd(B * N, 3 * D))
@@ -532,14 +532,14 @@ def check_attn_bwd(B, N, H, dh=64, fused_bias=False, slab=False):
     try:
         dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
     finally:
-        ext.set_attn_bwd_slab(0)
+        ext.set_attn_bwd_slab(1)
     qr = qkv.float().requires_grad_(True)
     oref, _ = _attn_ref(qr, B, N, H)
     oref.backward(do.float())
     m = worst((dqkv, qr.grad))
     if fused_bias:
         m["dbias_l2"], m["dbias_max"] = errs(dbias, qr.grad.sum(0))
-    return (f"attn_bwd B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}{' slab' if slab else ''}", m,
+    return (f"attn_bwd B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}{'' if slab else ' atomics'}", m,
             lim(5e-3, 1e-2, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
 
 
@@ -1471,8 +1471,8 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd(2, 257, 3, 80),
         lambda: check_attn_bwd(2, 257, 3, 80, True),  # lastkey path + in-kernel bias partials (dh 80)
         lambda: check_attn_bwd(2, 577, 2, 64, True),  # tail split + bias partials from the tail's final dQ pass
-        lambda: check_attn_bwd(2, 577, 2, 64, True, slab=True),  # same with the f32-slab dQ (A/B variant)
-        lambda: check_attn_bwd(2, 577, 3, 80, False, slab=True),
+        lambda: check_attn_bwd(2, 577, 2, 64, True, slab=False),  # same with f32-atomic dQ (A/B variant)
+        lambda: check_attn_bwd(2, 577, 3, 80, False, slab=False),
         lambda: check_attn_bwd_q8(2, 257, 3, 80),    # e5m2 dQKV copy: lastkey path (pre-pass writes key N - 1)
         lambda: check_attn_bwd_q8(2, 577, 2, 64),    # tail split (body dK/dV, tail's final dQ pass)
         lambda: check_attn_bwd_q8(3, 197, 2, 80, 0.1),  # one key block, attention dropout
