@@ -943,43 +943,62 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __re
   const float c = scale * LOG2E;
   float av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float ov_sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of dO (the v-bias gradient)
-  for (int q = rs; q < N; q += RS) {
-    const int64_t row = (int64_t)b * N + q;
-    float dv[8], ov[8];
-    unpack(*(const uint4*)(dout + row * ld_do + h * DH + cc * 8), dv);
-    unpack(*(const uint4*)(o + row * ld_o + h * DH + cc * 8), ov);
+  // U rows per thread per trip with all their loads issued first (the loop is latency-bound:
+  // one row at a time waited a global-load round trip per 16 rows of the head)
+  constexpr int U = LAST ? 2 : 4;  // (LAST: three rows of loads each; keep ~6 waves per SIMD)
+  for (int q0 = rs; q0 < N; q0 += RS * U) {
+    uint4 dw[U], ow[U], qw[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ov_sum[j] += dv[j];
-    float dl = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dl = fmaf(dv[j], ov[j], dl);
-    if (!act) dl = 0.f;
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) dl += __shfl_xor(dl, off, 16);  // the row's 16 lanes
-    if constexpr (LAST) {
-      float qv[8];
-      unpack(*(const uint4*)(qbase + (int64_t)q * ld), qv);
-      float sdot = 0.f, dpdot = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sdot = fmaf(qv[j], kf[j], sdot);
-        dpdot = fmaf(dv[j], vf[j], dpdot);
-      }
-#pragma unroll
-      for (int off = 8; off > 0; off >>= 1) {
-        sdot += __shfl_xor(sdot, off, 16);
-        dpdot += __shfl_xor(dpdot, off, 16);
-      }
-      const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -lse[(int64_t)pr * N + q] * LOG2E));
-      const float ds = p * (dpdot - dl);
-      if (ch == 0) dsl[(int64_t)pr * N + q] = ds;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        av[j] = fmaf(p, dv[j], av[j]);
-        ak[j] = fmaf(ds, qv[j], ak[j]);
-      }
+    for (int u = 0; u < U; ++u) {
+      const int q = min(q0 + u * RS, N - 1);
+      const int64_t row = (int64_t)b * N + q;
+      dw[u] = *(const uint4*)(dout + row * ld_do + h * DH + cc * 8);
+      ow[u] = *(const uint4*)(o + row * ld_o + h * DH + cc * 8);
+      if constexpr (LAST) qw[u] = *(const uint4*)(qbase + (int64_t)q * ld);
     }
-    if (ch == 0) dlt[(int64_t)pr * N + q] = dl;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * RS;
+      const bool live = q < N;  // (uniform per row slot; the row's 16 lanes agree)
+      float dv[8], ov[8];
+      unpack(dw[u], dv);
+      unpack(ow[u], ov);
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ov_sum[j] += dv[j];
+      }
+      float dl = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl = fmaf(dv[j], ov[j], dl);
+      if (!act) dl = 0.f;
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) dl += __shfl_xor(dl, off, 16);  // the row's 16 lanes
+      if constexpr (LAST) {
+        float qv[8];
+        unpack(qw[u], qv);
+        float sdot = 0.f, dpdot = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sdot = fmaf(qv[j], kf[j], sdot);
+          dpdot = fmaf(dv[j], vf[j], dpdot);
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) {
+          sdot += __shfl_xor(sdot, off, 16);
+          dpdot += __shfl_xor(dpdot, off, 16);
+        }
+        const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -lse[(int64_t)pr * N + min(q, N - 1)] * LOG2E));
+        const float ds = live ? p * (dpdot - dl) : 0.f;
+        const float pl = live ? p : 0.f;
+        if (ch == 0 && live) dsl[(int64_t)pr * N + q] = ds;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          av[j] = fmaf(pl, dv[j], av[j]);
+          ak[j] = fmaf(ds, qv[j], ak[j]);
+        }
+      }
+      if (ch == 0 && live) dlt[(int64_t)pr * N + q] = dl;
+    }
   }
   if (!LAST && !bpart) return;
   if (act) {
