@@ -945,7 +945,9 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __re
   float ov_sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of dO (the v-bias gradient)
   // U rows per thread per trip with all their loads issued first (the loop is latency-bound:
   // one row at a time waited a global-load round trip per 16 rows of the head)
-  constexpr int U = LAST ? 2 : 4;  // (LAST: three rows of loads each; keep ~6 waves per SIMD)
+  // (LAST: one row per trip: two rows cost the registers of 4 -> 6 waves per SIMD and measured
+  // 131-136 vs 123-130 us per ViT-H/14 b256 layer; profiles/r4/ab11 vs ab9)
+  constexpr int U = LAST ? 1 : 4;
   for (int q0 = rs; q0 < N; q0 += RS * U) {
     uint4 dw[U], ow[U], qw[U];
 #pragma unroll
