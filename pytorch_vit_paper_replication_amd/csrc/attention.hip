@@ -19,7 +19,11 @@
 // keys' K and V fragments in registers and accumulates dK^T, dV^T over all query blocks of 32
 // (key on the lane: S and dP accumulators are directly the B operands of the dV/dK products).
 // dS crosses LDS once for dQ = dS . K, which the waves split by output fragment, so dQ needs no
-// atomics when one workgroup holds every key (N <= 256).
+// atomics when one workgroup holds every key (N <= 256). The query blocks are software-pipelined
+// (dQ of block t-1 beside S/dP of block t, one barrier per block). A pre-pass per (batch, head)
+// supplies delta = rowsum(dO * O), the dO column sums (v-bias gradient) and, for N = 256 + 1, the
+// last key's dS / dK / dV. Heads with more keys accumulate dQ in f32 slabs (or atomics) that the
+// tail launch's final pass turns into bf16 dQ, its optional e5m2 copy and the q-bias partials.
 #include "attn_common.h"
 
 namespace pvr {

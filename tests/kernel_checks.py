@@ -1476,7 +1476,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd_q8(2, 257, 3, 80),    # e5m2 dQKV copy: lastkey path (pre-pass writes key N - 1)
         lambda: check_attn_bwd_q8(2, 577, 2, 64),    # tail split (body dK/dV, tail's final dQ pass)
         lambda: check_attn_bwd_q8(3, 197, 2, 80, 0.1),  # one key block, attention dropout
-        lambda: check_attn_bwd(3, 257, 4, 64),    # N = 256 + 1: key-block body + last-key kernel
+        lambda: check_attn_bwd(3, 257, 4, 64),    # N = 256 + 1: key-block body + the pre-pass's last key
         lambda: check_attn_bwd(2, 257, 2, 128),
         lambda: check_attn_bwd(1, 40, 2, 80),
         lambda: check_attn_fwd(1, 197, 2, 128),
