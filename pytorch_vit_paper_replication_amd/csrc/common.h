@@ -298,5 +298,31 @@ PVR_DEV uint2 pack8_fp8(const float (&v)[8], float qs) {
   r.y = (uint32_t)pack2_fp8<FMT, true>(v[6] * qs, v[7] * qs, pack2_fp8<FMT, false>(v[4] * qs, v[5] * qs, 0));
   return r;
 }
+// pack8_fp8 that pays the saturation / NaN handling (4 VALU per value) only when some lane of the
+// wave needs it: with vmax = max |v| of the lane's 8 values (NaN-propagating; the producers record
+// it for the amax anyway), vmax * qs <= FMAX for every active lane - the delayed-scaling steady
+// state - means every product is finite and rounds to at most FMAX, so the conversion runs directly
+// 4 f32 -> 4 fp8 bytes, direct conversion (caller guarantees |v * qs| <= FMAX and no NaN)
+template <int FMT>
+PVR_DEV uint32_t pack4_fp8_direct(float a, float b, float c, float d) {
+  if constexpr (FMT == 0)
+    return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false), true);
+  else
+    return (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(c, d, __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false), true);
+}
+// true when every active lane's vmax * qs <= FMAX (wave-uniform): pack4_fp8_direct is exact
+template <int FMT>
+PVR_DEV bool fp8_direct_ok(float vmax, float qs) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
+  return __builtin_amdgcn_ballot_w64(!(vmax * qs <= FMAX)) == 0;  // NaN compares false
+}
+template <int FMT>
+PVR_DEV uint2 pack8_fp8_fast(const float (&v)[8], float qs, float vmax) {
+  if (!fp8_direct_ok<FMT>(vmax, qs)) return pack8_fp8<FMT>(v, qs);
+  uint2 r;
+  r.x = pack4_fp8_direct<FMT>(v[0] * qs, v[1] * qs, v[2] * qs, v[3] * qs);
+  r.y = pack4_fp8_direct<FMT>(v[4] * qs, v[5] * qs, v[6] * qs, v[7] * qs);
+  return r;
+}
 
 }  // namespace pvr

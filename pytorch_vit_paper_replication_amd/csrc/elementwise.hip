@@ -77,9 +77,11 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
           *(uint4*)(dz + (int64_t)r * ld_dz + c * 8) = o;
         }
         if constexpr (Q8) {
-          *(uint2*)(qout + (int64_t)r * ld_q + c * 8) = pack8_fp8<1>(v, qs);
+          float vm = 0.f;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qam = nan_max(qam, fabsf(v[j]));
+          for (int j = 0; j < 8; ++j) vm = nan_max(vm, fabsf(v[j]));
+          qam = nan_max(qam, vm);
+          *(uint2*)(qout + (int64_t)r * ld_q + c * 8) = pack8_fp8_fast<1>(v, qs, vm);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += v[j];

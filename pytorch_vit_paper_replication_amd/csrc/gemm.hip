@@ -1050,10 +1050,12 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         if (qon) {
           // rows past M / columns past N: out-of-range offset (dropped); their values are 0 anyway
           const uint32_t vq = c0[jp] < p.N ? (uint32_t)((int64_t)(16 * i + li) * p.ld_q + c0[jp]) : OOB;
-          const uint2 q8 = p.q_fmt ? pack8_fp8<1>(v, qsc) : pack8_fp8<0>(v, qsc);
-          __builtin_amdgcn_raw_buffer_store_b64((v2u_q){q8.x, q8.y}, qrs, vq, 0, 0);
+          float vm = 0.f;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) qam = nan_max(qam, fabsf(v[e]));
+          for (int e = 0; e < 8; ++e) vm = nan_max(vm, fabsf(v[e]));
+          qam = nan_max(qam, vm);
+          const uint2 q8 = p.q_fmt ? pack8_fp8_fast<1>(v, qsc, vm) : pack8_fp8_fast<0>(v, qsc, vm);
+          __builtin_amdgcn_raw_buffer_store_b64((v2u_q){q8.x, q8.y}, qrs, vq, 0, 0);
         }
       }
     }

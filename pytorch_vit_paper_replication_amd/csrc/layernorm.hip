@@ -142,16 +142,18 @@ __global__ void __launch_bounds__(256) ln_fwd_q8_kernel(const uint16_t* __restri
         const float ww[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
         const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
         float o[8];
+        float vm = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           o[j] = (v[i][j] - mean) * rstd * ww[j] + bb[j];
-          am = nan_max(am, fabsf(o[j]));
+          vm = nan_max(vm, fabsf(o[j]));
         }
+        am = nan_max(am, vm);
         uint4 q;
         q.x = pack2bf(o[0], o[1]); q.y = pack2bf(o[2], o[3]);
         q.z = pack2bf(o[4], o[5]); q.w = pack2bf(o[6], o[7]);
         if (yr) *(uint4*)(yr + c * 8) = q;
-        *(uint2*)(qr + c * 8) = pack8_fp8<0>(o, qs);
+        *(uint2*)(qr + c * 8) = pack8_fp8_fast<0>(o, qs, vm);
       }
     }
     if (lane == 0) {
@@ -318,11 +320,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
         }
         if constexpr (Q8) {  // e5m2 copy of the gradient written last (dz, else dx) for the next fp8 dgrad GEMM
           uint32_t b4[W / 4];
+          float vm = 0.f;
 #pragma unroll
-          for (int j = 0; j < W; j += 4) {
-            b4[j >> 2] = (uint32_t)pack2_fp8<1, true>(o[j + 2] * qs, o[j + 3] * qs, pack2_fp8<1, false>(o[j] * qs, o[j + 1] * qs, 0));
+          for (int j = 0; j < W; ++j) vm = nan_max(vm, fabsf(o[j]));
+          qam = nan_max(qam, vm);
+          if (fp8_direct_ok<1>(vm, qs)) {  // no saturation / NaN handling needed in this wave
 #pragma unroll
-            for (int e = 0; e < 4; ++e) qam = nan_max(qam, fabsf(o[j + e]));
+            for (int j = 0; j < W; j += 4) b4[j >> 2] = pack4_fp8_direct<1>(o[j] * qs, o[j + 1] * qs, o[j + 2] * qs, o[j + 3] * qs);
+          } else {
+#pragma unroll
+            for (int j = 0; j < W; j += 4)
+              b4[j >> 2] = (uint32_t)pack2_fp8<1, true>(o[j + 2] * qs, o[j + 3] * qs, pack2_fp8<1, false>(o[j] * qs, o[j + 1] * qs, 0));
           }
           uint8_t* qp = qout + (int64_t)row * q_stride + c * W;
           if constexpr (W == 8)
