@@ -152,6 +152,8 @@ void attach_tail(pvr::GemmParams& p, const torch::Tensor& like) {
   p.tail_cnt_elems = (int)it->second.cnt.numel();
 }
 void set_gemm_tail(bool on) { g_gemm_tail = on; }
+static int g_tail_min_kt = 12;
+void set_gemm_tail_min_kt(int64_t n) { g_tail_min_kt = (int)n; }
 
 // C = A . B^T with the given operand layouts; see csrc/gemm.hip for the epilogue contract.
 void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torch::Tensor C, int64_t M, int64_t N, int64_t K,
@@ -214,6 +216,7 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   if (epi <= 2 && p.k_split_len >= K && tail_limit >= 0) {
     attach_tail(p, C);
     p.tail_max_units = (int)tail_limit;
+    p.tail_min_kt = g_tail_min_kt;
   }
   check(pvr_gemm(&p, stream()), "gemm");
 }
@@ -682,6 +685,7 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
   if (epi <= 2 && tail_limit >= 0) {  // tail_limit: as for gemm()
     attach_tail(p, C);
     p.tail_max_units = (int)tail_limit;
+    p.tail_min_kt = g_tail_min_kt;
   }
   check(pvr_gemm(&p, stream()), "gemm_fp8");
 }
@@ -995,6 +999,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     "K-parts of the split tail round this GEMM shape gets (0: none)");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
   m.def("set_attn_bwd_slab", &pvr_set_attn_bwd_slab, "multi-block attention backward: dQ through f32 slabs (1, default) or f32 atomics (0; A/B)");
+  m.def("set_gemm_tail_min_kt", &set_gemm_tail_min_kt, "fewest K-tiles per split-tail part (default 12; A/B)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

@@ -1509,7 +1509,8 @@ void plan_tail(GemmParams& q, int ntiles, int bke) {
   q.tail_from = 0;
   q.tail_split = 0;
   if (!q.tail_ws || !q.tail_cnt) return;
-  const TailPlan t = plan_tail_c(ntiles, q.K / bke, device_cus(), q.tail_ws_elems, q.tail_cnt_elems, q.tail_max_units);
+  const TailPlan t = plan_tail_c(ntiles, q.K / bke, device_cus(), q.tail_ws_elems, q.tail_cnt_elems, q.tail_max_units,
+                                    q.tail_min_kt > 0 ? q.tail_min_kt : 12);
   q.tail_from = t.from;
   q.tail_split = t.split;
 }

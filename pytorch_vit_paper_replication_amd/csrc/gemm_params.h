@@ -47,6 +47,8 @@ struct GemmParams {
   // limit: there the weight-gradient side stream's long workgroups occupy the CUs a wide split
   // round would need, and the dgrad chain then waits for them (measured -0.6 % per step).
   int tail_max_units;
+  // fewest K-tiles a split part may keep (default 12: measured on the K = 768 bf16 GEMMs)
+  int tail_min_kt;
 };
 
 }  // namespace pvr

@@ -23,14 +23,14 @@ struct TailPlan {
   int split;  // K-parts per leftover tile (0: no split)
 };
 
-constexpr TailPlan plan_tail_c(int ntiles, int nkt, int cus, long long ws_elems, int cnt_elems, int max_units) {
+constexpr TailPlan plan_tail_c(int ntiles, int nkt, int cus, long long ws_elems, int cnt_elems, int max_units, int min_kt = 12) {
   TailPlan t{0, 0};
   if (cus <= 0 || ntiles < cus) return t;
   const int rem = ntiles % cus;
   if (rem == 0) return t;
   int s = cus / rem;
   s = s < 4 ? s : 4;
-  while (s > 1 && nkt / s < 12) --s;
+  while (s > 1 && nkt / s < min_kt) --s;
   if (max_units > 0)
     while (s > 1 && rem * s > max_units) --s;
   if (s < 2) return t;
