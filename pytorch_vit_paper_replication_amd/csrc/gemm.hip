@@ -734,20 +734,24 @@ PVR_DEV void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// fp8 fragment half h of a 16 x 128 (k) operand tile: lane (row r0 + (l&15)) gets bytes
-// 32 (l>>4) + 16 h .. +15 of its 128-B row; A and B use the same read, so the k order the MFMA
-// assigns to the 32 bytes of a lane is the same for both operands.
+// fp8 fragment half h of a 16 x 128 (k) operand tile: lane (row r0 + (l&15)) gets 16-B chunk
+// (l>>4) + 4h of its 128-B row. A and B use the same read, so the k order the MFMA assigns to the
+// 32 bytes of a lane is the same for both operands and the product is unchanged by which chunks a
+// lane holds. Chunk (l>>4) + 4h (the bf16 read_frag order) keeps each ds_read_b128 lane group on 16
+// distinct bank quads of the swz_k image; the former 2 (l>>4) + h hit 8 (2-way conflicts on every
+// fragment read: SQ_LDS_BANK_CONFLICT ~4 cycles per LDS instruction, profiles/r4/pmc_gemm).
+// The fp8 kernels never mix a k-contiguous operand with an mn-contiguous one (read_frag_mn8_async).
 PVR_DEV v8s frag_fp8(const char* img, int r0, int h, int lane) {
   const int row = r0 + (lane & 15);
-  const int c = 2 * (lane >> 4) + h;
+  const int c = (lane >> 4) + 4 * h;
   return ds_read_b128(img + row * 128 + ((c ^ swz_k(row)) << 4));
 }
 
 typedef uint32_t v2u8 __attribute__((ext_vector_type(2)));
 // fp8 operand fragment of an mn-contiguous [128 k][128 B] image (4 x ds_read_b64_tr_b8, async: the
 // caller waits with lds_wait): lane (g = l >> 4, i = l & 15) gets image column c0 + i at k-rows
-// 32g + 8j .. +7 in r[j], i.e. k = 32g .. 32g + 31 of its row as frag_fp8 delivers it for a
-// k-contiguous image. Per 16-lane group, lane 2q + p supplies row q, bytes 8p .. 8p + 7.
+// 32g + 8j .. +7 in r[j], i.e. k = 32g .. 32g + 31 of its row (both operands of the wgrad kernel
+// use this read). Per 16-lane group, lane 2q + p supplies row q, bytes 8p .. 8p + 7.
 PVR_DEV void read_frag_mn8_async(const char* img, int c0, int lane, v2u8 (&r)[4]) {
   const int g = lane >> 4, i = lane & 15;
   const int row = 32 * g + (i >> 1);  // + 8j for read j: swz8 is the same on all four
