@@ -216,12 +216,53 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
     __syncthreads();
   }
   float qam = 0.f;
+  // Output rows through LDS (the K/V images are idle after the last barrier): each wave writes its
+  // 16-query groups' bf16 O rows and e4m3 rows into its own region, then stores them as 16-B chunks
+  // of whole rows (a wave instruction covers 6-16 consecutive rows' bytes instead of 16 rows x 8 B
+  // (bf16) / 4 B (e4m3) per store: the direct stores were issue-bound). Needs 16-B aligned rows.
+  constexpr int OB = DH * 2, QB = DH;  // bytes per bf16 / e4m3 head row
+  constexpr int WB = 16 * (OB + QB);    // LDS bytes per (wave, group)
+  static_assert(4 * QG * WB <= 4 * TILE_BYTES, "staged output fits the K/V images");
+  const bool qon = q8.out != nullptr;
+  // (dh 64 without the copy: 128-B rows, whose direct stores already fill whole lines - measured
+  // 0.303 direct vs 0.308 staged at ViT-L/16@384; dh 80: 0.283 -> 0.269, with the copy 0.332 -> 0.296;
+  // profiles/r4/aq8/attn_q8_ab.log)
+  const bool staged = !q8.direct && (qon || DH != 64) && (((uintptr_t)out | (uintptr_t)(ld_o * 2)) & 15) == 0 &&
+                      (!qon || (((uintptr_t)q8.out | (uintptr_t)q8.ld) & 15) == 0);
+  const float qs = qon ? *q8.qs : 1.f;
 #pragma unroll
   for (int gi = 0; gi < QG; ++gi) {
     float l = l_run[gi];
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const int q = q0 + 16 * gi + li;
+    if (staged) {
+      if (q0 + 16 * gi < N) {  // uniform: the group holds a valid query
+        char* st = smem + (wave * QG + gi) * WB;
+        const bool live = q < N;
+        const float inv = live ? 1.f / l : 0.f;
+        float vm = 0.f;
+#pragma unroll
+        for (int e = 0; e < C::NE; ++e) {
+          const float v0 = o[gi][e][0] * inv, v1 = o[gi][e][1] * inv, v2 = o[gi][e][2] * inv, v3 = o[gi][e][3] * inv;
+          *(uint2*)(st + li * OB + (16 * e + 4 * g) * 2) = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+          vm = nan_max(vm, nan_max(nan_max(fabsf(v0), fabsf(v1)), nan_max(fabsf(v2), fabsf(v3))));
+        }
+        if (qon) {  // e4m3 copy for the fp8 out-proj GEMM
+          qam = nan_max(qam, vm);
+          const bool fast = fp8_direct_ok<0>(vm, qs);
+#pragma unroll
+          for (int e = 0; e < C::NE; ++e) {
+            const float v0 = o[gi][e][0] * inv * qs, v1 = o[gi][e][1] * inv * qs, v2 = o[gi][e][2] * inv * qs,
+                        v3 = o[gi][e][3] * inv * qs;
+            *(uint32_t*)(st + 16 * OB + li * QB + 16 * e + 4 * g) =
+                fast ? pack4_fp8_direct<0>(v0, v1, v2, v3) : (uint32_t)pack2_fp8<0, true>(v2, v3, pack2_fp8<0, false>(v0, v1, 0));
+          }
+        }
+        if (g == 0 && live) lse[(int64_t)bh * N + q] = (m_run[gi] + __log2f(l)) * LN2;
+      }
+      continue;
+    }
     if (q < N) {
       const float inv = 1.f / l;
       uint16_t* orow = out + ((int64_t)b * N + q) * ld_o + h * DH;
@@ -233,7 +274,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
         *(uint2*)(orow + 16 * e + 4 * g) = w;
       }
       if (q8.out) {  // e4m3 copy for the fp8 out-proj GEMM
-        const float qs = *q8.qs;
         uint8_t* qrow = q8.out + ((int64_t)b * N + q) * q8.ld + h * DH;
 #pragma unroll
         for (int e = 0; e < C::NE; ++e) {
@@ -245,6 +285,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
         }
       }
       if (g == 0) lse[(int64_t)bh * N + q] = (m_run[gi] + __log2f(l)) * LN2;
+    }
+  }
+  if (staged) {  // LDS images -> whole-row 16-B chunks (each wave reads back only its own region)
+#pragma unroll
+    for (int gi = 0; gi < QG; ++gi) {
+      const int r0 = q0 + 16 * gi;
+      const int nrow = min(16, N - r0);
+      if (nrow <= 0) continue;
+      const char* st = smem + (wave * QG + gi) * WB;
+      constexpr int OC = OB / 16, QC = QB / 16;  // 16-B chunks per row
+#pragma unroll
+      for (int k = 0; k < (16 * OC + 63) / 64; ++k) {
+        const int ch = lane + 64 * k, row = ch / OC, cc = ch % OC;
+        if (ch < 16 * OC && row < nrow)
+          *(uint4*)((char*)(out + ((int64_t)b * N + r0 + row) * ld_o + h * DH) + cc * 16) = *(const uint4*)(st + row * OB + cc * 16);
+      }
+      if (qon) {
+#pragma unroll
+        for (int k = 0; k < (16 * QC + 63) / 64; ++k) {
+          const int ch = lane + 64 * k, row = ch / QC, cc = ch % QC;
+          if (ch < 16 * QC && row < nrow)
+            *(uint4*)(q8.out + ((int64_t)b * N + r0 + row) * q8.ld + h * DH + cc * 16) = *(const uint4*)(st + 16 * OB + row * QB + cc * 16);
+        }
+      }
     }
   }
   if (q8.out) {
@@ -1527,6 +1591,8 @@ static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t
 // (L/16-384, N = 577: 640 either way, QG 2 0.399 vs 0.440 ms; H/14, N = 257: 384 vs 320 rows, QG 2
 // 0.376 vs 0.319 ms, scripts/attn_ab.py). g_attn_fwd_qg: 0 = that rule, 1 / 2 = forced, 3 = QG 1 with
 // 64-key tiles at every head dim (A/B).
+// forward output through LDS (false, default) or straight from the registers (true: A/B)
+bool g_attn_fwd_direct = false;
 int g_attn_fwd_qg = 0;
 static bool attn_fwd_use_qg2(int N) {
   if (g_attn_fwd_qg) return g_attn_fwd_qg == 2;
@@ -1591,7 +1657,7 @@ extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* ou
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
   if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
   const AttnDrop drop{seed, seed_off, thr16, keep_scale};
-  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax};
+  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, 0, g_attn_fwd_direct ? 1 : 0};
   switch (D / H) {
     case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
     case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
@@ -1633,6 +1699,7 @@ static bool attn_bwd_tail_split(int N, bool dbias, bool drop) {
 int g_attn_bwd_slab = 1;
 static bool attn_bwd_slab_path(int N, bool dbias, bool drop) { return g_attn_bwd_slab && attn_bwd_tail_split(N, dbias, drop); }
 extern "C" void pvr_set_attn_bwd_slab(int on) { g_attn_bwd_slab = on ? 1 : 0; }
+extern "C" void pvr_set_attn_fwd_direct(int on) { g_attn_fwd_direct = on != 0; }
 
 // the generic backward's kernels write every final dQ value (no f32 atomics + conversion pass)
 static bool attn_bwd_final_dq_in_kernel(int N, bool dbias, bool drop) {
