@@ -56,6 +56,8 @@ def parse():
                    help="A/B: weight-gradient batches whose inputs stay held at once (0 = no count bound)")
     p.add_argument("--side-hold-gb", type=float, default=None,
                    help="A/B: GB of weight-gradient inputs held at once (0 = until the end of backward)")
+    p.add_argument("--fp8-persistent", type=int, default=None,
+                   help="fp8 GEMMs on the persistent ping-pong: 0 never, 1 no per-row inputs (default), 2 also residual (A/B)")
     p.add_argument("--no-gemm-tail", action="store_true",
                    help="A/B: no split-K tail on the last dispatch round of the one-tile-per-workgroup GEMMs")
     p.add_argument("--main-prio", type=int, default=-1,
@@ -124,6 +126,10 @@ def main():
         if args.side_hold_gb is not None:
             param_store.SIDE_HOLD_BYTES = int(args.side_hold_gb * 2**30)
     rank, world, device = init_distributed()
+    if args.fp8_persistent is not None and args.impl == "fused":
+        from pytorch_vit_paper_replication_amd import _ext
+
+        _ext.ext().set_fp8_persistent(args.fp8_persistent)
     if args.no_gemm_tail and args.impl == "fused":
         from pytorch_vit_paper_replication_amd import _ext
 

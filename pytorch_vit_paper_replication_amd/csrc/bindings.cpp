@@ -25,6 +25,7 @@ int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
 void pvr_set_attn_fwd_qg(int qg);
 void pvr_set_attn_bwd_slab(int on);
 void pvr_set_attn_fwd_direct(int on);
+void pvr_set_fp8_persistent(int mode);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
@@ -999,6 +1000,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
     "K-parts of the split tail round this GEMM shape gets (0: none)");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
+  m.def("set_fp8_persistent", &pvr_set_fp8_persistent, "fp8 fwd/dgrad GEMMs on the persistent ping-pong: 0 never, 1 no per-row inputs (default), 2 also residual (A/B)");
   m.def("set_attn_fwd_direct", &pvr_set_attn_fwd_direct, "attention forward: O stores straight from registers (1) or through LDS (0, default; A/B)");
   m.def("set_attn_bwd_slab", &pvr_set_attn_bwd_slab, "multi-block attention backward: dQ through f32 slabs (1, default) or f32 atomics (0; A/B)");
   m.def("set_gemm_tail_min_kt", &set_gemm_tail_min_kt, "fewest K-tiles per split-tail part (default 12; A/B)");

@@ -1551,6 +1551,7 @@ hipError_t launch_pp(const GemmParams& p, hipStream_t s) {
 // with its operands landed and its prologue latency is hidden under tile i's tail and epilogue.
 // The epilogue stages through a separate 32 KiB LDS region (8 passes of 32 rows) so it never
 // touches the K-tile buffers the in-flight DMAs are writing. k-contiguous bf16 operands, K >= 128.
+template <int ES = 2>
 PVR_DEV void ppp_issue_kind(int kind, __amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, char* buf, int64_t lda, int64_t ldb,
                             int kb, int wave, int lane) {
 #pragma unroll
@@ -1561,13 +1562,13 @@ PVR_DEV void ppp_issue_kind(int kind, __amdgpu_buffer_rsrc_t ars, __amdgpu_buffe
       const int rowb = (2 * (d >> 3) + hh) * 64 + (d & 7) * 8;
       const int row = rowb + (lane >> 3);
       const int c = (lane & 7) ^ swz_k(row);
-      dma16(ars, to_lds(buf + rowb * 128), (uint32_t)(row * lda * 2 + kb + c * 16));
+      dma16(ars, to_lds(buf + rowb * 128), (uint32_t)(row * lda * ES + kb + c * 16));
     } else {
       const int hh = kind == 2;
       const int rowb = (2 * (d >> 2) + hh) * 32 + (d & 3) * 8;
       const int row = rowb + (lane >> 3);
       const int c = (lane & 7) ^ swz_k(row);
-      dma16(brs, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * 2 + kb + c * 16));
+      dma16(brs, to_lds(buf + 256 * 128 + rowb * 128), (uint32_t)(row * ldb * ES + kb + c * 16));
     }
   }
 }
@@ -1577,6 +1578,7 @@ struct PppTile {
   __amdgpu_buffer_rsrc_t ars, brs;
 };
 
+template <int ES = 2>
 PVR_DEV PppTile ppp_tile(const GemmParams& p, int v, int ntiles, int ntn) {
   PppTile t;
   if (v >= ntiles) {  // past this workgroup's last tile: every DMA reads as out of range
@@ -1588,14 +1590,19 @@ PVR_DEV PppTile ppp_tile(const GemmParams& p, int v, int ntiles, int ntn) {
   const int tt = xcd_remap(v, ntiles);
   t.m0 = (tt / ntn) * 256;
   t.n0 = (tt % ntn) * 256;
-  t.ars = make_rsrc(p.A + (int64_t)t.m0 * p.lda, rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)t.m0 * p.lda));
-  t.brs = make_rsrc(p.B + (int64_t)t.n0 * p.ldb, rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)t.n0 * p.ldb));
+  if constexpr (ES == 1) {  // fp8: lda / ldb / K in bytes (rsrc_bytes counts 2-B elements)
+    t.ars = make_rsrc((const uint8_t*)p.A + (int64_t)t.m0 * p.lda, rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)t.m0 * p.lda) / 2);
+    t.brs = make_rsrc((const uint8_t*)p.B + (int64_t)t.n0 * p.ldb, rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)t.n0 * p.ldb) / 2);
+  } else {
+    t.ars = make_rsrc(p.A + (int64_t)t.m0 * p.lda, rsrc_bytes((int64_t)(p.M - 1) * p.lda + p.K, (int64_t)t.m0 * p.lda));
+    t.brs = make_rsrc(p.B + (int64_t)t.n0 * p.ldb, rsrc_bytes((int64_t)(p.N - 1) * p.ldb + p.K, (int64_t)t.n0 * p.ldb));
+  }
   return t;
 }
 
 // Phase of the continuous stream: reads / MFMAs of K-tile (current buffer) and the DMA of global
 // half-tile `h_issue`, which belongs to this tile (K-tile kt_i) or to the next one.
-template <int QM, int QN, int RD_A, int RD_B, bool SWAP, int VM = 8>
+template <int QM, int QN, int RD_A, int RD_B, bool SWAP, int VM = 8, int ES = 2, int FA = 0, int FB = 0>
 PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, char* smem, const PppTile& cur,
                        const PppTile& nxt, int G_issue, int kind, int tile_first_G, int nk, const GemmParams& p, int wave, int lane,
                        int wm, int wn) {
@@ -1603,25 +1610,44 @@ PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], co
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+      for (int ks = 0; ks < 2; ++ks)
+        af[ii][ks] = ES == 1 ? frag_fp8(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane)
+                             : read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
   }
   if constexpr (RD_B) {
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
+      for (int ks = 0; ks < 2; ++ks)
+        bf[QN][jj][ks] = ES == 1 ? frag_fp8(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane)
+                                 : read_frag<256, true>(buf + 256 * 128, wn * 64 + QN * 32 + 16 * jj, ks, lane);
   }
   {
     const int rel = G_issue - tile_first_G;  // K-tile index relative to the current tile
     const bool same = rel < nk;
     const PppTile& t = same ? cur : nxt;
     const int kt = same ? rel : rel - nk;
-    ppp_issue_kind(kind, t.ars, t.brs, smem + (G_issue & 1) * PP_BUF, p.lda, p.ldb, kt * 128, wave, lane);
+    ppp_issue_kind<ES>(kind, t.ars, t.brs, smem + (G_issue & 1) * PP_BUF, p.lda, p.ldb, kt * 128, wave, lane);
   }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM) : "memory");
   pp_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_setprio(1);
+  if constexpr (ES == 1) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        v4f& c = acc[QM * 4 + ii][QN * 2 + jj];
+        if constexpr (SWAP)
+          c = mfma_fp8<FB, FA>(bf[QN][jj][0], bf[QN][jj][1], af[ii][0], af[ii][1], c);
+        else
+          c = mfma_fp8<FA, FB>(af[ii][0], af[ii][1], bf[QN][jj][0], bf[QN][jj][1], c);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+    return;
+  }
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1638,8 +1664,11 @@ PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], co
   pp_barrier();
 }
 
-template <bool SWAP, int EPI, bool DIRECT>
+// ES = 1: fp8 operands (register-direct epilogue only; the GELU epilogue's e4m3 copy adds 16 stores
+// per wave beyond INFL, which only makes the counted waits retire more of them: still correct)
+template <bool SWAP, int EPI, bool DIRECT, int ES = 2, int FA = 0, int FB = 0>
 __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
+  static_assert(ES == 2 || DIRECT, "fp8 persistent GEMM: register-direct epilogue");
   // epilogue stores per wave left in flight across the tile boundary (0: drain): the register-direct
   // BF16 epilogue issues 16 x 16 B, GELU 32 (output + derivative), dGELU 16 + 8 column-sum atomics
   // (to a 0-byte resource without colsum)
@@ -1649,19 +1678,19 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256, ntiles = ntm * ntn;
-  const int nk = p.K / PP_BK;  // >= 2 (host check)
+  const int nk = p.K / (128 / ES);  // K-tiles of 128 B (64 bf16 / 128 fp8); >= 2 (host check)
   int v = blockIdx.x;
   if (v >= ntiles) return;
 
-  PppTile cur = ppp_tile(p, v, ntiles, ntn);
-  PppTile nxt = ppp_tile(p, v + gridDim.x, ntiles, ntn);
+  PppTile cur = ppp_tile<ES>(p, v, ntiles, ntn);
+  PppTile nxt = ppp_tile<ES>(p, v + gridDim.x, ntiles, ntn);
   // prologue of the first tile: half-tiles 0..5 (global K-tiles 0 and 1 of the stream)
-  ppp_issue_kind(0, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
-  ppp_issue_kind(1, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
-  ppp_issue_kind(2, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
-  ppp_issue_kind(3, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
-  ppp_issue_kind(0, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
-  ppp_issue_kind(1, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
+  ppp_issue_kind<ES>(0, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind<ES>(1, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind<ES>(2, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind<ES>(3, cur.ars, cur.brs, smem, p.lda, p.ldb, 0, wave, lane);
+  ppp_issue_kind<ES>(0, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
+  ppp_issue_kind<ES>(1, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pp_barrier();
 
@@ -1681,20 +1710,20 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
         // the four half-tiles this K-tile waits for, so every wait leaves them in flight (counted);
         // the first wait for a half-tile issued after them (next K-tile) retires them
         const char* buf = smem + (G0 & 1) * PP_BUF;
-        ppp_phase<0, 0, 1, 1, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 2, G0, nk, p, wave, lane, wm, wn);
-        ppp_phase<0, 1, 0, 1, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 3, G0, nk, p, wave, lane, wm, wn);
-        ppp_phase<1, 1, 1, 0, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 0, G0, nk, p, wave, lane, wm, wn);
-        ppp_phase<1, 0, 0, 0, SWAP, 8 + INFL>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 1, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<0, 0, 1, 1, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 2, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<0, 1, 0, 1, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 3, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<1, 1, 1, 0, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 0, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<1, 0, 0, 0, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 1, G0, nk, p, wave, lane, wm, wn);
         kt = 1;
       }
     }
     for (; kt < nk; ++kt) {
       const int G = G0 + kt;
       const char* buf = smem + (G & 1) * PP_BUF;
-      ppp_phase<0, 0, 1, 1, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 1, 2, G0, nk, p, wave, lane, wm, wn);
-      ppp_phase<0, 1, 0, 1, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 1, 3, G0, nk, p, wave, lane, wm, wn);
-      ppp_phase<1, 1, 1, 0, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 2, 0, G0, nk, p, wave, lane, wm, wn);
-      ppp_phase<1, 0, 0, 0, SWAP>(acc, af, bf, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<0, 0, 1, 1, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 1, 2, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<0, 1, 0, 1, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 1, 3, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<1, 1, 1, 0, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 2, 0, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<1, 0, 0, 0, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
     }
     if (wm == 0) pp_barrier();  // re-align the groups for the epilogue
     // The next tile's first DMAs are in flight into the K-tile buffers; the epilogue works from
@@ -1702,10 +1731,10 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
     // separate region behind them.
     if constexpr (DIRECT) {
       if (p.resid)
-        epilogue_direct<EPI, true>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
+        epilogue_direct<EPI, true, ES == 1>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
       else
-        epilogue_direct<EPI, false>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
-    } else {
+        epilogue_direct<EPI, false, ES == 1>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
+    } else if constexpr (ES == 2) {
       if (p.resid)
         epilogue_staged<EPI, 32, true>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
       else
@@ -1715,7 +1744,7 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
     if (v >= ntiles) break;
     G0 += nk;
     cur = nxt;
-    nxt = ppp_tile(p, v + gridDim.x, ntiles, ntn);
+    nxt = ppp_tile<ES>(p, v + gridDim.x, ntiles, ntn);
     if constexpr (INFL == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain (stores + the K-tiles already issued)
       __syncthreads();
@@ -1724,11 +1753,11 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
 
-template <bool SWAP, int EPI>
+template <bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
 hipError_t launch_ppp(const GemmParams& p, hipStream_t s) {
   constexpr int SMEM = 2 * PP_BUF + 32 * 1024;
-  auto kd = gemm_ppp_kernel<SWAP, EPI, true>;
-  auto ks = gemm_ppp_kernel<SWAP, EPI, false>;
+  auto kd = gemm_ppp_kernel<SWAP, EPI, true, ES, FA, FB>;
+  auto ks = gemm_ppp_kernel<SWAP, EPI, ES == 1, ES, FA, FB>;  // fp8: the direct form only
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
@@ -1737,6 +1766,7 @@ hipError_t launch_ppp(const GemmParams& p, hipStream_t s) {
     attr_set = true;
   }
   const bool direct = !p.epi_staged && direct_ok(p);
+  if (ES == 1 && !direct) return hipErrorInvalidValue;  // caller checks (fp8_persistent_ok)
   auto kern = direct ? kd : ks;
   const int ntiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   const int cus = device_cus();
@@ -1786,6 +1816,11 @@ extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_
   return q.tail_split;
 }
 
+// fp8 forward / dgrad GEMMs on the persistent ping-pong (see pvr_gemm): 0 = never, 1 = without
+// per-row epilogue inputs (default), 2 = also with the residual
+static int g_fp8_persistent = 1;
+extern "C" void pvr_set_fp8_persistent(int mode) { g_fp8_persistent = mode; }
+
 // Host entry. Returns hipSuccess, or hipErrorInvalidValue for an unsupported layout/epilogue pair.
 extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
   using namespace pvr;
@@ -1810,12 +1845,24 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
       return launch_pp<true, true, true, EPI_F32_STORE, 1, 1, 0>(p, s);
     }
     if (p.k_split_len < p.K) return hipErrorInvalidValue;
+    // persistent form (tile 13) when there are >= 4 output tiles per CU, the K loop is short
+    // (<= 16 K-tiles: the next tile's prologue / this tile's epilogue are a large share of a tile)
+    // and the register-direct epilogue applies; g_fp8_persistent 0 = never (A/B), 1 = epilogues
+    // without per-row inputs, 2 = also the residual epilogue. ViT-H/14 b256 (profiles/r4/g8b):
+    // fc1 GELU fwd 0.800 -> 0.688 ms, qkv fwd 0.363 -> 0.357, out dgrad 0.126 -> 0.121; the K = 3840 /
+    // 5120 GEMMs lose 3-8 % persistent and stay one tile per workgroup
+    const int ntiles8 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+    const bool pers = g_fp8_persistent > 0 && ntiles8 >= 4 * device_cus() && p.K >= 256 && p.K <= 2048 && !p.epi_staged &&
+                      direct_ok(p) && (!p.resid || g_fp8_persistent > 1);
     switch (p.epi) {
       case EPI_BF16:
+        if (pers && f == 0) return launch_ppp<true, EPI_BF16, 1, 0, 0>(p, s);
+        if (pers && f == 2) return launch_ppp<true, EPI_BF16, 1, 1, 0>(p, s);
         if (f == 0) return launch_pp<true, true, true, EPI_BF16, 1, 0, 0>(p, s);
         if (f == 2) return launch_pp<true, true, true, EPI_BF16, 1, 1, 0>(p, s);
         break;
       case EPI_GELU:
+        if (pers && f == 0) return launch_ppp<true, EPI_GELU, 1, 0, 0>(p, s);
         if (f == 0) return launch_pp<true, true, true, EPI_GELU, 1, 0, 0>(p, s);
         break;
       case EPI_DGELU:

@@ -52,7 +52,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--persistent", type=int, default=None, help="ext.set_fp8_persistent mode (A/B)")
     a = ap.parse_args()
+    if a.persistent is not None:
+        _ext.ext().set_fp8_persistent(a.persistent)
+        print(f"# fp8 persistent GEMM mode {a.persistent}", flush=True)
     dev = "cuda"
     D, M, N = 1280, 5120, 257
     T = a.batch * N

@@ -1,11 +1,13 @@
 #!/bin/bash
-# GPU session: fp8 GEMM checks, fp8 GEMMs vs torch._scaled_mm, counters, H/14 bench (round 4)
+# GPU session: fp8 persistent GEMM - kernel checks, per-GEMM A/B vs torch._scaled_mm, H/14 benches
 R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 O=gpurun_out/${1:-g8}; mkdir -p "$O"
 step() { local t=$1 log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "[$log] rc=$rc"; tail -n 1 "$O/$log" | cut -c1-160; [ $rc -eq 0 ] || exit $rc; }
 step 600 kernel_checks.log python -u -m pytest tests/test_gpu_kernels.py -q -p no:cacheprovider --timeout 120 --timeout-method thread -x
-step 300 fp8_vs_scaled_mm.log python scripts/fp8_vs_scaled_mm.py
-grep -v amdgpu.ids "$O/fp8_vs_scaled_mm.log"
-step 300 probe_h14.log python scripts/fc1_epi_probe.py --model h14
-step 300 h14_def.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4
-timeout -k 10 400 bash scripts/pmc_gemm.sh "$(basename "$O")/pmc"
+for m in 0 1 2; do
+  step 300 fp8_mm_p$m.log python scripts/fp8_vs_scaled_mm.py --rounds 3 --persistent $m
+  grep -v amdgpu.ids "$O/fp8_mm_p$m.log" | grep -E "fwd|dgrad"
+done
+for m in 0 1 2 1; do
+  step 300 h14_p$m.log python bench.py --model vit_h14 --dtype fp8 --batch 256 --steps 8 --warmup 4 --fp8-persistent $m
+done

@@ -686,6 +686,45 @@ def check_gemm_fp8(M, N, K, resid=False, gelu=False):
     return (f"gemm_fp8 e4m3 M{M} N{N} K{K} r{int(resid)} g{int(gelu)}", m, lim(3.5e-3, 6e-3, bf16_l2=6.5e-2))
 
 
+def check_gemm_fp8_persistent(M=16384, N=4096, K=384):
+    """The persistent fp8 ping-pong (tile 13 form, >= 4 output tiles per CU) against the one-tile-per-
+    workgroup kernel (ext.set_fp8_persistent(0)) on the same operands: bias, bias + residual, and
+    the GELU epilogue with dropout, derivative and the e4m3 copy + amax. Same MFMA order and the same
+    epilogue code, so every output must be bit-identical."""
+    from pytorch_vit_paper_replication_amd.ops import fp8 as F8
+
+    ext = _ext.ext()
+    x, w = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05))
+    xq, xs, _ = _fp8_operand(x)
+    wq, ws, _ = _fp8_operand(w)
+    b = rnd(N)
+    r = bf(rnd(M, N))
+    seed = torch.tensor([77], dtype=torch.int64, device=DEV)
+
+    def run(mode):
+        ext.set_fp8_persistent(mode)
+        try:
+            meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+            meta.calibrated[0] = True
+            meta.qscale.fill_(40.0)
+            meta.dscale.copy_(1.0 / meta.qscale)
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            y0 = F8.linear_fwd_fp8(xq, xs, wq, ws, b)
+            y1 = F8.linear_fwd_fp8(xq, xs, wq, ws, b, resid=r)
+            y2, (q, _) = F8.linear_fwd_fp8(xq, xs, wq, ws, b, gelu_aux=aux, drop=(seed, 5 << 32, 0.1), quant=meta.producer(0))
+            torch.cuda.synchronize()
+            return [y0, y1, y2, aux, q, meta.amax.clone()]
+        finally:
+            ext.set_fp8_persistent(1)
+
+    ref, got = run(0), run(2)
+    ndiff = sum(int((a.view(torch.uint8) != c.view(torch.uint8)).sum().item()) if a.dtype != torch.int32 else int((a != c).sum().item())
+                for a, c in zip(ref, got))
+    m = {"differing_bytes": float(ndiff), "nonfinite": float(not torch.isfinite(got[2].float()).all().item())}
+    return (f"gemm_fp8 persistent vs one-tile kernel M{M} N{N} K{K} (bias / resid / GELU+drop+e4m3)", m,
+            {"differing_bytes": 0, "nonfinite": 0})
+
+
 def _fp8_code_dist(q: torch.Tensor, ref: torch.Tensor) -> float:
     """Largest distance between two fp8 byte tensors in representable steps (sign-magnitude codes:
     adjacent magnitudes are one step apart; a sign flip counts the steps through zero)."""
@@ -1475,6 +1514,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd(2, 577, 2, 64, True),  # tail split + bias partials from the tail's final dQ pass
         lambda: check_attn_bwd(2, 577, 2, 64, True, slab=False),  # same with f32-atomic dQ (A/B variant)
         lambda: check_attn_bwd(2, 577, 3, 80, False, slab=False),
+        check_gemm_fp8_persistent,
         lambda: check_attn_bwd_q8(2, 257, 3, 80),    # e5m2 dQKV copy: lastkey path (pre-pass writes key N - 1)
         lambda: check_attn_bwd_q8(2, 577, 2, 64),    # tail split (body dK/dV, tail's final dQ pass)
         lambda: check_attn_bwd_q8(3, 197, 2, 80, 0.1),  # one key block, attention dropout
