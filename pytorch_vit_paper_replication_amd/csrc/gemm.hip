@@ -1865,7 +1865,9 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
         if (pers && f == 0) return launch_ppp<true, EPI_GELU, 1, 0, 0>(p, s);
         if (f == 0) return launch_pp<true, true, true, EPI_GELU, 1, 0, 0>(p, s);
         break;
-      case EPI_DGELU:
+      case EPI_DGELU:  // mode 3 (A/B only): the dGELU dgrad persistent too - its up-front derivative-factor
+                       // loads drain the next tile's DMAs: 0.565 -> 0.632 ms (profiles/r4/g8c)
+        if (pers && g_fp8_persistent > 2 && f == 2) return launch_ppp<true, EPI_DGELU, 1, 1, 0>(p, s);
         if (f == 2) return launch_pp<true, true, true, EPI_DGELU, 1, 1, 0>(p, s);
         break;
     }

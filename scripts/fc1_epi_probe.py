@@ -42,7 +42,10 @@ class Meta:  # one delayed-scaling slot
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="h14")
+    ap.add_argument("--persistent", type=int, default=None, help="ext.set_fp8_persistent mode (A/B)")
     a = ap.parse_args()
+    if a.persistent is not None:
+        _ext.ext().set_fp8_persistent(a.persistent)
     dev = "cuda"
     D, M, B = (1280, 5120, 256) if a.model == "h14" else (768, 3072, 256)
     T = B * (257 if a.model == "h14" else 197)

@@ -712,17 +712,26 @@ def check_gemm_fp8_persistent(M=16384, N=4096, K=384):
             y0 = F8.linear_fwd_fp8(xq, xs, wq, ws, b)
             y1 = F8.linear_fwd_fp8(xq, xs, wq, ws, b, resid=r)
             y2, (q, _) = F8.linear_fwd_fp8(xq, xs, wq, ws, b, gelu_aux=aux, drop=(seed, 5 << 32, 0.1), quant=meta.producer(0))
+            # dGELU dgrad (mode 3): e5m2 gradient x e4m3 W^T rows, derivative factor, column sums, e5m2 copy
+            m5 = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2)
+            m5.calibrated[0] = True
+            m5.qscale.fill_(3.0)
+            m5.dscale.copy_(1.0 / m5.qscale)
+            cs = torch.zeros(N, device=DEV)
+            y3, (q3, _) = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=aux, colsum=cs, quant=m5.producer(0))
             torch.cuda.synchronize()
-            return [y0, y1, y2, aux, q, meta.amax.clone()]
+            return [y0, y1, y2, aux, q, meta.amax.clone(), y3, q3, m5.amax.clone()], cs
         finally:
             ext.set_fp8_persistent(1)
 
-    ref, got = run(0), run(2)
+    gq, gs, _ = _fp8_operand(bf(rnd(M, K, scale=0.01)), 1)
+    (ref, cs0), (got, cs1) = run(0), run(3)
     ndiff = sum(int((a.view(torch.uint8) != c.view(torch.uint8)).sum().item()) if a.dtype != torch.int32 else int((a != c).sum().item())
                 for a, c in zip(ref, got))
-    m = {"differing_bytes": float(ndiff), "nonfinite": float(not torch.isfinite(got[2].float()).all().item())}
-    return (f"gemm_fp8 persistent vs one-tile kernel M{M} N{N} K{K} (bias / resid / GELU+drop+e4m3)", m,
-            {"differing_bytes": 0, "nonfinite": 0})
+    m = {"differing_bytes": float(ndiff), "nonfinite": float(not torch.isfinite(got[2].float()).all().item()),
+         "colsum_rel": errs(cs1, cs0)[0]}
+    return (f"gemm_fp8 persistent vs one-tile kernel M{M} N{N} K{K} (bias / resid / GELU+drop+e4m3 / dGELU+colsum+e5m2)", m,
+            {"differing_bytes": 0, "nonfinite": 0, "colsum_rel": 1e-5})  # column sums: f32 atomics, any order
 
 
 def _fp8_code_dist(q: torch.Tensor, ref: torch.Tensor) -> float:
