@@ -56,6 +56,8 @@ def parse():
                    help="A/B: weight-gradient batches whose inputs stay held at once (0 = no count bound)")
     p.add_argument("--side-hold-gb", type=float, default=None,
                    help="A/B: GB of weight-gradient inputs held at once (0 = until the end of backward)")
+    p.add_argument("--persistent-max-k", type=int, default=None,
+                   help="A/B: bf16 GEMMs on the persistent ping-pong only up to this K (default: any K)")
     p.add_argument("--fp8-persistent", type=int, default=None,
                    help="fp8 GEMMs on the persistent ping-pong: 0 never, 1 no per-row inputs (default), 2 also residual (A/B)")
     p.add_argument("--no-gemm-tail", action="store_true",
@@ -126,6 +128,10 @@ def main():
         if args.side_hold_gb is not None:
             param_store.SIDE_HOLD_BYTES = int(args.side_hold_gb * 2**30)
     rank, world, device = init_distributed()
+    if args.persistent_max_k is not None:
+        from pytorch_vit_paper_replication_amd.ops import gemm as _gemm
+
+        _gemm.PERSISTENT_MAX_K = args.persistent_max_k
     if args.fp8_persistent is not None and args.impl == "fused":
         from pytorch_vit_paper_replication_amd import _ext
 

@@ -30,6 +30,10 @@ def _n_cus() -> int:
 _N_CUS = None
 # test hook (tests/kernel_checks.py): force one tile config for every GEMM while set
 FORCE_TILE: Optional[int] = None
+# bf16 persistent ping-pong (13) only up to this K (None: any K). A/B knob (bench.py --persistent-max-k):
+# unlike the fp8 kernels, the long-K bf16 GEMMs do not lose on the persistent form (ViT-L/16@384 b128
+# 722 img/s any K vs 719 with K <= 2048, same box: profiles/r4/pmaxk/)
+PERSISTENT_MAX_K: Optional[int] = None
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
@@ -54,7 +58,8 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
         # the next tile's first K-tile (qkv fwd 0.171-0.179 vs 0.183-0.185 ms, fc1 GELU fwd 0.347-0.352
         # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log). The dGELU
         # dgrad (column-sum exchange at every tile end) stays on 12: 0.300 vs 0.325 ms (profiles/r3/gemm_ab.log)
-        if K >= 128 and not dgelu and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
+        if (K >= 128 and not dgelu and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus()
+                and (PERSISTENT_MAX_K is None or K <= PERSISTENT_MAX_K)):
             return 13
         return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
