@@ -1032,10 +1032,15 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
           gelu_and_grad2((v2f){v[2 * q], v[2 * q + 1]}, g2, d2);
           g2 *= s2;
           d2 *= s2;
-          out[q] = pack2bf(g2.x, g2.y);
           ax[q] = pack2bf(d2.x, d2.y);
-          v[2 * q] = g2.x;  // the output, for the fp8 copy
+          v[2 * q] = g2.x;  // the output (bf16 below, the fp8 copy)
           v[2 * q + 1] = g2.y;
+        }
+        if (!p.c_skip) {  // uniform; c_skip: stored to a 0-byte range (the store count stays fixed)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) out[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+        } else {
+          out = v4u{0u, 0u, 0u, 0u};
         }
         __builtin_amdgcn_raw_buffer_store_b128(ax, xrs, vx[jp] + so_x, 0, 0);  // no aux (inference): 0-byte resource
       } else {  // EPI_DGELU
@@ -1046,8 +1051,12 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) csum[jp][e] += v[e];
+        if (!p.c_skip) {  // uniform; c_skip: stored to a 0-byte range (the store count stays fixed)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) out[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+          for (int q = 0; q < 4; ++q) out[q] = pack2bf(v[2 * q], v[2 * q + 1]);
+        } else {
+          out = v4u{0u, 0u, 0u, 0u};
+        }
       }
       __builtin_amdgcn_raw_buffer_store_b128(out, crs, vc[jp] + so_c, 0, 0);
       if constexpr (QOK) {
