@@ -17,14 +17,48 @@ _ERR: BaseException | None = None
 _TRIED = False
 
 
+class StaleExtensionError(RuntimeError):
+    """The in-tree ``_C`` was built from other ``csrc/`` sources than the ones in the tree."""
+
+
+def check_source_hash(so, csrc) -> str:
+    """Compare the source hash compiled into ``so`` with the hash of the sources in ``csrc``;
+    returns the hash, raises :class:`StaleExtensionError` on a mismatch (or a binary without one)."""
+    from .build import embedded_hash, source_hash
+
+    want = source_hash(csrc)
+    have = embedded_hash(so)
+    if have != want:
+        raise StaleExtensionError(
+            f"{so} was built from other sources (binary {have}, csrc/ {want}): rebuild with "
+            "`python -m pytorch_vit_paper_replication_amd.build` (or set PVR_AUTOBUILD=1)")
+    return want
+
+
 def load():
-    """Import the compiled extension once; returns the module or None."""
+    """Import the compiled extension once; returns the module or None.
+
+    The binary must carry the content hash of the ``csrc/`` sources next to it (build.py compiles
+    it in): a stale ``_C`` is rebuilt first under ``PVR_AUTOBUILD=1`` and refused otherwise, so an
+    edited kernel can never be tested through an old binary."""
     global _C, _ERR, _TRIED
     if _TRIED:
         return _C
     _TRIED = True
     debug = os.environ.get("PVR_DEBUG_KERNELS", "0") == "1"
     try:
+        from .build import CSRC, ext_path
+
+        if CSRC.is_dir() and ext_path(debug).exists():
+            try:
+                check_source_hash(ext_path(debug), CSRC)
+            except StaleExtensionError:
+                if os.environ.get("PVR_AUTOBUILD", "0") != "1":
+                    raise
+                from .build import build_extension
+
+                build_extension(debug=debug)
+                check_source_hash(ext_path(debug), CSRC)
         if debug:  # kernels with device-side invariant checks (build_extension(debug=True))
             from . import _C_debug as mod  # noqa: F401
         else:

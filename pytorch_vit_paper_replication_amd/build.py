@@ -41,6 +41,34 @@ def _hipcc() -> str:
     return str(Path(rocm) / "bin" / "hipcc")
 
 
+HASH_TAG = b"PVR_SRC_HASH="
+
+
+def source_hash(csrc: Path = CSRC) -> str:
+    """Content hash of every native source (``csrc/*.hip|*.h|*.cpp``, by name and bytes): the
+    identity compiled into ``_C`` so that :mod:`._ext` can refuse a binary built from other sources."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(p for p in Path(csrc).iterdir() if p.suffix in (".hip", ".h", ".cpp")):
+        h.update(f.name.encode() + b"\0")
+        h.update(f.read_bytes())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(so: Path) -> str | None:
+    """The source hash a built ``_C`` carries (read from the file, without importing it)."""
+    try:
+        data = Path(so).read_bytes()
+    except OSError:
+        return None
+    i = data.find(HASH_TAG)
+    if i < 0:
+        return None
+    return data[i + len(HASH_TAG):i + len(HASH_TAG) + 16].decode("ascii", "replace")
+
+
 def _newer(src_files, target: Path) -> bool:
     if not target.exists():
         return True
@@ -106,8 +134,21 @@ def build_extension(verbose: bool = False, force: bool = False, jobs: int | None
             for out in ex.map(_run, jobs_list):
                 if verbose and out.strip():
                     print(out)
+    # the source identity: a tiny C unit holding the tag, regenerated whenever the hash changes
+    # (a rebuild from the same sources keeps it, so the incremental check stays exact)
+    shash = source_hash()
+    hsrc = build_dir / "src_hash.c"
+    htext = (f'__attribute__((used)) const char pvr_src_hash_tag[] = "{HASH_TAG.decode()}{shash}";\n'
+             'const char* pvr_src_hash(void) { return pvr_src_hash_tag + ' + str(len(HASH_TAG)) + '; }\n')
+    if not hsrc.exists() or hsrc.read_text() != htext:
+        hsrc.write_text(htext)
+    hobj = build_dir / "src_hash.o"
+    hash_changed = force or _newer([hsrc], hobj)
+    if hash_changed:
+        _run([os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-c", str(hsrc), "-o", str(hobj)])
+    objs.append(hobj)
     so = ext_path(debug)
-    if force or jobs_list or not so.exists():
+    if force or jobs_list or hash_changed or not so.exists() or embedded_hash(so) != shash:
         link = [
             _hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(so),
             f"-L{lib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",

@@ -156,6 +156,8 @@ void attach_tail(pvr::GemmParams& p, const torch::Tensor& like) {
 void set_gemm_tail(bool on) { g_gemm_tail = on; }
 static int g_tail_min_kt = 12;
 void set_gemm_tail_min_kt(int64_t n) { g_tail_min_kt = (int)n; }
+static int g_gemm_skew = 0;
+void set_gemm_skew(int64_t c) { g_gemm_skew = (int)c; }
 
 // C = A . B^T with the given operand layouts; see csrc/gemm.hip for the epilogue contract.
 void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torch::Tensor C, int64_t M, int64_t N, int64_t K,
@@ -214,6 +216,7 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   p.k_split_len = k_split > 0 ? (int)(((k_split + 63) / 64) * 64) : (int)(((K + 63) / 64) * 64);
   p.epi = (int)epi;
   p.tile_cfg = (int)tile_cfg;
+  p.skew_cycles = g_gemm_skew;
   // tail_limit: -1 = no split tail, 0 = unlimited, n > 0 = at most n workgroups in the split round
   if (epi <= 2 && p.k_split_len >= K && tail_limit >= 0) {
     attach_tail(p, C);
@@ -993,8 +996,12 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
 
 }  // namespace
 
+extern "C" const char* pvr_src_hash(void);  // _build/src_hash.c (build.py): hash of csrc/*
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for pytorch_vit_paper_replication_amd";
+  m.def("source_hash", []() { return std::string(pvr_src_hash()); },
+        "content hash of the csrc/ sources this binary was built from (build.source_hash())");
   m.def("gemm_tail_split", [](int64_t M, int64_t N, int64_t K, int64_t elem_bytes, int64_t max_units) {
     return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes, (int)max_units); },
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
@@ -1004,6 +1011,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_attn_fwd_direct", &pvr_set_attn_fwd_direct, "attention forward: O stores straight from registers (1) or through LDS (0, default; A/B)");
   m.def("set_attn_bwd_slab", &pvr_set_attn_bwd_slab, "multi-block attention backward: dQ through f32 slabs (1, default) or f32 atomics (0; A/B)");
   m.def("set_gemm_tail_min_kt", &set_gemm_tail_min_kt, "fewest K-tiles per split-tail part (default 12; A/B)");
+  m.def("set_gemm_skew", &set_gemm_skew, "A/B: first-round workgroup start skew in shader cycles (0 = off)");
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

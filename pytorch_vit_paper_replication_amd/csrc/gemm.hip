@@ -35,6 +35,14 @@ enum GemmEpi : int {
 
 namespace {
 
+PVR_DEV void start_skew(const GemmParams& p, int b) {
+  if (p.skew_cycles > 0 && b < 256) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t w = (uint64_t)p.skew_cycles * (uint64_t)(b & 3);
+    while (__builtin_amdgcn_s_memtime() - t0 < w) __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 PVR_DEV void stamp(const GemmParams& p, int slot) {
   if (p.dbg && threadIdx.x == 0) {
     const int b = blockIdx.x + gridDim.x * blockIdx.z;
@@ -1443,6 +1451,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   v8s af[4][2], bf[2][2][2];
 
+  if (tpart < 0) start_skew(p, (int)blockIdx.x);
   stamp(p, 0);
   // prologue: half-tiles 0..5 = all of K-tile 0, A0/B0 of K-tile 1
   pp_issue<0, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
@@ -1690,6 +1699,7 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   const int nk = p.K / (128 / ES);  // K-tiles of 128 B (64 bf16 / 128 fp8); >= 2 (host check)
   int v = blockIdx.x;
   if (v >= ntiles) return;
+  start_skew(p, v);
 
   PppTile cur = ppp_tile<ES>(p, v, ntiles, ntn);
   PppTile nxt = ppp_tile<ES>(p, v + gridDim.x, ntiles, ntn);

@@ -88,6 +88,14 @@ def main():
     variants = [("", lambda: None)]
     if a.ab == "tail":
         variants = [("tail on ", lambda: ext.set_gemm_tail(True)), ("tail off", lambda: ext.set_gemm_tail(False))]
+    elif a.ab.startswith("skew:"):
+        # skew:0,6000,12000 - first-round workgroup start skew (shader cycles per step of b & 3)
+        variants = [(f"sk{c:6s}", (lambda c=c: ext.set_gemm_skew(int(c)))) for c in a.ab.split(":", 1)[1].split(",")]
+    elif a.ab.startswith("tiles:"):
+        # tiles:def,7,8 - the default tile selection vs forced tile configs (every case)
+        def force(t):
+            return lambda: setattr(G, "FORCE_TILE", None if t == "def" else int(t))
+        variants = [(f"t{t:6s}", force(t)) for t in a.ab.split(":", 1)[1].split(",")]
     cs = [c for c in cases(T, D, M, dev) if not a.only or any(s in c[0] for s in a.only.split(","))]
     res = {}
     for rnd in range(a.rounds):
@@ -103,6 +111,8 @@ def main():
             if rnd % 2 == 0:
                 res.setdefault((name, "lib"), []).append(timeit(lib))
     ext.set_gemm_tail(True)
+    ext.set_gemm_skew(0)
+    G.FORCE_TILE = None
     print(f"# {a.model} batch {a.batch} (T = {T}), {a.rounds} rounds; median (min) ms, TFLOP/s at the median", flush=True)
     for name, fl, _, _ in cs:
         tl = statistics.median(res[(name, "lib")])
