@@ -29,7 +29,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 256 @1 GPU, 512/GPU @>1)")
+    p.add_argument("--batch", type=int, default=None,
+                   help="per-GPU batch (default: ViT-B/16 256 on 1 GPU, 512 per GPU on more; ViT-L/16 128; ViT-H/14 256)")
     p.add_argument("--model", default="vit_b16")
     p.add_argument("--image-size", type=int, default=224)
     p.add_argument("--num-classes", type=int, default=1000)
@@ -56,10 +57,6 @@ def parse():
                    help="A/B: weight-gradient batches whose inputs stay held at once (0 = no count bound)")
     p.add_argument("--side-hold-gb", type=float, default=None,
                    help="A/B: GB of weight-gradient inputs held at once (0 = until the end of backward)")
-    p.add_argument("--persistent-max-k", type=int, default=None,
-                   help="A/B: bf16 GEMMs on the persistent ping-pong only up to this K (default: any K)")
-    p.add_argument("--fp8-persistent", type=int, default=None,
-                   help="fp8 GEMMs on the persistent ping-pong: 0 never, 1 no per-row inputs (default), 2 also residual (A/B)")
     p.add_argument("--no-gemm-tail", action="store_true",
                    help="A/B: no split-K tail on the last dispatch round of the one-tile-per-workgroup GEMMs")
     p.add_argument("--main-prio", type=int, default=-1,
@@ -69,13 +66,42 @@ def parse():
 
 MODEL_NAMES = {"vit_b16": "ViT-B/16", "vit_l16": "ViT-L/16", "vit_h14": "ViT-H/14"}
 
+# Per-GPU batch when --batch is not given: BASELINE config 2 (ViT-B/16, 1 GPU) is batch 256; the
+# data-parallel configs use a per-GPU batch sized to fit one MI355X's 288 GB with margin (configs 3-5:
+# ViT-B/16 512 -> 4096 on 8 GPUs; ViT-L/16@384 128; ViT-H/14 fp8 256, ~134 GB measured at b256).
+PER_GPU_BATCH = {"vit_b16": 512, "vit_l16": 128, "vit_h14": 256}
+# Peak-memory model for the fail-fast check, fitted to measured peaks (bench.py's peak_mem_gb):
+# GB = fixed + per_image * batch * (tokens / tokens_ref); profiles/r4/final2 and profiles/r5/configs
+MEM_MODEL = {  # model: (fixed GB, GB per image at the reference token count, reference tokens)
+    "vit_b16": (2.0, 0.0622, 197),    # b256: 17.9 GB
+    "vit_l16": (5.5, 0.4556, 577),    # 384 px b128: 63.8 GB
+    "vit_h14": (12.0, 0.477, 257),    # fp8 b256: 134.2 GB
+}
+
+
+def default_per_gpu_batch(model: str, world: int) -> int:
+    if model == "vit_b16" and world == 1:
+        return 256
+    return PER_GPU_BATCH.get(model, 256 if world == 1 else 512)
+
+
+def estimate_peak_gb(model: str, image_size: int, batch: int) -> float | None:
+    """Peak device memory of one training step (None: model not calibrated)."""
+    from pytorch_vit_paper_replication_amd.models.presets import PRESETS
+
+    if model not in MEM_MODEL or model not in PRESETS:
+        return None
+    fixed, per_img, tok_ref = MEM_MODEL[model]
+    tokens = (image_size // int(PRESETS[model]["patch_size"])) ** 2 + 1
+    return fixed + per_img * batch * tokens / tok_ref
+
 
 def describe(args, world: int) -> dict:
     """The run's configuration as reported (and as BASELINE.json names it), from the arguments and the
     world size alone: no GPU or model needed (tests/test_bench_cli.py checks configs 2-5 with it)."""
     from pytorch_vit_paper_replication_amd.models.presets import PRESETS
 
-    per_gpu = args.batch or (256 if world == 1 else 512)
+    per_gpu = args.batch or default_per_gpu_batch(args.model, world)
     name = MODEL_NAMES.get(args.model, args.model)
     patch = int(PRESETS[args.model]["patch_size"]) if args.model in PRESETS else 16
     if args.infer:
@@ -128,14 +154,6 @@ def main():
         if args.side_hold_gb is not None:
             param_store.SIDE_HOLD_BYTES = int(args.side_hold_gb * 2**30)
     rank, world, device = init_distributed()
-    if args.persistent_max_k is not None:
-        from pytorch_vit_paper_replication_amd.ops import gemm as _gemm
-
-        _gemm.PERSISTENT_MAX_K = args.persistent_max_k
-    if args.fp8_persistent is not None and args.impl == "fused":
-        from pytorch_vit_paper_replication_amd import _ext
-
-        _ext.ext().set_fp8_persistent(args.fp8_persistent)
     if args.no_gemm_tail and args.impl == "fused":
         from pytorch_vit_paper_replication_amd import _ext
 
@@ -151,6 +169,11 @@ def main():
                                              timeout=datetime.timedelta(seconds=600))
     desc = describe(args, world)
     per_gpu = desc["per_gpu_batch"]
+    est = estimate_peak_gb(args.model, args.image_size, per_gpu) if not args.infer else None
+    hbm = torch.cuda.get_device_properties(device).total_memory / 2**30
+    if est is not None and est > 0.95 * hbm:
+        raise SystemExit(f"bench.py: {desc['name']} at {args.image_size} px needs ~{est:.0f} GB per GPU at batch {per_gpu} "
+                         f"(device has {hbm:.0f} GB); pass a smaller --batch (default {default_per_gpu_batch(args.model, world)})")
     torch.manual_seed(1234)
 
     model = vit(args.model, image_size=args.image_size, num_classes=args.num_classes).to(device)

@@ -88,6 +88,35 @@ def available() -> bool:
     return load() is not None
 
 
+_DETERMINISTIC_ENV = os.environ.get("PVR_DETERMINISTIC", "0") not in ("", "0")
+
+
+def deterministic() -> bool:
+    """Deterministic reductions on the fused path (``set_deterministic`` / ``PVR_DETERMINISTIC=1`` /
+    ``torch.use_deterministic_algorithms(True)``): every bias / LayerNorm-parameter gradient and the
+    weight gradients are reduced in a fixed order, so a training step produces the same bits on every
+    run. Off by default: the float-atomic reductions are order-dependent in the last bits."""
+    m = _C if _TRIED else load()
+    on = torch.are_deterministic_algorithms_enabled() or _DETERMINISTIC_ENV
+    if m is not None and bool(m.deterministic()) != on:
+        m.set_deterministic(on)
+    return on
+
+
+@contextlib.contextmanager
+def deterministic_mode(on: bool = True):
+    """Context: deterministic reductions inside the block (see :func:`deterministic`)."""
+    global _DETERMINISTIC_ENV
+    old = _DETERMINISTIC_ENV
+    _DETERMINISTIC_ENV = on
+    try:
+        deterministic()
+        yield
+    finally:
+        _DETERMINISTIC_ENV = old
+        deterministic()
+
+
 def ext():
     m = load()
     if m is None:

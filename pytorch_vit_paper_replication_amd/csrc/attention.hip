@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
   // (dh 64 without the copy: 128-B rows, whose direct stores already fill whole lines - measured
   // 0.303 direct vs 0.308 staged at ViT-L/16@384; dh 80: 0.283 -> 0.269, with the copy 0.332 -> 0.296;
   // profiles/r4/aq8/attn_q8_ab.log)
-  const bool staged = !q8.direct && (qon || DH != 64) && (((uintptr_t)out | (uintptr_t)(ld_o * 2)) & 15) == 0 &&
+  const bool staged = (qon || DH != 64) && (((uintptr_t)out | (uintptr_t)(ld_o * 2)) & 15) == 0 &&
                       (!qon || (((uintptr_t)q8.out | (uintptr_t)q8.ld) & 15) == 0);
   const float qs = qon ? *q8.qs : 1.f;
 #pragma unroll
@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   const __amdgpu_buffer_rsrc_t krs = make_rsrc(base + D + h * DH, clamp_bytes(extent));
   const uint16_t* dobase = dout + (int64_t)b * N * ld_do;
   const __amdgpu_buffer_rsrc_t dors = make_rsrc(dobase + h * DH, clamp_bytes(((int64_t)(N - 1) * ld_do + DH) * 2));
-  // dQ destination of this batch. dq_mode 0-2 with dq_acc: f32 atomics into the accumulator [N][D];
+  // dQ destination of this batch. dq_mode 0 with dq_acc: f32 atomics into the accumulator [N][D];
   // dq_mode 3 (key-block body of a multi-block head): plain f32 stores of this key block's partial
   // dQ into slab (L % nkb) of dq_acc [slabs][B*N][D] (6 TB/s stores instead of 1.3 TB/s atomics);
   // dq_mode 4 (the tail launch after a mode-3 body): its own partial into slab nslab, then the
@@ -789,7 +789,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   dq_block(nqb - 1, slq_prev);
   // bpart (the launch that writes the final dQ): this pair's q-bias partials, the column sums of the
   // wave's dQ fragments over all query blocks -> [bh][a][16e + li] (the pre-pass adds the v sums)
-  if (bpart && dq_mode == 0) {  // (modes 1, 2, 4: the final pass below writes them)
+  if (bpart && dq_mode == 0) {  // (mode 4: the final pass below writes them)
     int kfr = 0;
     for (int fr = wave; fr < 2 * C::NE && kfr < 2; fr += NW, ++kfr) {
       float cs = kfr == 0 ? dqb0 : dqb1;
@@ -885,9 +885,6 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     if (lane == 0) amax_record(q8.amax, q8am);
   }
   // Final dQ pass of the last launch of a multi-block head (one workgroup per (batch, head)):
-  //   dq_mode 1 / 2: the other key blocks' f32 atomics landed before this launch started and this
-  //     workgroup's own are acknowledged after the wait below: convert the pair's accumulated rows
-  //     (and, in mode 2, zero them again for the next use of a persistent workspace);
   //   dq_mode 4: every key block stored its partial dQ as an f32 slab (the body launch before this
   //     one, this workgroup's own just now): sum the nslab + 1 slabs in slab order (deterministic).
   // Coalesced 16-B loads; writes the final dQ: bf16 (unless only the fp8 copy is wanted), its e5m2
@@ -895,7 +892,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   // (no agent-scope fence: it would write back the whole L2. The body launch completed before this
   // one started; this workgroup's own stores / atomics performed in its XCD's L2, which the loads
   // below go through; the CU's L1 holds no line of these rows.)
-  if ((dq_mode == 1 || dq_mode == 2 || dq_mode == 4) && dq_acc) {
+  if (dq_mode == 4 && dq_acc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     constexpr int C4 = DH / 4, U = 4;
@@ -912,7 +909,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       v4f sum[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) sum[u] = v4f{0.f, 0.f, 0.f, 0.f};
-      const int nsrc = dq_mode == 4 ? nslab + 1 : 1;
+      const int nsrc = nslab + 1;
       for (int sl = 0; sl < nsrc; ++sl) {
         const __amdgpu_buffer_rsrc_t srs = make_rsrc(dq_acc + sl * slab_stride + (int64_t)b * N * D, sbytes);
         v4u v[U];
@@ -924,10 +921,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
           v[u] = __builtin_amdgcn_raw_buffer_load_b128(srs, off[u], 0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          sum[u] += __builtin_bit_cast(v4f, v[u]);
-          if (dq_mode == 2) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, srs, off[u], 0, 0);
-        }
+        for (int u = 0; u < U; ++u) sum[u] += __builtin_bit_cast(v4f, v[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1589,10 +1583,9 @@ static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t
 // tiles at every head dim (64 KiB of LDS at dh 80: two workgroups per CU). QG 2 pads the query
 // count to 128 instead of 64: it is chosen only when that padding costs < 10 % more query rows
 // (L/16-384, N = 577: 640 either way, QG 2 0.399 vs 0.440 ms; H/14, N = 257: 384 vs 320 rows, QG 2
-// 0.376 vs 0.319 ms, scripts/attn_ab.py). g_attn_fwd_qg: 0 = that rule, 1 / 2 = forced, 3 = QG 1 with
-// 64-key tiles at every head dim (A/B).
-// forward output through LDS (false, default) or straight from the registers (true: A/B)
-bool g_attn_fwd_direct = false;
+// 0.376 vs 0.319 ms, scripts/attn_ab.py). g_attn_fwd_qg: 0 = that rule, 1 / 2 = forced (A/B of
+// the two production forms). (Measured losers removed in round 5: QG 1 with 64-key tiles at every
+// head dim; O stored straight from the registers instead of through LDS, profiles/r4/aq8.)
 int g_attn_fwd_qg = 0;
 static bool attn_fwd_use_qg2(int N) {
   if (g_attn_fwd_qg) return g_attn_fwd_qg == 2;
@@ -1619,7 +1612,6 @@ static hipError_t attn_fwd_tiled(const uint16_t* qkv, int64_t ld, uint16_t* out,
 template <int DH, bool DROP>
 static hipError_t attn_fwd_tiled_pick(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N, int H,
                                       int D, float scale, const pvr::AttnDrop& drop, const pvr::AttnQ8& q8, hipStream_t s) {
-  if (g_attn_fwd_qg == 3) return attn_fwd_tiled<DH, DROP, 1, 64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);  // A/B
   if (attn_fwd_use_qg2(N)) return attn_fwd_tiled<DH, DROP, 2, 64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
   return attn_fwd_tiled<DH, DROP, 1, (pvr::Hd<DH>::NH == 1 ? 64 : 32)>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
 }
@@ -1646,7 +1638,7 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
   return attn_fwd_tiled_pick<DH, false>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
 }
 
-extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg >= 1 && qg <= 3 ? qg : 0; }
+extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg == 1 || qg == 2 ? qg : 0; }
 
 // seed (optional): attention-probability dropout with keep threshold thr16 (see AttnDrop); the
 // backward must get the same seed / seed_off / thr16
@@ -1657,7 +1649,7 @@ extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* ou
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
   if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
   const AttnDrop drop{seed, seed_off, thr16, keep_scale};
-  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, 0, g_attn_fwd_direct ? 1 : 0};
+  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, 0};
   switch (D / H) {
     case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
     case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
@@ -1693,13 +1685,9 @@ static bool attn_bwd_tail_split(int N, bool dbias, bool drop) {
   const int rem = N % KB;
   return !attn_bwd_lastkey_path(N, dbias, drop) && (N + KB - 1) / KB > 1 && rem >= 16 && rem <= 128 && !dbias;
 }
-// dQ of the tail-split path through f32 slabs summed by the tail (1, default) or f32 atomics
-// converted by the tail (0): 1.215 vs 1.260 ms per ViT-L/16@384 b128 layer, same process
-// (profiles/r4/ab10/attn_ab.log)
-int g_attn_bwd_slab = 1;
-static bool attn_bwd_slab_path(int N, bool dbias, bool drop) { return g_attn_bwd_slab && attn_bwd_tail_split(N, dbias, drop); }
-extern "C" void pvr_set_attn_bwd_slab(int on) { g_attn_bwd_slab = on ? 1 : 0; }
-extern "C" void pvr_set_attn_fwd_direct(int on) { g_attn_fwd_direct = on != 0; }
+// dQ of the tail-split path through f32 slabs summed by the tail (the f32-atomics alternative lost:
+// 1.215 vs 1.260 ms per ViT-L/16@384 b128 layer, same process, profiles/r4/ab10/attn_ab.log; removed)
+static bool attn_bwd_slab_path(int N, bool dbias, bool drop) { return attn_bwd_tail_split(N, dbias, drop); }
 
 // the generic backward's kernels write every final dQ value (no f32 atomics + conversion pass)
 static bool attn_bwd_final_dq_in_kernel(int N, bool dbias, bool drop) {
@@ -1767,7 +1755,7 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
   const bool lastkey = attn_bwd_lastkey_path(N, dbias != nullptr, DROP);
   const int rem_ = N % KB;
   const bool tail_split = !lastkey && nkb > 1 && rem_ >= 16 && rem_ <= 128 && !dbias;
-  const bool slab_path = tail_split && g_attn_bwd_slab;
+  const bool slab_path = tail_split;
   if (nkb > 1 && !dq_acc && !lastkey && !slab_path) return hipErrorInvalidValue;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   if (!ws) return hipErrorInvalidValue;
@@ -1811,18 +1799,12 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
     // 3 live waves holding a CU each (818 vs 862 us at B64 H16). A 1-key tail (257 = 256 + 1, the
     // CLS token of 224/14) takes the lastkey path above instead.
     // The tail launch, one workgroup per (batch, head) running after the body, ends with a final
-    // dQ pass over the pair's rows: f32 atomics of every key block into dq_acc, converted there
-    // (default), or (g_attn_bwd_slab) plain f32 slabs per key block summed there. Either way the
+    // dQ pass over the pair's rows: every key block's f32 slab summed there in slab order; the
     // final pass also writes the e5m2 copy and the q-bias partials.
-    if (slab_path) {
-      const int nslab = (N - rem) / KB;
-      const int64_t sstride = (int64_t)B * N * D;
-      launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
-      launch(pvr_attn_bwd_waves(rem), N - rem, N, 4, slab, sstride, nslab, bpart);
-    } else {
-      launch(NW, 0, N - rem, 0, dq_acc, 0, 0, nullptr);
-      launch(pvr_attn_bwd_waves(rem), N - rem, N, dq_rezero ? 2 : 1, dq_acc, 0, 0, bpart);
-    }
+    const int nslab = (N - rem) / KB;
+    const int64_t sstride = (int64_t)B * N * D;
+    launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
+    launch(pvr_attn_bwd_waves(rem), N - rem, N, 4, slab, sstride, nslab, bpart);
     return hipGetLastError();
   }
   launch(NW, 0, N, 0, nkb > 1 ? dq_acc : nullptr, 0, 0, nkb > 1 ? nullptr : bpart);
@@ -1892,7 +1874,7 @@ extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
   if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
   const pvr::AttnDrop drop{seed, seed_off, thr16, keep_scale};
-  if (q8_only && (!q8_out || dq_acc)) return hipErrorInvalidValue;  // atomics-path dQ needs the bf16 conversion
+  if (q8_only && !q8_out) return hipErrorInvalidValue;
   const pvr::AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, q8_only};
   switch (D / H) {
 #define PVR_BWD_DH(DH) \

@@ -118,7 +118,6 @@ struct AttnQ8 {
   const float* qs;
   unsigned* amax;
   int only;  // backward: store only the fp8 copy, not the bf16 gradient (every reader takes the copy)
-  int direct;  // forward: store O (and its copy) straight from the registers instead of through LDS (A/B)
 };
 // max|x| record with few same-address atomics: most waves find the running amax already larger
 PVR_DEV void amax_record(unsigned* amax, float m) {

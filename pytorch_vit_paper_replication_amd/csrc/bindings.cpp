@@ -1,3 +1,4 @@
+#include <cstdlib>
 // pybind11 / ATen bindings for the gfx950 kernels. Every entry point launches on PyTorch's current
 // HIP stream (so it composes with torch streams, events and hipGraph capture) and validates dtypes,
 // shapes and strides before touching device memory.
@@ -23,27 +24,28 @@ extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
 void pvr_set_attn_fwd_qg(int qg);
-void pvr_set_attn_bwd_slab(int on);
-void pvr_set_attn_fwd_direct(int on);
 void pvr_set_fp8_persistent(int mode);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
-hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, uint8_t*, int64_t, const float*, unsigned*, int, int, hipStream_t);
+hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, uint8_t*, int64_t, const float*, unsigned*, int, int, float*, hipStream_t);
+int pvr_layernorm_bwd_blocks(int, int);
+int pvr_colsum_part_rows(int);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
 hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, int, int, hipStream_t);
 hipError_t pvr_pad_cols_bf16(const uint16_t*, int, int, uint16_t*, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t,
-                      const float*, unsigned*, hipStream_t);
+                      const float*, unsigned*, float*, hipStream_t);
 hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
 hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 int pvr_patch_bwd_groups(int);
+int64_t pvr_patch_bwd_ws_floats(int, int, int);
 hipError_t pvr_head_fwd(const uint16_t*, int64_t, int, int, const float*, const float*, float, const float*, const float*, int, float*, float*,
                         float*, hipStream_t);
 hipError_t pvr_head_bwd(const float*, const float*, const float*, const float*, const float*, const float*, int, int, int, int, float*,
-                        float*, float*, float*, float*, uint16_t*, hipStream_t);
+                        float*, float*, float*, float*, uint16_t*, float*, hipStream_t);
 hipError_t pvr_scale_by(const float*, const float*, float*, int64_t, hipStream_t);
 hipError_t pvr_mean(const float*, int, float*, hipStream_t);
 hipError_t pvr_metrics_accum(float*, const float*, const int*, int, hipStream_t);
@@ -154,10 +156,30 @@ void attach_tail(pvr::GemmParams& p, const torch::Tensor& like) {
   p.tail_cnt_elems = (int)it->second.cnt.numel();
 }
 void set_gemm_tail(bool on) { g_gemm_tail = on; }
-static int g_tail_min_kt = 12;
-void set_gemm_tail_min_kt(int64_t n) { g_tail_min_kt = (int)n; }
-static int g_gemm_skew = 0;
-void set_gemm_skew(int64_t c) { g_gemm_skew = (int)c; }
+// fewest K-tiles per split-tail part: 12 (6 / 4 / 3 measured no better or worse on the short-K
+// GEMMs, profiles/r4/ab14/tail_kt.log)
+constexpr int g_tail_min_kt = 12;
+
+// Deterministic mode (set_deterministic): the reductions that otherwise add float atomics in
+// arrival order (LayerNorm backward dgamma / dbeta / fused bias sums, the column-sum kernel, the
+// classifier LayerNorm's dgamma / dbeta) write one partial row per workgroup instead and an ordered
+// pass sums the rows: every run of a step produces the same bits (bit-exact resume).
+bool g_deterministic = [] {
+  const char* e = std::getenv("PVR_DETERMINISTIC");
+  return e && std::atoi(e) != 0;
+}();
+void set_deterministic(bool on) { g_deterministic = on; }
+bool deterministic() { return g_deterministic; }
+// partial-row scratch of the deterministic reductions, one per (device, stream), grown on demand
+float* det_scratch(int64_t numel, const torch::TensorOptions& opts) {
+  static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
+  torch::Tensor*& t = cache[std::make_pair((int)opts.device().index(), stream())];
+  if (!t || t->numel() < numel) {
+    delete t;
+    t = new torch::Tensor(torch::empty({numel}, opts.dtype(torch::kFloat32)));
+  }
+  return t->data_ptr<float>();
+}
 
 // C = A . B^T with the given operand layouts; see csrc/gemm.hip for the epilogue contract.
 void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torch::Tensor C, int64_t M, int64_t N, int64_t K,
@@ -216,7 +238,6 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
   p.k_split_len = k_split > 0 ? (int)(((k_split + 63) / 64) * 64) : (int)(((K + 63) / 64) * 64);
   p.epi = (int)epi;
   p.tile_cfg = (int)tile_cfg;
-  p.skew_cycles = g_gemm_skew;
   // tail_limit: -1 = no split tail, 0 = unlimited, n > 0 = at most n workgroups in the split round
   if (epi <= 2 && p.k_split_len >= K && tail_limit >= 0) {
     attach_tail(p, C);
@@ -322,7 +343,9 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
   check(pvr_layernorm_bwd(bf(dy, "dy"), dy_stride, bf(x, "x"), x_stride, f32(mean, "mean"), f32(rstd, "rstd"), f32(w, "w"),
                           opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
                           opt_ptr<float>(db), opt_ptr<float>(dsum), dzp, ldz, d.seed, (uint64_t)seed_offset, d.thr, d.scale,
-                          dz_nostore ? 1 : 0, qp, ldq, qs, qa, (int)rows, (int)D, stream()),
+                          dz_nostore ? 1 : 0, qp, ldq, qs, qa, (int)rows, (int)D,
+                          g_deterministic && (opt_ptr<float>(dw) || opt_ptr<float>(db) || opt_ptr<float>(dsum)) ? det_scratch((int64_t)pvr_layernorm_bwd_blocks((int)rows, (int)D) * 3 * D, x.options()) : nullptr,
+                          stream()),
         "layernorm_bwd");
 }
 
@@ -414,7 +437,8 @@ void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tens
     qa = reinterpret_cast<unsigned*>(q_amax->data_ptr());
   }
   check(pvr_colsum(bf(dy, "dy"), ld_of(dy, "dy"), (int)rows, (int)N, opt_ptr<float>(db), dzp, ldz, d.seed, (uint64_t)seed_offset,
-                   d.thr, d.scale, qp, ldq, qs, qa, stream()),
+                   d.thr, d.scale, qp, ldq, qs, qa,
+                   g_deterministic && opt_ptr<float>(db) ? det_scratch((int64_t)pvr_colsum_part_rows((int)rows) * N, dy.options()) : nullptr, stream()),
         "colsum");
 }
 
@@ -454,7 +478,7 @@ void patch_bwd(torch::Tensor dE, int64_t B, int64_t ntok, int64_t D, c10::option
     scale = (float)(65536.0 / (65536.0 - thr));
   }
   TORCH_CHECK(dE.numel() == B * ntok * D, "patch_bwd: dE must hold B * ntok * D elements");
-  auto ws = torch::empty({(int64_t)pvr_patch_bwd_groups((int)B) * ntok * D}, dE.options().dtype(torch::kFloat32));
+  auto ws = torch::empty({pvr_patch_bwd_ws_floats((int)B, (int)ntok, (int)D)}, dE.options().dtype(torch::kFloat32));
   check(pvr_patch_bwd(bf(dE, "dE"), (int)B, (int)ntok, (int)D, ws.data_ptr<float>(), opt_ptr<float>(dpos), opt_ptr<float>(dcls), opt_ptr<uint16_t>(dconv),
                       opt_ptr<float>(dbias), sp, (uint64_t)seed_offset, thr, scale, stream()),
         "patch_bwd");
@@ -582,7 +606,8 @@ torch::Tensor head_bwd(torch::Tensor dlogits, torch::Tensor xhat, torch::Tensor 
   auto dtok = torch::empty({B * N, D}, xhat.options().dtype(torch::kBFloat16));
   check(pvr_head_bwd(f32(dlogits, "dlogits"), f32(xhat, "xhat"), f32(rstd, "rstd"), f32(gamma, "gamma"), f32(beta, "beta"), f32(W, "W"),
                      (int)B, (int)C, (int)D, (int)N, pdw, opt_ptr<float>(db), opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
-                     dy.data_ptr<float>(), reinterpret_cast<uint16_t*>(dtok.data_ptr()), stream()),
+                     dy.data_ptr<float>(), reinterpret_cast<uint16_t*>(dtok.data_ptr()),
+                     g_deterministic && (opt_ptr<float>(dgamma) || opt_ptr<float>(dbeta)) ? det_scratch(((B + 15) / 16) * 2 * D, xhat.options()) : nullptr, stream()),
         "head_bwd");
   return dtok;
 }
@@ -895,6 +920,18 @@ torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts, bool
   return *t;
 }
 
+// Scratch of the generic attention backward, one per (device, stream), grown to the largest request
+// (never freed: see dq_workspace). Calls on one stream are serialised, so they share it.
+torch::Tensor attn_scratch(int64_t numel, const torch::TensorOptions& opts) {
+  static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
+  torch::Tensor*& t = cache[std::make_pair((int)opts.device().index(), stream())];
+  if (!t || t->numel() < numel) {
+    delete t;
+    t = new torch::Tensor(torch::empty({numel}, opts.dtype(torch::kFloat32)));
+  }
+  return *t;
+}
+
 // R > 0: for the standard layouts of this shape (qkv [T][3D], dO / O [T][D]) the backward emits the
 // in_proj bias gradient as f32 [B*H][R][192] partials (pipelined or chunked kernel); 0: it does not
 int64_t attn_bwd_bias_rows(int64_t B, int64_t N, int64_t H, int64_t D, bool drop) {
@@ -971,9 +1008,10 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   }
   float* dbias_arg = pipe && dbias_part.defined() ? dbias_part.data_ptr<float>() : old_db ? old_part.data_ptr<float>() : nullptr;
   float* bpart_arg = !pipe && dbias_part.defined() ? dbias_part.data_ptr<float>() : nullptr;
-  // pre-pass outputs of the generic backward (per-query delta, lastkey path: ds_last; slab path: dQ slabs)
-  auto ws = torch::empty({pvr_attn_bwd_ws_floats((int)B, (int)N, (int)H, (int)D, old_db, has_drop)},
-                          qkv.options().dtype(torch::kFloat32));
+  // pre-pass outputs of the generic backward (per-query delta, lastkey path: ds_last; slab path: dQ
+  // slabs): a persistent per-(device, stream) scratch, so the slab path (~0.9 GB per ViT-L/16@384
+  // b128 layer) is not allocated on every backward
+  auto ws = attn_scratch(pvr_attn_bwd_ws_floats((int)B, (int)N, (int)H, (int)D, old_db, has_drop), qkv.options());
   const hipError_t err = pvr_attn_bwd(bf(qkv, "qkv"), lds[0], bf(out, "out"), lds[2], bf(dout, "dout"), lds[1], f32(lse, "lse"),
                                       bf_mut(dqkv, "dqkv"), lds[3], dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
                                       dbias_arg, bpart_arg, ws.data_ptr<float>(), (int)B, (int)N, (int)H, (int)D, (float)scale,
@@ -1007,11 +1045,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
     "K-parts of the split tail round this GEMM shape gets (0: none)");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
-  m.def("set_fp8_persistent", &pvr_set_fp8_persistent, "fp8 fwd/dgrad GEMMs on the persistent ping-pong: 0 never, 1 no per-row inputs (default), 2 also residual (A/B)");
-  m.def("set_attn_fwd_direct", &pvr_set_attn_fwd_direct, "attention forward: O stores straight from registers (1) or through LDS (0, default; A/B)");
-  m.def("set_attn_bwd_slab", &pvr_set_attn_bwd_slab, "multi-block attention backward: dQ through f32 slabs (1, default) or f32 atomics (0; A/B)");
-  m.def("set_gemm_tail_min_kt", &set_gemm_tail_min_kt, "fewest K-tiles per split-tail part (default 12; A/B)");
-  m.def("set_gemm_skew", &set_gemm_skew, "A/B: first-round workgroup start skew in shader cycles (0 = off)");
+  m.def("set_fp8_persistent", &pvr_set_fp8_persistent, "fp8 fwd/dgrad GEMMs on the persistent ping-pong: 1 when the epilogue has no per-row input (default), 0 never (A/B)");
+  m.def("set_deterministic", &set_deterministic, "deterministic reductions (partial rows + ordered sum) instead of float atomics");
+  m.def("deterministic", &deterministic);
   m.def("set_gemm_tail", &set_gemm_tail, "split-K tail of the last dispatch round on (True, default) / off (A/B)");
   m.def("gemm", &gemm,py::arg("A"), py::arg("a_kcontig"), py::arg("B"), py::arg("b_kcontig"), py::arg("C"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epi"), py::arg("bias"), py::arg("resid"), py::arg("addend"),

@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
                                                       float* __restrict__ db, uint16_t* __restrict__ dz, int64_t ld_dz,
                                                       const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
                                                       uint8_t* __restrict__ qout, int64_t ld_q, const float* __restrict__ qscale,
-                                                      unsigned* __restrict__ amax) {
+                                                      unsigned* __restrict__ amax, float* __restrict__ part) {
   __shared__ float red[4][64 * 8];
   const float qs = Q8 ? *qscale : 1.f;
   float qam = 0.f;
@@ -93,7 +93,10 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * 8; i += 256) {
     const int col = blockIdx.x * 64 * 8 + i;
-    if (col < N && db) atomicAdd(db + col, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+    if (col < N && part)  // deterministic mode: this row group's partial (rows_reduce sums them in order)
+      part[(int64_t)blockIdx.y * N + col] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    else if (col < N && db)
+      atomicAdd(db + col, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
   }
   if constexpr (Q8) {  // one amax atomic per workgroup
     qam = wave_max_nan(qam);
@@ -173,7 +176,8 @@ __global__ void __launch_bounds__(256) cls_rows_kernel(const float* __restrict__
 //          8 independent 16-B loads in flight per thread; writes the masked gradient (dconv) and
 //          the group's per-(token, column) sums to ws[group][ntok][D] with plain stores;
 //  pass 2: thread = (8-column chunk, token) sums the groups, owns dpos[n] (and dcls for n = 0), and
-//          the block reduces its tokens' dbias partials in LDS before one atomic per column.
+//          the block reduces its tokens' dbias partials in LDS into one partial row per token block;
+//  pass 3: the conv-bias gradient sums those rows in block order (deterministic, no atomics).
 constexpr int PB_BAT = 32, PB_UNROLL = 8;
 __global__ void __launch_bounds__(256) patch_bwd_kernel(const uint16_t* __restrict__ dE, int B, int ntok, int D,
                                                          float* __restrict__ ws, uint16_t* __restrict__ dconv,
@@ -229,7 +233,7 @@ __global__ void __launch_bounds__(256) patch_bwd_kernel(const uint16_t* __restri
 constexpr int PR_CH = 32, PR_TOK = 8;  // pass-2 block: 32 column chunks x 8 tokens
 __global__ void __launch_bounds__(256) patch_bwd_reduce_kernel(const float* __restrict__ ws, int G, int ntok, int D,
                                                                 float* __restrict__ dpos, float* __restrict__ dcls,
-                                                                float* __restrict__ dbias) {
+                                                                float* __restrict__ dbias_part) {
   __shared__ float red[PR_TOK][PR_CH * 8];
   const int nch = D >> 3;
   const int cl = threadIdx.x % PR_CH, tl = threadIdx.x / PR_CH;
@@ -272,14 +276,44 @@ __global__ void __launch_bounds__(256) patch_bwd_reduce_kernel(const float* __re
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[tl][cl * 8 + j] = (ok && n > 0) ? t[j] : 0.f;
   __syncthreads();
-  if (dbias) {
+  if (dbias_part) {  // this token block's partial column sums (summed in block order below: deterministic)
     const int col = blockIdx.x * PR_CH * 8 + threadIdx.x;  // 256 columns per block, one per thread
     if (col < D) {
       float a = 0.f;
 #pragma unroll
       for (int k = 0; k < PR_TOK; ++k) a += red[k][threadIdx.x];
-      atomicAdd(dbias + col, a);
+      dbias_part[(int64_t)blockIdx.y * D + col] = a;
     }
+  }
+}
+
+// Deterministic column reduction of partial rows: dst[c] += sum_r part[r][c] in row order, the C
+// columns split into segments of `seg` going to d0 / d1 / d2 (null: dropped). Block = 8 row lanes x
+// 32 columns; lane rl sums rows rl, rl + 8, ... and the 8 lane sums are added in lane order: the same
+// bits on every run (the float-atomic reductions it replaces are order-dependent).
+__global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restrict__ part, int R, int C, int seg,
+                                                           float* __restrict__ d0, float* __restrict__ d1, float* __restrict__ d2) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float a = 0.f;
+  if (c < C) {
+    int r = rl;
+    for (; r + 24 < R; r += 32) {  // four independent loads in flight
+      const float x0 = part[(int64_t)r * C + c], x1 = part[(int64_t)(r + 8) * C + c];
+      const float x2 = part[(int64_t)(r + 16) * C + c], x3 = part[(int64_t)(r + 24) * C + c];
+      a += x0; a += x1; a += x2; a += x3;
+    }
+    for (; r < R; r += 8) a += part[(int64_t)r * C + c];
+  }
+  red[rl][cl] = a;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    float t = red[0][cl];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][cl];
+    float* d = c < seg ? d0 : (c < 2 * seg ? d1 : d2);
+    if (d) d[c % seg] += t;
   }
 }
 
@@ -427,19 +461,28 @@ extern "C" hipError_t pvr_cast_f32_bf16(const float* in, uint16_t* out, int64_t 
   return hipGetLastError();
 }
 
+// row groups of the column-sum kernel's grid (= the partial rows of its deterministic mode)
+extern "C" int pvr_colsum_part_rows(int rows) {
+  const int gy = (rows + 63) / 64;
+  return gy > 256 ? 256 : gy;
+}
+extern "C" hipError_t pvr_rows_reduce(const float* part, int R, int C, int seg, float* d0, float* d1, float* d2, hipStream_t s);
+
 extern "C" hipError_t pvr_colsum(const uint16_t* dy, int64_t ld, int rows, int N, float* db, uint16_t* dz, int64_t ld_dz,
                                  const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale, uint8_t* q, int64_t ld_q,
-                                 const float* qscale, unsigned* amax, hipStream_t s) {
+                                 const float* qscale, unsigned* amax, float* part, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (N % 8 != 0) return hipErrorInvalidValue;
   if (q && (!qscale || !amax || ld_q % 8 != 0 || reinterpret_cast<uintptr_t>(q) % 8 != 0)) return hipErrorInvalidValue;
   const int gx = (N / 8 + 63) / 64;
-  int gy = (rows + 63) / 64;
-  if (gy > 256) gy = 256;
+  const int gy = pvr_colsum_part_rows(rows);
+  if (!db) part = nullptr;
   hipLaunchKernelGGL(q ? colsum_kernel<true> : colsum_kernel<false>, dim3(gx, gy), dim3(256), 0, s, dy, ld, rows, N, db, dz, ld_dz,
-                     seed_ptr, seed_off, thr, scale, q, ld_q, qscale, amax);
-  return hipGetLastError();
+                     seed_ptr, seed_off, thr, scale, q, ld_q, qscale, amax, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !part) return e;
+  return pvr_rows_reduce(part, gy, N, N, db, nullptr, nullptr, s);
 }
 
 extern "C" hipError_t pvr_im2col(const float* img, uint16_t* out, int B, int C, int H, int W, int P, int Kp, hipStream_t s) {
@@ -474,12 +517,30 @@ extern "C" hipError_t pvr_patch_bwd(const uint16_t* dE, int B, int ntok, int D, 
                      seed_ptr, seed_off, thr, scale);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(patch_bwd_reduce_kernel, dim3((D / 8 + PR_CH - 1) / PR_CH, (ntok + PR_TOK - 1) / PR_TOK), dim3(256), 0, s,
-                     ws, G, ntok, D, dpos, dcls, dbias);
+  // ws also holds the conv-bias partials of the reduction's token blocks, after the group sums
+  const int RB = (ntok + PR_TOK - 1) / PR_TOK;
+  float* part = dbias ? ws + (int64_t)G * ntok * D : nullptr;
+  hipLaunchKernelGGL(patch_bwd_reduce_kernel, dim3((D / 8 + PR_CH - 1) / PR_CH, RB), dim3(256), 0, s,
+                     ws, G, ntok, D, dpos, dcls, part);
+  e = hipGetLastError();
+  if (e != hipSuccess || !dbias) return e;
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3((D + 31) / 32), dim3(256), 0, s, part, RB, D, D, dbias, (float*)nullptr, (float*)nullptr);
   return hipGetLastError();
 }
 
 extern "C" int pvr_patch_bwd_groups(int B) { return (B + pvr::PB_BAT - 1) / pvr::PB_BAT; }
+
+// d0/d1/d2[c % seg] += sum over the R rows of part[R][C] (row order: deterministic)
+extern "C" hipError_t pvr_rows_reduce(const float* part, int R, int C, int seg, float* d0, float* d1, float* d2, hipStream_t s) {
+  if (R <= 0 || C <= 0) return hipSuccess;
+  if (seg <= 0 || C > 3 * seg) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pvr::rows_reduce_kernel, dim3((C + 31) / 32), dim3(256), 0, s, part, R, C, seg, d0, d1, d2);
+  return hipGetLastError();
+}
+// floats of the scratch pvr_patch_bwd needs: the group sums and the conv-bias partials
+extern "C" int64_t pvr_patch_bwd_ws_floats(int B, int ntok, int D) {
+  return ((int64_t)pvr_patch_bwd_groups(B) * ntok + (ntok + pvr::PR_TOK - 1) / pvr::PR_TOK) * D;
+}
 
 // Second half of the small-M split-K forward GEMM (few output tiles: serving-size batches): sum the
 // S fp32 partial products ws[s][m][n] in a fixed order (deterministic) and apply the forward

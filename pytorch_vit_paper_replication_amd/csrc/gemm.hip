@@ -35,14 +35,6 @@ enum GemmEpi : int {
 
 namespace {
 
-PVR_DEV void start_skew(const GemmParams& p, int b) {
-  if (p.skew_cycles > 0 && b < 256) {
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    const uint64_t w = (uint64_t)p.skew_cycles * (uint64_t)(b & 3);
-    while (__builtin_amdgcn_s_memtime() - t0 < w) __builtin_amdgcn_s_sleep(4);
-  }
-}
-
 PVR_DEV void stamp(const GemmParams& p, int slot) {
   if (p.dbg && threadIdx.x == 0) {
     const int b = blockIdx.x + gridDim.x * blockIdx.z;
@@ -961,11 +953,13 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   for (int jp = 0; jp < 2; ++jp)
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[jp][e] = 0.f;
-  // every row input (residual / dGELU factor) of the wave's 128 rows is requested up front (64
-  // VGPRs, free now that the main loop's fragments are dead): the loads' latency overlaps instead
-  // of being paid per fragment row. Row offsets go into the VGPR offset: the SGPR offset of a
-  // buffer access is outside its range check, so rows past M would be accessed.
+  // the row inputs (residual / dGELU factor) of the wave's 128 rows go through a ring of RING fragment
+  // rows (8 VGPRs each), each requested RING rows ahead of its use: the loads' latency overlaps the
+  // rows before it without holding all 64 VGPRs at once (which spilled to scratch next to the 128
+  // accumulators). Row offsets go into the VGPR offset: the SGPR offset of a buffer access is outside
+  // its range check, so rows past M would be accessed.
   constexpr bool HAS_IN = (EPI == EPI_BF16 && RES) || EPI == EPI_DGELU;
+  constexpr int RING = 4;
   // fp8 copy of the GELU / dGELU output (fp8 GEMMs only): 8 bytes per lane and fragment row
   constexpr bool QOK = SCALED && (EPI == EPI_GELU || EPI == EPI_DGELU);
   const bool qon = QOK && p.q_out != nullptr;
@@ -973,13 +967,13 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
                                                qon && rows ? (uint32_t)((int64_t)(rows - 1) * p.ld_q + p.N) : 0u);
   const float qsc = qon ? *p.q_scale : 1.f;
   float qam = 0.f;
-  v4u xin_all[HAS_IN ? 8 : 1][2];
+  v4u xring[HAS_IN ? RING : 1][2];
   if constexpr (HAS_IN) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < RING; ++i)
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp)
-        xin_all[i][jp] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vx[jp] + (uint32_t)(i * 16 * (int)ldx * 2), 0, 0);
+        xring[i][jp] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vx[jp] + (uint32_t)(i * 16 * (int)ldx * 2), 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -988,7 +982,11 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
 #pragma unroll
     for (int jp = 0; jp < 2; ++jp) {
       v4u xin = {0u, 0u, 0u, 0u};
-      if constexpr (HAS_IN) xin = xin_all[i][jp];
+      if constexpr (HAS_IN) {
+        xin = xring[i % RING][jp];
+        if (i + RING < 8)  // refill the slot with the row RING ahead
+          xring[i % RING][jp] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vx[jp] + (uint32_t)((i + RING) * 16 * (int)ldx * 2), 0, 0);
+      }
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1451,7 +1449,6 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   v8s af[4][2], bf[2][2][2];
 
-  if (tpart < 0) start_skew(p, (int)blockIdx.x);
   stamp(p, 0);
   // prologue: half-tiles 0..5 = all of K-tile 0, A0/B0 of K-tile 1
   pp_issue<0, AK, BKC, ES>(ars, brs, nul, smem, p.lda, p.ldb, 0, nk, wave, lane);
@@ -1699,7 +1696,6 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   const int nk = p.K / (128 / ES);  // K-tiles of 128 B (64 bf16 / 128 fp8); >= 2 (host check)
   int v = blockIdx.x;
   if (v >= ntiles) return;
-  start_skew(p, v);
 
   PppTile cur = ppp_tile<ES>(p, v, ntiles, ntn);
   PppTile nxt = ppp_tile<ES>(p, v + gridDim.x, ntiles, ntn);
@@ -1835,10 +1831,11 @@ extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_
   return q.tail_split;
 }
 
-// fp8 forward / dgrad GEMMs on the persistent ping-pong (see pvr_gemm): 0 = never, 1 = without
-// per-row epilogue inputs (default), 2 = also with the residual
+// fp8 forward / dgrad GEMMs on the persistent ping-pong (see pvr_gemm): 1 = when the epilogue has
+// no per-row input (default), 0 = never (A/B of the two production forms; the residual and dGELU
+// epilogues lost on the persistent form and stay one tile per workgroup: profiles/r4/g8b, g8c)
 static int g_fp8_persistent = 1;
-extern "C" void pvr_set_fp8_persistent(int mode) { g_fp8_persistent = mode; }
+extern "C" void pvr_set_fp8_persistent(int mode) { g_fp8_persistent = mode ? 1 : 0; }
 
 // Host entry. Returns hipSuccess, or hipErrorInvalidValue for an unsupported layout/epilogue pair.
 extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
@@ -1866,13 +1863,13 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
     if (p.k_split_len < p.K) return hipErrorInvalidValue;
     // persistent form (tile 13) when there are >= 4 output tiles per CU, the K loop is short
     // (<= 16 K-tiles: the next tile's prologue / this tile's epilogue are a large share of a tile)
-    // and the register-direct epilogue applies; g_fp8_persistent 0 = never (A/B), 1 = epilogues
-    // without per-row inputs, 2 = also the residual epilogue. ViT-H/14 b256 (profiles/r4/g8b):
+    // and the register-direct epilogue applies (epilogues without per-row inputs; g_fp8_persistent
+    // 0 = never, A/B). ViT-H/14 b256 (profiles/r4/g8b):
     // fc1 GELU fwd 0.800 -> 0.688 ms, qkv fwd 0.363 -> 0.357, out dgrad 0.126 -> 0.121; the K = 3840 /
     // 5120 GEMMs lose 3-8 % persistent and stay one tile per workgroup
     const int ntiles8 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
     const bool pers = g_fp8_persistent > 0 && ntiles8 >= 4 * device_cus() && p.K >= 256 && p.K <= 2048 && !p.epi_staged &&
-                      direct_ok(p) && (!p.resid || g_fp8_persistent > 1);
+                      direct_ok(p) && !p.resid;
     switch (p.epi) {
       case EPI_BF16:
         if (pers && f == 0) return launch_ppp<true, EPI_BF16, 1, 0, 0>(p, s);
@@ -1884,9 +1881,7 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
         if (pers && f == 0) return launch_ppp<true, EPI_GELU, 1, 0, 0>(p, s);
         if (f == 0) return launch_pp<true, true, true, EPI_GELU, 1, 0, 0>(p, s);
         break;
-      case EPI_DGELU:  // mode 3 (A/B only): the dGELU dgrad persistent too - its up-front derivative-factor
-                       // loads drain the next tile's DMAs: 0.565 -> 0.632 ms (profiles/r4/g8c)
-        if (pers && g_fp8_persistent > 2 && f == 2) return launch_ppp<true, EPI_DGELU, 1, 1, 0>(p, s);
+      case EPI_DGELU:
         if (f == 2) return launch_pp<true, true, true, EPI_DGELU, 1, 1, 0>(p, s);
         break;
     }

@@ -49,9 +49,6 @@ struct GemmParams {
   int tail_max_units;
   // fewest K-tiles a split part may keep (default 12: measured on the K = 768 bf16 GEMMs)
   int tail_min_kt;
-  // A/B: start-time skew (shader cycles) of the first round of workgroups: workgroup b waits
-  // (b & 3) * skew_cycles before its first tile (desynchronises the CUs' epilogue bursts)
-  int skew_cycles;
 };
 
 }  // namespace pvr

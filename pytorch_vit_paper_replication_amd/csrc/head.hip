@@ -126,13 +126,14 @@ __global__ void __launch_bounds__(256) head_logits_kernel(const float* __restric
 //  tiles [0, nA): dW[c][d] += sum_b dl[b][c] * xc[b][d] (xc = xhat * gamma + beta; each (c, d) owned
 //    by one lane: plain read-modify-write), and for the tiles of the first 16 dims db[c] += sum_b dl[b][c];
 //  tiles [nA, nA + nB): dy[b][d] = sum_c dl[b][c] * W[c][d], plus dgamma[d] += sum_b dy * xhat,
-//    dbeta[d] += sum_b dy over the tile's 16 images (f32 atomics, B / 16 adds per dim).
+//    dbeta[d] += sum_b dy over the tile's 16 images (f32 atomics, B / 16 adds per dim; deterministic
+//    mode: partial rows summed in order by rows_reduce).
 __global__ void __launch_bounds__(256) head_bwd_gemm_kernel(const float* __restrict__ dl, const float* __restrict__ xhat,
                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
                                                              const float* __restrict__ W, int B, int C, int D, int nA, int nB,
                                                              float* __restrict__ dW, float* __restrict__ db,
                                                              float* __restrict__ dy, float* __restrict__ dgamma,
-                                                             float* __restrict__ dbeta) {
+                                                             float* __restrict__ dbeta, float* __restrict__ part) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile = blockIdx.x;
   const int r = lane & 15, kq = (lane >> 4) * 4;
@@ -216,8 +217,13 @@ __global__ void __launch_bounds__(256) head_bwd_gemm_kernel(const float* __restr
   pb += __shfl_xor(pb, 16, 64);
   pb += __shfl_xor(pb, 32, 64);
   if (lane < 16) {
-    if (dgamma) atomicAdd(dgamma + d, pg);
-    if (dbeta) atomicAdd(dbeta + d, pb);
+    if (part) {  // deterministic mode: this image block's partial row [b-block][dgamma | dbeta]
+      part[(int64_t)(b0 / 16) * 2 * D + d] = pg;
+      part[(int64_t)(b0 / 16) * 2 * D + D + d] = pb;
+    } else {
+      if (dgamma) atomicAdd(dgamma + d, pg);
+      if (dbeta) atomicAdd(dbeta + d, pb);
+    }
   }
 }
 
@@ -320,11 +326,14 @@ extern "C" hipError_t pvr_head_fwd(const uint16_t* tok, int64_t ld_tok, int B, i
   return hipGetLastError();
 }
 
+extern "C" hipError_t pvr_rows_reduce(const float* part, int R, int C, int seg, float* d0, float* d1, float* d2, hipStream_t s);
+
 extern "C" hipError_t pvr_head_bwd(const float* dl, const float* xhat, const float* rstd, const float* gamma, const float* beta,
                                    const float* W, int B, int C, int D, int ntok, float* dW, float* db, float* dgamma, float* dbeta,
-                                   float* dy, uint16_t* dtok, hipStream_t s) {
+                                   float* dy, uint16_t* dtok, float* part, hipStream_t s) {
   using namespace pvr;
   if (B <= 0) return hipSuccess;
+  if (!dgamma && !dbeta) part = nullptr;
   if (D % 16 != 0 || C <= 0) return hipErrorInvalidValue;
   const int ntd = D / 16;
   // dW tiles; without dW but with db (classifier weight frozen, bias trainable): one tile per
@@ -332,7 +341,11 @@ extern "C" hipError_t pvr_head_bwd(const float* dl, const float* xhat, const flo
   const int nA = dW ? ((C + 15) / 16) * ntd : db ? (C + 15) / 16 : 0;
   const int nB = ((B + 15) / 16) * ntd;
   hipLaunchKernelGGL(head_bwd_gemm_kernel, dim3(nA + nB), dim3(256), 0, s, dl, xhat, gamma, beta, W, B, C, D, nA, nB, dW, db,
-                     dy, dgamma, dbeta);
+                     dy, dgamma, dbeta, part);
+  if (part) {  // part: f32 [ceil(B / 16)][2 D] (deterministic mode)
+    const hipError_t e = pvr_rows_reduce(part, (B + 15) / 16, 2 * D, D, dgamma, dbeta, nullptr, s);
+    if (e != hipSuccess) return e;
+  }
   const int nrow = (B + 3) / 4;
   const int64_t zero_chunks = (int64_t)B * (ntok - 1) * (D / 8);
   if (zero_chunks >= (1ll << 31)) return hipErrorInvalidValue;

@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       const uint16_t* __restrict__ dres, int64_t dres_stride,
                                                       uint16_t* __restrict__ dx, int64_t dx_stride,
                                                       float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dsum,
+                                                      float* __restrict__ part,
                                                       uint16_t* __restrict__ dz, int64_t dz_stride,
                                                       const uint64_t* __restrict__ seed_ptr, uint64_t seed_off, uint32_t thr,
                                                       float dscale, int dz_nostore, uint8_t* __restrict__ qout, int64_t q_stride,
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
   }
   // block reduction of the dgamma / dbeta / dsum partials, one quantity at a time through a
   // [4][D] LDS buffer (keeps LDS at 4*D*4 bytes so occupancy is register-, not LDS-, bound),
-  // then one atomic per column per block
+  // then one atomic per column per block (deterministic mode: one partial row per block)
   float* outs[3] = {dw, db, dsum};
 #pragma unroll
   for (int qn = 0; qn < 3; ++qn) {
@@ -368,8 +369,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
       }
     }
     __syncthreads();
-    for (int col = threadIdx.x; col < D; col += 256)
-      atomicAdd(outs[qn] + col, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
+    if (part) {  // deterministic mode: the block's partial row [block][quantity][D] (rows_reduce sums them)
+      float* pr = part + ((int64_t)blockIdx.x * 3 + qn) * D;
+      for (int col = threadIdx.x; col < D; col += 256) pr[col] = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+    } else {
+      for (int col = threadIdx.x; col < D; col += 256)
+        atomicAdd(outs[qn] + col, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
+    }
   }
   if constexpr (Q8) {  // max |gradient| of the block's rows: one atomic per workgroup (delayed-scaling amax record)
     qam = wave_max_nan(qam);
@@ -433,12 +439,24 @@ extern "C" hipError_t pvr_layernorm_fwd_q8(const uint16_t* x, int64_t x_stride, 
   return hipGetLastError();
 }
 
+extern "C" hipError_t pvr_rows_reduce(const float* part, int R, int C, int seg, float* d0, float* d1, float* d2, hipStream_t s);
+
+// grid of the LayerNorm backward (= the partial rows [blocks][3][D] of its deterministic mode)
+extern "C" int pvr_layernorm_bwd_blocks(int rows, int D) {
+  const bool use_w4 = (D / 4) % 64 == 0 && (D / 8) % 64 != 0 && D / 4 <= 64 * 5;
+  // D = 768 on 4-column chunks (146 VGPRs, 3 blocks per CU): one grid of exactly the resident blocks,
+  // so no block starts late; otherwise 1024
+  const int cap = use_w4 && D == 768 ? device_cus() * 3 : 1024;
+  const int nblk = (rows + 3) / 4;
+  return nblk > cap ? cap : nblk;
+}
+
 extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, const uint16_t* x, int64_t x_stride,
                                         const float* mean, const float* rstd, const float* w, const uint16_t* dres,
                                         int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
                                         float* dsum, uint16_t* dz, int64_t dz_stride, const uint64_t* seed_ptr,
                                         uint64_t seed_off, uint32_t thr, float dscale, int dz_nostore, uint8_t* q, int64_t q_stride,
-                                        const float* qscale, unsigned* amax, int rows, int D, hipStream_t s) {
+                                        const float* qscale, unsigned* amax, int rows, int D, float* part, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
@@ -448,18 +466,15 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
   // linked dropout backward); forcing 4 waves/SIMD (<= 128 VGPRs) spilled 18 VGPRs and took 114 us.
   // 4-column chunks when they tile the row over the 64 lanes exactly and 8-column ones do not
   const bool use_w4 = (D / 4) % 64 == 0 && (D / 8) % 64 != 0 && D / 4 <= 64 * 5;
-  // D = 768 on 4-column chunks (146 VGPRs, 3 blocks per CU): one grid of exactly the resident blocks,
-  // so no block starts late; otherwise 1024
-  const int cap = use_w4 && D == 768 ? device_cus() * 3 : 1024;
-  int nblk = (rows + 3) / 4;
   // 1024 blocks (4 per CU, ~12 pipelined rows per wave): in-step 0.2 % ahead of 512 and 768
   // (profiles/ln_bwd_grid_step_ab_r2.log); 2048 was 22 % slower in isolation, its 2048 x 3 x D column
   // atomics contending on the same addresses (profiles/kbench_ln_grid.log)
-  if (nblk > cap) nblk = cap;
+  const int nblk = pvr_layernorm_bwd_blocks(rows, D);
+  if (!dw && !db && !dsum) part = nullptr;
   const dim3 grid(nblk), block(256);
 #define PVR_LN_BWD(MC, W)                                                                                                   \
   hipLaunchKernelGGL(q ? (ln_bwd_kernel<MC, W, true>) : (ln_bwd_kernel<MC, W, false>), grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, \
-                     dx_stride, dw, db, dsum, dz, dz_stride, seed_ptr, seed_off, thr, dscale, dz_nostore, q, q_stride, qscale, amax, \
+                     dx_stride, dw, db, dsum, part, dz, dz_stride, seed_ptr, seed_off, thr, dscale, dz_nostore, q, q_stride, qscale, amax, \
                      rows, D)
   if (use_w4) {
     switch (D / 256) {
@@ -476,5 +491,7 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
     }
   }
 #undef PVR_LN_BWD
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !part) return e;
+  return pvr_rows_reduce(part, nblk, 3 * D, D, dw, db, dsum, s);
 }

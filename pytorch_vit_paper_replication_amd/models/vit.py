@@ -330,5 +330,38 @@ class ViT(nn.Module):
         st.wgrad = cfg[3] and cfg[2]
         return st
 
+    # ------------------------------------------------------------------ resume state
+    def runtime_state_dict(self) -> dict:
+        """Fused-path state outside ``state_dict()`` that a bit-exact resume needs (CPU tensors, loads
+        with ``weights_only=True``): the device dropout counter (next seed of the counter-based masks)
+        and the fp8 delayed-scaling state (amax histories, scales, calibration flags)."""
+        out = {}
+        rng = getattr(self, "_pvr_rng", None)
+        if rng is not None:
+            out["dropout_rng"] = rng.detach().cpu().clone()
+        st = getattr(self, "_fp8", None)
+        if st is not None:
+            out["fp8"] = st.state_dict()
+        return out
+
+    def load_runtime_state_dict(self, sd: dict, device=None) -> None:
+        """Restore :meth:`runtime_state_dict` (``device``: where the fused path will run; default the
+        parameters' device). The fp8 state needs ``enable_fp8`` with the same history first."""
+        dev = torch.device(device) if device is not None else next(self.parameters()).device
+        if "dropout_rng" in sd:
+            object.__setattr__(self, "_pvr_rng", sd["dropout_rng"].to(device=dev, dtype=torch.int64).clone())
+        if "fp8" in sd:
+            cfg = getattr(self, "_fp8_cfg", None)
+            if cfg is None:
+                raise RuntimeError("checkpoint holds fp8 scaling state: call enable_fp8(...) before loading it")
+            from ..ops import fp8 as F8
+
+            st = getattr(self, "_fp8", None)
+            if st is None or st.device != dev:
+                st = F8.Fp8State(self.config["num_transformer_layer"], dev, history=cfg[0], margin=cfg[1],
+                                 dgrad=cfg[2], wgrad=cfg[3])
+                object.__setattr__(self, "_fp8", st)
+            st.load_state_dict(sd["fp8"])
+
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())

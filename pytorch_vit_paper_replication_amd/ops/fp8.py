@@ -76,12 +76,28 @@ class Fp8Meta:
         ext = _ext.ext()
         am = self.amax[slot:slot + 1]
         if current or not self.calibrated[slot]:
+            if current:  # current scaling: this tensor's amax alone (the last quantize pass recorded one)
+                am.zero_()
             ext.fp8_quant(x, None, None, am, self.fmt)
             self._update(slot, slot + 1)
             self.calibrated[slot] = True
         y = out if out is not None else torch.empty(x.shape, dtype=torch.uint8, device=x.device)
         ext.fp8_quant(x, y, self.qscale[slot:slot + 1], am, self.fmt)
         return y, self.dscale[slot:slot + 1]
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """Delayed-scaling state (CPU copies): amax histories, the running amax, both scales and the
+        per-slot calibration flags; with it a resumed run quantizes exactly like the original."""
+        return {"hist": self.hist.detach().cpu().clone(), "amax": self.amax.detach().cpu().clone(),
+                "qscale": self.qscale.detach().cpu().clone(), "dscale": self.dscale.detach().cpu().clone(),
+                "calibrated": torch.tensor(self.calibrated, dtype=torch.bool)}
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+        if tuple(sd["hist"].shape) != tuple(self.hist.shape):
+            raise ValueError(f"fp8 state: history shape {tuple(sd['hist'].shape)} != {tuple(self.hist.shape)}")
+        for k in ("hist", "amax", "qscale", "dscale"):
+            getattr(self, k).copy_(sd[k].to(getattr(self, k).device))
+        self.calibrated = [bool(v) for v in sd["calibrated"].tolist()]
 
     def producer(self, slot: int) -> Optional[Tuple["Fp8Meta", int]]:
         """(self, slot) if the slot is calibrated, so the kernel producing the tensor can write its fp8
@@ -110,6 +126,14 @@ class Fp8State:
         self._batch_gen: Optional[int] = None
         self._layout = None
         self.device = device
+
+    def state_dict(self) -> Dict[str, Dict[str, torch.Tensor]]:
+        """Activation / gradient slot state (weights use current scaling: nothing to keep)."""
+        return {"act": self.act.state_dict(), "grad": self.grad.state_dict()}
+
+    def load_state_dict(self, sd) -> None:
+        self.act.load_state_dict(sd["act"])
+        self.grad.load_state_dict(sd["grad"])
 
     def begin_step(self, training: bool) -> None:
         if training:
@@ -198,6 +222,9 @@ class Fp8State:
                 chunk0 += (n + per - 1) // per
             self._batch = (torch.tensor(rows, dtype=torch.int64, device=self.device), chunk0, len(keys))
         segs, nchunks, _ = self._batch
+        # current scaling: each weight's scale from its own amax now (the quantize pass of the previous
+        # generation left its amax recorded, which would make the scale depend on the last two weights)
+        meta.amax.zero_()
         ext.fp8_quant_multi(segs, nchunks, None, meta.amax, E4M3, True)
         meta._update(0, meta.n)
         ext.fp8_quant_multi(segs, nchunks, meta.qscale, meta.amax, E4M3, False)

@@ -53,9 +53,12 @@ class PatchEmbedFn(torch.autograd.Function):
         ext.im2col(img, patches, patch, kp)
         w16 = store.bf16(conv_w).reshape(D, kc)
         if kp != kc:
-            w16p = torch.empty(D, kp, dtype=torch.bfloat16, device=img.device)
-            ext.pad_cols_bf16(w16, w16p)
-            w16 = w16p
+            if kc % 4 == 0:
+                w16p = torch.empty(D, kp, dtype=torch.bfloat16, device=img.device)
+                ext.pad_cols_bf16(w16, w16p)  # 8-B column groups
+                w16 = w16p
+            else:  # odd patch sizes (kc = 3 * P * P odd): plain zero padding
+                w16 = torch.nn.functional.pad(w16, (0, kp - kc))
         tokens = torch.empty(B * ntok, D, dtype=torch.bfloat16, device=img.device)
         drop = site_drop(seed, 0, p_drop, training)
         gemm.linear_fwd(patches, w16, conv_b, addend=pos.reshape(ntok, D), addend_period=ntok,
@@ -86,8 +89,6 @@ class PatchEmbedFn(torch.autograd.Function):
         return (None,) * 10
 
 
-LN_BWD_FP8_COPY = True  # the LayerNorm backward writes dx1 / dz2's e5m2 copies (False: quantize passes, A/B)
-ATTN_BWD_FP8_COPY = True  # the attention backward writes dQKV's e5m2 copy (False: a quantize pass, A/B)
 # test hook: bf16 outputs left unwritten on the fp8 path (only their fp8 copies are consumed) are
 # filled with NaN, so any reader of one would poison the loss / gradients (tests/kernel_checks.py)
 POISON_SKIPPED = False
@@ -102,7 +103,7 @@ def _ln_grad_quant(f8d, which: int, shape, device):
     """Producer-side e5m2 copy of a LayerNorm-backward output for gradient slot ``which`` of the fp8
     block ``f8d = (Fp8State, block)``: (layernorm_bwd kwargs, (copy, dequant scale)) once the slot is
     calibrated, else ({}, None) (the first step calibrates it through the quantize pass)."""
-    if f8d is None or not LN_BWD_FP8_COPY:
+    if f8d is None:
         return {}, None
     prod = f8d[0].grad_producer(f8d[1], which)
     if prod is None:
@@ -312,9 +313,14 @@ class EncoderBlockFn(torch.autograd.Function):
         gw2, gw1 = g(w2), g(w1)
         # dU's bf16 copy is not stored when both of its readers take the e5m2 copy the dGELU epilogue
         # writes: the fc1 dgrad (fp8, W1^T shadow present) and the fc1 weight gradient (fp8, calibrated)
-        du_fp8_only = (f8d is not None and T >= 256 and store.bf16_t(w1) is not None
+        det = _ext.deterministic()
+        du_fp8_only = (f8d is not None and T >= 256 and store.bf16_t(w1) is not None and not det
                        and f8d[0].wgrad_ready(f8d[1], 1, 2) and f8d[0].grad_producer(f8d[1], 1) is not None)
-        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=gb1, skip_out=du_fp8_only)
+        # deterministic mode: d(b1) from the column-sum kernel's ordered partials over dU (the bf16 dU,
+        # as the reference's autocast bias gradient) instead of the epilogue's per-tile float atomics
+        du = dgrad(dz2, w2, 0, dgelu_aux=u, colsum=None if det else gb1, skip_out=du_fp8_only)
+        if det and gb1 is not None:
+            gemm.bias_grad(du, gb1)
 
         def mlp_wgrads():
             if gw2 is not None:
@@ -343,7 +349,7 @@ class EncoderBlockFn(torch.autograd.Function):
         # fp8: dQKV's e5m2 copy (grad slot 3: the qkv dgrad and weight-gradient operand) written by the
         # attention backward's own stores once the slot is calibrated (generic kernels)
         q8kw, q8res = {}, None
-        if fp8_qkv and ATTN_BWD_FP8_COPY:
+        if fp8_qkv:
             prod = f8d[0].grad_producer(f8d[1], 3)
             if prod is not None and ext.attn_bwd_q8_ok(B, N, H, D, aseed is not None):
                 meta, slot = prod

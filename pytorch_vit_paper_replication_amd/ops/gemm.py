@@ -30,10 +30,6 @@ def _n_cus() -> int:
 _N_CUS = None
 # test hook (tests/kernel_checks.py): force one tile config for every GEMM while set
 FORCE_TILE: Optional[int] = None
-# bf16 persistent ping-pong (13) only up to this K (None: any K). A/B knob (bench.py --persistent-max-k):
-# unlike the fp8 kernels, the long-K bf16 GEMMs do not lose on the persistent form (ViT-L/16@384 b128
-# 722 img/s any K vs 719 with K <= 2048, same box: profiles/r4/pmaxk/)
-PERSISTENT_MAX_K: Optional[int] = None
 
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
@@ -58,8 +54,8 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
         # the next tile's first K-tile (qkv fwd 0.171-0.179 vs 0.183-0.185 ms, fc1 GELU fwd 0.347-0.352
         # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log). The dGELU
         # dgrad (column-sum exchange at every tile end) stays on 12: 0.300 vs 0.325 ms (profiles/r3/gemm_ab.log)
-        if (K >= 128 and not dgelu and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus()
-                and (PERSISTENT_MAX_K is None or K <= PERSISTENT_MAX_K)):
+        # (any K: limiting it to K <= 2048 measured no gain, profiles/r4/pmaxk/)
+        if K >= 128 and not dgelu and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
             return 13
         return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
@@ -204,11 +200,15 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.
     K = x.shape[1]
     tile = _tile(N, K, T, "wgrad")
     splits = wgrad_splits(T, N, K, tile)
+    if tile != 12 and splits > 1 and _ext.deterministic():
+        splits = 1  # the atomic path: one token range, so one add per element (deterministic)
     ksplit = math.ceil(math.ceil(T / splits) / 64) * 64
     ext = _ext.ext()
     nsplit = math.ceil(T / ksplit)
     narrow = out.shape[-1] < K
-    if tile == 12 and nsplit > 1 and out.is_contiguous() and N % 4 == 0:
+    # the split-K reduction writes 16-B column groups: a narrow out needs a width % 4 == 0 (odd
+    # patch sizes, kc = 3 * P * P odd, take the temporary below)
+    if tile == 12 and nsplit > 1 and out.is_contiguous() and N % 4 == 0 and out.shape[-1] % 4 == 0:
         ws = _workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
         ext.gemm(dy, False, x, False, ws, N, K, T, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0,
                  None, 0, 0.0, ksplit, 14)

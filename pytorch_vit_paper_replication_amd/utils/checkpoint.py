@@ -7,7 +7,9 @@ here as fp32 CPU tensors with their own storages, so the file loads into the ref
 are views into the fused path's flat store.
 
 New: ``load_model`` and full training-state ``save_checkpoint``/``load_checkpoint`` (model,
-optimizer, scheduler, epoch, RNG, results) for resume — the reference had no load path at all.
+optimizer, scheduler, epoch, RNG, results, and the fused path's runtime state: the device dropout
+counter and the fp8 delayed-scaling histories) for a bit-exact resume — the reference had no load
+path at all (GM/utils.py:7-35 only saves).
 Only rank 0 writes under torch.distributed.
 """
 from __future__ import annotations
@@ -71,6 +73,11 @@ def save_checkpoint(target_dir: str, model: torch.nn.Module, optimizer=None, lr_
         state["optimizer"] = osd
     if lr_scheduler is not None:
         state["lr_scheduler"] = lr_scheduler.state_dict()
+    rt = getattr(_unwrap(model), "runtime_state_dict", None)
+    if rt is not None:
+        # fused-path state outside state_dict(): the device dropout counter and the fp8 scaling
+        # histories; without them a resumed run draws other dropout masks / re-calibrates fp8
+        state["runtime"] = rt()
     tmp = d / (name + ".tmp")
     torch.save(state, tmp)
     os.replace(tmp, d / name)
@@ -90,6 +97,8 @@ def load_checkpoint(path: str, model: torch.nn.Module, optimizer=None, lr_schedu
         optimizer.load_state_dict(state["optimizer"])
     if lr_scheduler is not None and "lr_scheduler" in state:
         lr_scheduler.load_state_dict(state["lr_scheduler"])
+    if "runtime" in state and hasattr(_unwrap(model), "load_runtime_state_dict"):
+        _unwrap(model).load_runtime_state_dict(state["runtime"])
     if restore_rng and "torch_rng" in state:
         torch.set_rng_state(state["torch_rng"])
         if torch.cuda.is_available() and "cuda_rng" in state:

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""In-kernel s_memtime stamps of the one-tile-per-workgroup ping-pong GEMM (tile 12): per-workgroup
+prologue / main-loop / epilogue cycles, at several grid sizes, to tell a bandwidth-bound epilogue
+(epilogue cycles grow with the number of workgroups storing at once) from a latency / issue-bound
+one (flat).
+
+  python scripts/gemm_stamps.py                 # qkv-fwd shape (N 2304, K 768), bias epilogue
+  python scripts/gemm_stamps.py --epi gelu      # fc1 shape with the GELU + aux epilogue
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
+from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epi", default="bias", choices=["bias", "resid", "gelu", "dgelu"])
+    ap.add_argument("--tiles", default="32,64,128,256,512,1024,2304")
+    a = ap.parse_args()
+    ext = _ext.ext()
+    N, K = {"bias": (2304, 768), "resid": (768, 768), "gelu": (3072, 768), "dgelu": (3072, 768)}[a.epi]
+    ntn = N // 256
+    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    seed = torch.tensor([7], dtype=torch.int64, device="cuda")
+    print(f"# epilogue {a.epi}, N {N}, K {K}, tile 12; cycles per workgroup (median over workgroups)", flush=True)
+    for nt in [int(t) for t in a.tiles.split(",")]:
+        M = max(256, (nt // ntn) * 256)
+        tiles = (M // 256) * ntn
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        dbg = torch.zeros(tiles * 4, dtype=torch.int64, device="cuda")
+        args = dict(epi=0, bias=b, resid=None, aux=None, drop=(None, 0, 0.0))
+        if a.epi == "resid":
+            args.update(resid=r)
+        elif a.epi == "gelu":
+            args.update(epi=1, aux=aux, drop=(seed, 3 << 32, 0.1))
+        elif a.epi == "dgelu":
+            args.update(epi=2, bias=None, aux=aux)
+        rows = []
+        for it in range(6):
+            ext.gemm(x, True, w, True, out, M, N, K, args["epi"], args["bias"], args["resid"], None, 0, args["aux"], 0, 0, 0,
+                     args["drop"][0], args["drop"][1], args["drop"][2], 0, 12, dbg=dbg, tail_limit=-1)
+            torch.cuda.synchronize()
+            if it >= 2:
+                d = dbg.view(tiles, 4).cpu().double()
+                rows.append(d)
+        d = torch.stack(rows).median(0).values
+        pro = (d[:, 1] - d[:, 0]).tolist()
+        loop = (d[:, 2] - d[:, 1]).tolist()
+        epi = (d[:, 3] - d[:, 2]).tolist()
+        span = (d[:, 3].max() - d[:, 0].min()).item()
+        print(f"tiles {tiles:5d}: prologue {statistics.median(pro):8.0f} loop {statistics.median(loop):8.0f} "
+              f"epilogue {statistics.median(epi):8.0f} (max {max(epi):8.0f})  span {span:10.0f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

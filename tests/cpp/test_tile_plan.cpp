@@ -24,7 +24,7 @@ static_assert(xcd_remap_c(0, 1) == 0, "trivial grid");
 static_assert(plan_tail_c(591, 48, 256, 256ll * 65536, 256, 0).split == 3, "ViT-B/16 fc2 forward: 3 K-parts");
 static_assert(plan_tail_c(591, 12, 256, 256ll * 65536, 256, 0).split == 0, "K = 768: no split");
 static_assert(plan_tail_c(591, 48, 256, 256ll * 65536, 256, 64).split == 0, "backward limit: 79 tiles x 2 > 64");
-// smallest part (min_kt, the set_gemm_tail_min_kt A/B knob): K = 768 (12 K-tiles) splits in 2 at 6
+// smallest part (min_kt, 12 in production): K = 768 (12 K-tiles) splits in 2 at 6
 static_assert(plan_tail_c(591, 12, 256, 256ll * 65536, 256, 0, 6).split == 2, "K = 768, parts >= 6 K-tiles: 2 parts");
 static_assert(plan_tail_c(5140, 10, 256, 256ll * 65536, 256, 0).split == 0, "ViT-H/14 fc1 fp8 (10 K-tiles): no split by default");
 

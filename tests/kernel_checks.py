@@ -521,27 +521,22 @@ def check_attn_fwd(B, N, H, dh=64):
     return (f"attn_fwd B{B} N{N} H{H} dh{dh}", m, lim(4.5e-3, 6e-3, lse_l2=1.5e-7, lse_max=3e-7))
 
 
-def check_attn_bwd(B, N, H, dh=64, fused_bias=False, slab=True):
-    """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference. slab=False:
-    the multi-block path's dQ through f32 atomics instead of f32 slabs (set_attn_bwd_slab, A/B)."""
+def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
+    """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference."""
     ext = _ext.ext()
     D = H * dh
     qkv = bf(rnd(B * N, 3 * D))
     o, lse = ext.attn_fwd(qkv, B, N, H, 1.0 / math.sqrt(dh))
     do = bf(rnd(B * N, D))
     dbias = torch.zeros(3 * D, device=DEV) if fused_bias else None
-    ext.set_attn_bwd_slab(1 if slab else 0)
-    try:
-        dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
-    finally:
-        ext.set_attn_bwd_slab(1)
+    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, 1.0 / math.sqrt(dh), dbias)
     qr = qkv.float().requires_grad_(True)
     oref, _ = _attn_ref(qr, B, N, H)
     oref.backward(do.float())
     m = worst((dqkv, qr.grad))
     if fused_bias:
         m["dbias_l2"], m["dbias_max"] = errs(dbias, qr.grad.sum(0))
-    return (f"attn_bwd B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}{'' if slab else ' atomics'}", m,
+    return (f"attn_bwd B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}", m,
             lim(5e-3, 1e-2, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
 
 
@@ -690,9 +685,10 @@ def check_gemm_fp8(M, N, K, resid=False, gelu=False):
 
 def check_gemm_fp8_persistent(M=16384, N=4096, K=384):
     """The persistent fp8 ping-pong (tile 13 form, >= 4 output tiles per CU) against the one-tile-per-
-    workgroup kernel (ext.set_fp8_persistent(0)) on the same operands: bias, bias + residual, and
-    the GELU epilogue with dropout, derivative and the e4m3 copy + amax. Same MFMA order and the same
-    epilogue code, so every output must be bit-identical."""
+    workgroup kernel (ext.set_fp8_persistent(0)) on the same operands: bias and the GELU epilogue
+    with dropout, derivative and the e4m3 copy + amax (the residual and dGELU epilogues run one tile
+    per workgroup in both modes). Same MFMA order and the same epilogue code, so every output must be
+    bit-identical."""
     from pytorch_vit_paper_replication_amd.ops import fp8 as F8
 
     ext = _ext.ext()
@@ -714,7 +710,7 @@ def check_gemm_fp8_persistent(M=16384, N=4096, K=384):
             y0 = F8.linear_fwd_fp8(xq, xs, wq, ws, b)
             y1 = F8.linear_fwd_fp8(xq, xs, wq, ws, b, resid=r)
             y2, (q, _) = F8.linear_fwd_fp8(xq, xs, wq, ws, b, gelu_aux=aux, drop=(seed, 5 << 32, 0.1), quant=meta.producer(0))
-            # dGELU dgrad (mode 3): e5m2 gradient x e4m3 W^T rows, derivative factor, column sums, e5m2 copy
+            # dGELU dgrad: e5m2 gradient x e4m3 W^T rows, derivative factor, column sums, e5m2 copy
             m5 = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2)
             m5.calibrated[0] = True
             m5.qscale.fill_(3.0)
@@ -727,7 +723,7 @@ def check_gemm_fp8_persistent(M=16384, N=4096, K=384):
             ext.set_fp8_persistent(1)
 
     gq, gs, _ = _fp8_operand(bf(rnd(M, K, scale=0.01)), 1)
-    (ref, cs0), (got, cs1) = run(0), run(3)
+    (ref, cs0), (got, cs1) = run(0), run(1)
     ndiff = sum(int((a.view(torch.uint8) != c.view(torch.uint8)).sum().item()) if a.dtype != torch.int32 else int((a != c).sum().item())
                 for a, c in zip(ref, got))
     m = {"differing_bytes": float(ndiff), "nonfinite": float(not torch.isfinite(got[2].float()).all().item()),
@@ -1523,8 +1519,6 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd(2, 257, 3, 80),
         lambda: check_attn_bwd(2, 257, 3, 80, True),  # lastkey path + in-kernel bias partials (dh 80)
         lambda: check_attn_bwd(2, 577, 2, 64, True),  # tail split + bias partials from the tail's final dQ pass
-        lambda: check_attn_bwd(2, 577, 2, 64, True, slab=False),  # same with f32-atomic dQ (A/B variant)
-        lambda: check_attn_bwd(2, 577, 3, 80, False, slab=False),
         check_gemm_fp8_persistent,
         lambda: check_attn_bwd_q8(2, 257, 3, 80),    # e5m2 dQKV copy: lastkey path (pre-pass writes key N - 1)
         lambda: check_attn_bwd_q8(2, 577, 2, 64),    # tail split (body dK/dV, tail's final dQ pass)

@@ -36,14 +36,27 @@ def test_headline_config_one_and_eight_gpus():
 
 def test_vit_h14_fp8_eight_gpus():
     d = _desc(["--gpus", "8", "--model", "vit_h14", "--dtype", "fp8"], 8)
-    assert d["per_gpu_batch"] == 512 and d["global_batch"] == 4096 and d["ddp"]
+    assert d["per_gpu_batch"] == 256 and d["global_batch"] == 2048 and d["ddp"]
     assert d["metric"] == "images/sec (whole node) ViT-H/14 224px fp8" and d["seq_len"] == 257
 
 
 def test_vit_l16_384_eight_gpus():
-    d = _desc(["--gpus", "8", "--model", "vit_l16", "--image-size", "384", "--batch", "128"], 8)
-    assert d["seq_len"] == 577 and d["global_batch"] == 1024
+    d = _desc(["--gpus", "8", "--model", "vit_l16", "--image-size", "384"], 8)
+    assert d["seq_len"] == 577 and d["per_gpu_batch"] == 128 and d["global_batch"] == 1024
     assert d["metric"] == "images/sec (whole node) ViT-L/16 384px bf16"
+
+
+def test_per_gpu_defaults_fit_hbm():
+    """Every data-parallel default per-GPU batch fits one MI355X (288 GB) with >= 10 % margin by the
+    fitted peak-memory model; a batch that would not is refused before any allocation."""
+    bench = _bench()
+    for model, size in (("vit_b16", 224), ("vit_l16", 384), ("vit_h14", 224)):
+        b = bench.default_per_gpu_batch(model, 8)
+        assert bench.estimate_peak_gb(model, size, b) < 0.9 * 288, (model, b)
+    assert bench.estimate_peak_gb("vit_h14", 224, 640) > 0.95 * 288  # refused up front
+    assert abs(bench.estimate_peak_gb("vit_b16", 224, 256) - 17.9) < 0.5
+    assert abs(bench.estimate_peak_gb("vit_l16", 384, 128) - 63.8) < 0.5
+    assert abs(bench.estimate_peak_gb("vit_h14", 224, 256) - 134.2) < 0.5
 
 
 def test_world1_forced_ddp_and_inference():

@@ -505,3 +505,128 @@ def test_device_prefetcher_copies_on_side_stream():
     # unpinned host tensors are pinned on the way (copy stays asynchronous)
     dl2 = DataLoader(TensorDataset(xs, ys), batch_size=16, pin_memory=False)
     assert torch.equal(torch.cat([x.cpu() for x, _ in DevicePrefetcher(dl2, "cuda")]), xs)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_resume_is_bit_exact(fp8, tmp_path):
+    """Checkpoint / resume on the fused path: 2 steps, save_checkpoint, a FRESH model + optimizer +
+    scheduler, load_checkpoint, 2 more steps equals 4 uninterrupted steps bit for bit, with dropout
+    on (the device dropout counter is saved) and in fp8 (the delayed-scaling histories are saved).
+    Runs in deterministic mode (ordered reductions instead of float atomics), so that two runs of the
+    same step are themselves bit-identical."""
+    from pytorch_vit_paper_replication_amd import _ext
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
+    from pytorch_vit_paper_replication_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+
+    cfg = dict(CFG, mlp_dropout=0.1, embedding_dropout=0.1)
+    xs = [torch.rand(16, 3, 64, 64, device="cuda") for _ in range(4)]
+    ys = [torch.randint(0, 10, (16,), device="cuda") for _ in range(4)]
+
+    def make(seed):
+        torch.manual_seed(seed)
+        m = ViT(**cfg).cuda()
+        if fp8:
+            m.enable_fp8()
+        o = FusedAdam(param_groups_weight_decay(m, 0.03), lr=1e-3)
+        return m, o, warmup_linear_decay(o, 10, 0.2)
+
+    def run(m, o, s, steps):
+        losses = []
+        for i in steps:
+            m.train()
+            loss = cross_entropy(m(xs[i]), ys[i])
+            o.zero_grad()
+            loss.backward()
+            o.step(clip_norm=1.0)
+            s.step()
+            losses.append(loss.detach().clone())
+        torch.cuda.synchronize()
+        return losses
+
+    with _ext.deterministic_mode():
+        _resume_check(make, run, fp8, tmp_path, save_checkpoint, load_checkpoint)
+
+
+def _resume_check(make, run, fp8, tmp_path, save_checkpoint, load_checkpoint):
+    ma, oa, sa = make(0)
+    torch.manual_seed(123)
+    la = run(ma, oa, sa, range(4))
+
+    mb, ob, sb = make(0)
+    torch.manual_seed(123)
+    lb = run(mb, ob, sb, range(2))
+    path = save_checkpoint(str(tmp_path), mb, ob, sb, epoch=1)
+    del mb, ob, sb
+    mc, oc, sc = make(1)  # different init: everything must come from the checkpoint
+    load_checkpoint(str(path), mc, oc, sc)
+    lb += run(mc, oc, sc, range(2, 4))
+    if fp8:
+        assert mc._fp8 is not None and all(mc._fp8.act.calibrated)
+    for i, (a, b) in enumerate(zip(la, lb)):
+        assert torch.equal(a, b), f"step {i}: loss {a.item()} vs {b.item()}"
+    for (n, p1), p2 in zip(ma.named_parameters(), mc.parameters()):
+        assert torch.equal(p1, p2), n
+    assert torch.equal(oa._fused[1], oc._fused[1]) and torch.equal(oa._fused[2], oc._fused[2])
+
+
+def test_odd_patch_size_fused_matches_reference():
+    """Odd patch size (image 63, P 9: kc = 243 columns, not a multiple of 4): the fused patch
+    embedding pads its weight with a plain zero pad and reduces the weight gradient through a
+    temporary; forward and every gradient match the module-by-module PyTorch path."""
+    from pytorch_vit_paper_replication_amd import _ext
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+
+    torch.manual_seed(0)
+    cfg = dict(CFG, image_size=63, patch_size=9, embedding_dim=256, num_heads=4, mlp_size=512,
+               mlp_dropout=0.0, embedding_dropout=0.0)
+    mf, mr = ViT(**cfg).cuda(), ViT(**cfg).cuda()
+    mr.load_state_dict(mf.state_dict())
+    # 96 x 49 = 4704 patch rows, D = 256, K padded 243 -> 256: the patch weight gradient takes the
+    # split-K ping-pong path, whose 16-B reduction cannot write 243 columns directly
+    x = torch.rand(96, 3, 63, 63, device="cuda")
+    y = torch.randint(0, 10, (96,), device="cuda")
+    assert _ext.use_fused(x) and mf._fused_supported(x)
+    lf = cross_entropy(mf(x), y)
+    lf.backward()
+    os.environ["PVR_DISABLE_FUSED"] = "1"
+    try:
+        lr_ = F.cross_entropy(mr(x).float(), y)
+        lr_.backward()
+    finally:
+        os.environ["PVR_DISABLE_FUSED"] = "0"
+    assert abs(lf.item() - lr_.item()) < 2e-2 * max(1.0, abs(lr_.item()))
+    for (n, pf), pr in zip(mf.named_parameters(), mr.parameters()):
+        g, gr = pf.grad.float(), pr.grad.float()
+        rel = ((g - gr).norm() / gr.norm().clamp_min(1e-12)).item()
+        assert rel < 5e-2, f"{n}: rel-L2 {rel:.3e}"
+
+
+def test_deterministic_mode_gradients_bitwise_repeatable():
+    """Deterministic mode at a size where the default reductions have many partial sums per element
+    (4160 token rows: hundreds of LayerNorm-backward workgroups, 17 GEMM row tiles, 65 patch tokens):
+    two backward passes of the same step give bit-identical gradients for every parameter."""
+    from pytorch_vit_paper_replication_amd import _ext
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+
+    torch.manual_seed(0)
+    m = ViT(**dict(CFG, image_size=128, embedding_dim=256, num_heads=4, mlp_size=1024, mlp_dropout=0.0,
+                   embedding_dropout=0.0)).cuda()
+    x = torch.rand(64, 3, 128, 128, device="cuda")
+    y = torch.randint(0, 10, (64,), device="cuda")
+
+    def grads():
+        m.zero_grad(set_to_none=False)
+        cross_entropy(m(x), y).backward()
+        torch.cuda.synchronize()
+        return [p.grad.detach().clone() for p in m.parameters()]
+
+    with _ext.deterministic_mode():
+        assert _ext.ext().deterministic()
+        g1, g2 = grads(), grads()
+    assert not _ext.ext().deterministic()
+    for (n, _), a, b in zip(m.named_parameters(), g1, g2):
+        assert torch.equal(a, b), n
