@@ -1329,6 +1329,11 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
   const int npr = p1 - p0;
   PairOff prv = cur;
   int sl = 0;  // ring slot of block t (t mod 3)
+  // global stores of a block (dQ of the previous block, its bias partials, a pair's dK / dV) are issued
+  // after the block's DMA group: the next block's wait retires the group but leaves them in flight
+  // (a plain vmcnt(0) there waited for their write acknowledgements, ~1-2 us per block)
+  const int pdb = dbp ? 1 + (wave == 7 ? 1 : 0) : 0;  // bias-partial stores per phase 2
+  int nst = 0;                                          // stores issued in the previous block
   for (int pi = 0; pi < npr; ++pi) {
     cur = pair_off(p0 + pi);
     const bool has_next = pi + 1 < npr;
@@ -1338,9 +1343,19 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
 #pragma unroll 1
     for (int qb = 0; qb < NQ; ++qb) {
       const int t = pi * NQ + qb;
-      // everything issued before (block t+1's DMA group, the previous stores) complete; dS^T of
-      // block t-1 and the table of block t visible; every wave past its reads of the reused buffers
-      wait_barrier_lds<0>();
+      // block t+1's DMA group (issued a block ago) complete, the previous block's stores may still be
+      // in flight; dS^T of block t-1 and the table of block t visible; every wave past its reads of
+      // the reused buffers
+      switch (nst) {  // wave-uniform: the count of stores younger than that group
+        case 1: wait_barrier_lds<1>(); break;
+        case 2: wait_barrier_lds<2>(); break;
+        case 3: wait_barrier_lds<3>(); break;
+        case 17: wait_barrier_lds<17>(); break;
+        case 18: wait_barrier_lds<18>(); break;
+        case 19: wait_barrier_lds<19>(); break;
+        default: wait_barrier_lds<0>(); break;
+      }
+      nst = (qb == 0 && pi > 0 ? 17 + pdb : 0) + (qb != 0 ? 1 + pdb : 0);
       const char* qimg = ring + sl * SLOT;
       const char* doimg = qimg + 4096;
       const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl1 == 2 ? 0 : sl1 + 1;

@@ -38,7 +38,7 @@ namespace {
 PVR_DEV void stamp(const GemmParams& p, int slot) {
   if (p.dbg && threadIdx.x == 0) {
     const int b = blockIdx.x + gridDim.x * blockIdx.z;
-    p.dbg[(int64_t)b * 4 + slot] = __builtin_amdgcn_s_memtime();
+    p.dbg[(int64_t)b * 8 + slot] = __builtin_amdgcn_s_memtime();
   }
 }
 
@@ -977,6 +977,7 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
+    if (i == 1) stamp(p, 4);  // diagnostic builds only (p.dbg): row 0 done (bias / first inputs landed)
     const uint32_t so_c = (uint32_t)(i * 16 * (int)p.ldc * 2), so_x = (uint32_t)(i * 16 * (int)ldx * 2);
     const int m = mb + 16 * i + li;
 #pragma unroll
@@ -1079,6 +1080,7 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
       }
     }
   }
+  stamp(p, 5);  // every row's stores issued
   if constexpr (EPI == EPI_DGELU) {
     {  // without colsum the atomics go to a 0-byte resource: the store count stays fixed
       // column sums over the wave's 128 rows (16 lanes of a row x 8 fragment rows: rows past M

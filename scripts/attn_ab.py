@@ -36,17 +36,14 @@ def timeit(fn, iters=10, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="l16_384,h14,b16")
-    ap.add_argument("--ab", default="", help="'fwd_qg': tiled forward with 2 vs 1 query groups per wave vs 1 with 64-key tiles")
+    ap.add_argument("--ab", default="", help="'fwd_qg': tiled forward with 2 vs 1 query groups per wave")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--bwd", action="store_true", help="also time the backward")
     a = ap.parse_args()
     ext = _ext.ext()
     variants = [("", lambda: None)]
-    if a.ab == "bwd_slab":
-        variants = [("atom", lambda: ext.set_attn_bwd_slab(0)), ("slab", lambda: ext.set_attn_bwd_slab(1))]
     if a.ab == "fwd_qg":
-        variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1)),
-                    ("kt64", lambda: ext.set_attn_fwd_qg(3))]
+        variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1))]
     res = {}
     data = {}
     for name in a.shapes.split(","):
@@ -63,11 +60,8 @@ def main():
                 setv()
                 res.setdefault((name, "fwd", vn), []).append(timeit(lambda: ext.attn_fwd(qkv, B, N, H, dh ** -0.5)))
             if a.bwd:
-                for vn, setv in (order if a.ab == "bwd_slab" else [("", lambda: None)]):
-                    setv()
-                    res.setdefault((name, "bwd", vn), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
+                res.setdefault((name, "bwd", ""), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
     ext.set_attn_fwd_qg(0)
-    ext.set_attn_bwd_slab(1)
     for name in a.shapes.split(","):
         B, N, H, dh = SHAPES[name]
         fl = 4.0 * B * H * N * N * dh

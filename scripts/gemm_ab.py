@@ -62,6 +62,12 @@ def cases(T, D, M, dev):
          lambda: G.linear_fwd(h, w["fc2"], b["fc2"], resid=r, drop=drop(4)), lambda: h @ w["fc2"].t()),
         ("fc2 dgrad dGELU+colsum", 2.0 * T * M * D,
          lambda: G.linear_dgrad(r, w["fc2"], dgelu_aux=u, wt=wt["fc2"], colsum=cs), lambda: r @ w["fc2"]),
+        ("fc2 dgrad dGELU", 2.0 * T * M * D,
+         lambda: G.linear_dgrad(r, w["fc2"], dgelu_aux=u, wt=wt["fc2"]), lambda: r @ w["fc2"]),
+        ("fc1 fwd   bias+GELU+aux", 2.0 * T * M * D,
+         lambda: G.linear_fwd(x, w["fc1"], b["fc1"], gelu_aux=u), lambda: x @ w["fc1"].t()),
+        ("fc1 fwd   bias", 2.0 * T * M * D, lambda: G.linear_fwd(x, w["fc1"], b["fc1"]), lambda: x @ w["fc1"].t()),
+        ("colsum    dU (bias grad pass)", 2.0 * T * M * D, lambda: G.bias_grad(h, cs), lambda: h.sum(0, dtype=torch.float32)),
         ("fc1 dgrad", 2.0 * T * M * D, lambda: G.linear_dgrad(h, w["fc1"], wt=wt["fc1"]), lambda: h @ w["fc1"]),
         ("out dgrad", 2.0 * T * D * D, lambda: G.linear_dgrad(r, w["out"], wt=wt["out"]), lambda: r @ w["out"]),
         ("qkv dgrad", 2.0 * T * 3 * D * D, lambda: G.linear_dgrad(d3, w["qkv"], wt=wt["qkv"]), lambda: d3 @ w["qkv"]),
@@ -88,9 +94,6 @@ def main():
     variants = [("", lambda: None)]
     if a.ab == "tail":
         variants = [("tail on ", lambda: ext.set_gemm_tail(True)), ("tail off", lambda: ext.set_gemm_tail(False))]
-    elif a.ab.startswith("skew:"):
-        # skew:0,6000,12000 - first-round workgroup start skew (shader cycles per step of b & 3)
-        variants = [(f"sk{c:6s}", (lambda c=c: ext.set_gemm_skew(int(c)))) for c in a.ab.split(":", 1)[1].split(",")]
     elif a.ab.startswith("tiles:"):
         # tiles:def,7,8 - the default tile selection vs forced tile configs (every case)
         def force(t):
@@ -111,7 +114,6 @@ def main():
             if rnd % 2 == 0:
                 res.setdefault((name, "lib"), []).append(timeit(lib))
     ext.set_gemm_tail(True)
-    ext.set_gemm_skew(0)
     G.FORCE_TILE = None
     print(f"# {a.model} batch {a.batch} (T = {T}), {a.rounds} rounds; median (min) ms, TFLOP/s at the median", flush=True)
     for name, fl, _, _ in cs:

@@ -16,7 +16,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("PVR_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # PVR_PKG_ROOT: an A/B build
 from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
 from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
 
@@ -40,7 +40,7 @@ def main():
         out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         aux = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
         r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-        dbg = torch.zeros(tiles * 4, dtype=torch.int64, device="cuda")
+        dbg = torch.zeros(tiles * 8, dtype=torch.int64, device="cuda")
         args = dict(epi=0, bias=b, resid=None, aux=None, drop=(None, 0, 0.0))
         if a.epi == "resid":
             args.update(resid=r)
@@ -54,15 +54,18 @@ def main():
                      args["drop"][0], args["drop"][1], args["drop"][2], 0, 12, dbg=dbg, tail_limit=-1)
             torch.cuda.synchronize()
             if it >= 2:
-                d = dbg.view(tiles, 4).cpu().double()
+                d = dbg.view(tiles, 8).cpu().double()
                 rows.append(d)
         d = torch.stack(rows).median(0).values
         pro = (d[:, 1] - d[:, 0]).tolist()
         loop = (d[:, 2] - d[:, 1]).tolist()
         epi = (d[:, 3] - d[:, 2]).tolist()
-        span = (d[:, 3].max() - d[:, 0].min()).item()
-        print(f"tiles {tiles:5d}: prologue {statistics.median(pro):8.0f} loop {statistics.median(loop):8.0f} "
-              f"epilogue {statistics.median(epi):8.0f} (max {max(epi):8.0f})  span {span:10.0f}", flush=True)
+        e_row0 = (d[:, 4] - d[:, 2]).tolist()   # register-direct epilogue: row 0 (bias / inputs landed)
+        e_rows = (d[:, 5] - d[:, 4]).tolist()   # rows 1-7 issued
+        e_tail = (d[:, 3] - d[:, 5]).tolist()   # column sums + store drain
+        med = statistics.median
+        print(f"tiles {tiles:5d}: prologue {med(pro):7.0f} loop {med(loop):7.0f} epilogue {med(epi):7.0f} "
+              f"(max {max(epi):7.0f}) = row0 {med(e_row0):6.0f} + rows1-7 {med(e_rows):6.0f} + tail {med(e_tail):6.0f}", flush=True)
 
 
 if __name__ == "__main__":

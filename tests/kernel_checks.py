@@ -1159,7 +1159,7 @@ def check_fp8_nonfinite_recovery(B=2):
     from pytorch_vit_paper_replication_amd.optim import FusedAdam
 
     torch.manual_seed(0)
-    m = ViT(**_FP8_CFG).to(DEV).enable_fp8(dgrad=True)
+    m = ViT(**_FP8_CFG).to(DEV).enable_fp8(dgrad=True, wgrad=True)
     opt = FusedAdam(m.parameters(), lr=1e-3)
     x = torch.rand(B * 64, 3, 64, 64, device=DEV)
     y = torch.randint(0, 10, (B * 64,), device=DEV)

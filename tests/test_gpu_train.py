@@ -411,7 +411,7 @@ def _gloo_gpu_recipe_worker(rank, world, port, out_dir, cfg, fp8, steps, poison_
     torch.manual_seed(100 + rank)  # different init per rank: the rank-0 broadcast must fix it
     m = ViT(**cfg).to(dev)
     if fp8:
-        m.enable_fp8()
+        m.enable_fp8(wgrad=True)  # every fp8 GEMM kind, the opt-in weight gradients included
     ddp = DistributedDataParallel(m, bucket_cap_mb=0.25)
     opt = FusedAdam(m.parameters(), lr=1e-3)
     g = torch.Generator().manual_seed(11 + rank)  # each rank its own data
@@ -528,7 +528,7 @@ def test_resume_is_bit_exact(fp8, tmp_path):
         torch.manual_seed(seed)
         m = ViT(**cfg).cuda()
         if fp8:
-            m.enable_fp8()
+            m.enable_fp8(wgrad=True)
         o = FusedAdam(param_groups_weight_decay(m, 0.03), lr=1e-3)
         return m, o, warmup_linear_decay(o, 10, 0.2)
 
