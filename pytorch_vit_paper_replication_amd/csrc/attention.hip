@@ -471,6 +471,24 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
   }
 }
 
+// Phase stamps of the backward (diagnostic builds only, -DPVR_ATTN_STAMPS; scripts/attn_stamps.py):
+// per wave, s_memtime cycles summed over the query-block loop by phase, written once at the end
+// (lane 0, vector stores) to g_attn_dbg[(workgroup * NW + wave) * 8 + phase]. Production builds
+// compile every stamp out.
+#ifdef PVR_ATTN_STAMPS
+__device__ uint64_t* g_attn_dbg;
+#define ASTAMP(k)                                          \
+  do {                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
+    st_acc[k] += t_ - st_last;                             \
+    st_last = t_;                                          \
+  } while (0)
+#else
+#define ASTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------------------- backward
 // grid (nkb, B*H), block NW*64 (NW in {1,2,4,8}); workgroup keys [kb*KB, kb*KB + KB), KB = 32*NW.
 // delta = rowsum(dO * O) of each query block is formed in-kernel from the staged dO and O rows
@@ -594,6 +612,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       if (fr < 2 * C::NE) kl_dq[j] = bf2f(base[(int64_t)(N - 1) * ld + D + h * DH + 16 * (fr % C::NE) + li]);
     }
   }
+#ifdef PVR_ATTN_STAMPS
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+  const uint64_t st_0 = st_last;
+#endif
   stage(0);
   float dqb0 = 0.f, dqb1 = 0.f;  // q-bias gradient partials (column sums of this wave's dQ fragments)
   // dQ stores this wave issues per query block (younger than the next block's staging DMAs)
@@ -668,6 +691,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
     // block qb landed (issued one iteration ago, before the dQ stores of block qb - 2, which may
     // stay in flight); every wave is done with slot (qb+1)&1, with dS buffer qb&1 (block qb - 2's)
     // and has written dS buffer (qb-1)&1
+    ASTAMP(7);
     if (qb < 2 || nst < 4)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (nst < 8)
@@ -676,9 +700,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     // a raw barrier: __syncthreads' release fence would drain those stores (vmcnt(0)) first
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ASTAMP(0);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    ASTAMP(1);
     if (qb + 1 < nqb) stage(qb + 1);
+    ASTAMP(2);
     const char* qimg = qdo + (qb & 1) * 2 * QB * RB;
     const char* doimg = qimg + QB * RB;
     const float* s_lse = s_ld + (qb & 1) * 768;
@@ -721,6 +748,17 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
         }
       }
     }
+    // dV / dK operands (transposed dO / Q reads) one head-dim fragment ahead of their MFMAs, the first
+    // under the exp work: -2.3 % L/16-384 backward time vs read-then-wait per fragment
+    // (profiles/r5/attn/readahead_ab.log; with attention dropout the extra registers spill)
+    constexpr bool TR_AHEAD = !DROP;
+    v4s tdlo[2], tdhi[2], tqlo[2], tqhi[2];
+    auto tr_load = [&](int e, int bsel) {
+      frag_tr_async(doimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane, tdlo[bsel], tdhi[bsel]);
+      frag_tr_async(qimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane, tqlo[bsel], tqhi[bsel]);
+    };
+    if constexpr (TR_AHEAD) tr_load(0, 0);
+    ASTAMP(3);
     // P and dS
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -753,13 +791,13 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       pf[f] = pack_p(s[0][f], s[1][f]);
       sf[f] = pack_p(dp[0][f], dp[1][f]);
     }
+    ASTAMP(4);
 #pragma unroll
     for (int e = 0; e < C::NE; ++e) {
-      v4s dlo, dhi, qlo, qhi;
-      frag_tr_async(doimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane, dlo, dhi);
-      frag_tr_async(qimg, QB, 4 * g, 16 + 4 * g, 16 * e, lane, qlo, qhi);
+      if constexpr (!TR_AHEAD) tr_load(e, e & 1);
       lds_wait();
-      const v8s dot = cat44(dlo, dhi), qt = cat44(qlo, qhi);
+      if (TR_AHEAD && e + 1 < C::NE) tr_load(e + 1, (e + 1) & 1);
+      const v8s dot = cat44(tdlo[e & 1], tdhi[e & 1]), qt = cat44(tqlo[e & 1], tqhi[e & 1]);
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         dv[e][f] = mfma16(dot, pf[f], dv[e][f]);
@@ -778,7 +816,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
       }
     }
     }  // active
+    ASTAMP(5);
     if (qb > 0) dq_block(qb - 1, slq_prev);
+    ASTAMP(6);
     slq_prev[0] = slq_cur[0];
     slq_prev[1] = slq_cur[1];
   }
@@ -787,6 +827,14 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   dq_block(nqb - 1, slq_prev);
+#ifdef PVR_ATTN_STAMPS
+  ASTAMP(7);
+  st_acc[7] = __builtin_amdgcn_s_memtime() - st_0;  // whole kernel up to here (slot 7: total, not a phase)
+  if (g_attn_dbg && lane == 0 && dq_mode != 4) {  // (not the tail launch of a split head)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g_attn_dbg[((int64_t)blockIdx.x * NW + wave) * 8 + k] = st_acc[k];
+  }
+#endif
   // bpart (the launch that writes the final dQ): this pair's q-bias partials, the column sums of the
   // wave's dQ fragments over all query blocks -> [bh][a][16e + li] (the pre-pass adds the v sums)
   if (bpart && dq_mode == 0) {  // (mode 4: the final pass below writes them)
@@ -1651,6 +1699,16 @@ static hipError_t attn_fwd_launch(const uint16_t* qkv, int64_t ld, uint16_t* out
     }
   }
   return attn_fwd_tiled_pick<DH, false>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
+}
+
+// diagnostic builds (-DPVR_ATTN_STAMPS): where the backward writes its phase stamps (null: nowhere)
+extern "C" void pvr_set_attn_dbg(void* p) {
+#ifdef PVR_ATTN_STAMPS
+  uint64_t* q = (uint64_t*)p;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pvr::g_attn_dbg), &q, sizeof(q));
+#else
+  (void)p;
+#endif
 }
 
 extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg == 1 || qg == 2 ? qg : 0; }

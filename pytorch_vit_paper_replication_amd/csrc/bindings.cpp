@@ -24,6 +24,7 @@ extern "C" {
 hipError_t pvr_gemm(const pvr::GemmParams* p, hipStream_t s);
 int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
 void pvr_set_attn_fwd_qg(int qg);
+void pvr_set_attn_dbg(void* p);
 void pvr_set_fp8_persistent(int mode);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
@@ -1044,6 +1045,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return pvr_gemm_tail_split((int)M, (int)N, (int)K, (int)elem_bytes, (int)max_units); },
     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("elem_bytes"), py::arg("max_units") = 0,
     "K-parts of the split tail round this GEMM shape gets (0: none)");
+  m.def("set_attn_dbg", [](torch::Tensor t) { pvr_set_attn_dbg(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
+        "diagnostic builds (-DPVR_ATTN_STAMPS): int64 buffer for the attention backward's phase stamps "
+        "[workgroup * waves + wave][8] (scripts/attn_stamps.py); a no-op otherwise");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
   m.def("set_fp8_persistent", &pvr_set_fp8_persistent, "fp8 fwd/dgrad GEMMs on the persistent ping-pong: 1 when the epilogue has no per-row input (default), 0 never (A/B)");
   m.def("set_deterministic", &set_deterministic, "deterministic reductions (partial rows + ordered sum) instead of float atomics");
