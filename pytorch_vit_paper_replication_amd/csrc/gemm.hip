@@ -1386,7 +1386,8 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   // Tile and K range of this workgroup. Plain grid: one whole tile per workgroup (split-K over
   // blockIdx.z for the weight gradients). Split tail (tail_split > 1): workgroups < tail_from own
   // one whole tile each; the rest are K-parts of the tail tiles, the parts of one tile on
-  // consecutive remapped ids (one XCD, so the last part reads the others' partials from its L2).
+  // consecutive remapped ids (usually one XCD; a locality hint only, some tiles straddle two XCDs:
+  // the sc1 partial stores / loads and the agent-scope arrival counter make the hand-off correct).
   int tt, kbeg, kend, tloc = 0, tpart = -1;
   const TailPlan tp{p.tail_from, p.tail_split};
   PVR_ASSERT((int)blockIdx.x < tail_grid(tp, ntm * ntn));

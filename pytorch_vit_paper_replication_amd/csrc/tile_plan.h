@@ -41,8 +41,12 @@ constexpr TailPlan plan_tail_c(int ntiles, int nkt, int cus, long long ws_elems,
 }
 
 // Workgroups of a split-tail launch: ids [0, from) whole tiles, then units * split K-parts. A part's
-// (leftover tile, part) comes from the XCD remap over the units, so consecutive parts of one tile
-// land on one XCD (the last part then reads the others' partials from its own L2).
+// (leftover tile, part) comes from the XCD remap over the units, so the parts of one tile mostly land
+// on one XCD. That is a locality hint only: the XCD ranges (units / 8 ids each) do not align with the
+// tiles' part groups, so some tiles straddle two XCDs (ViT-B/16 fc2: 79 tiles x 3 parts, counted by
+// tests/cpp/test_tile_plan.cpp). The hand-off is correct because the partials are stored and read
+// with sc1 (device-coherent, L2-bypassing) accesses and counted by an agent-scope atomic, not because
+// the parts share an L2.
 constexpr int tail_grid(const TailPlan& t, int ntiles) {
   return t.split > 1 ? t.from + (ntiles - t.from) * t.split : ntiles;
 }

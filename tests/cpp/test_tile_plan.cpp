@@ -80,7 +80,29 @@ static void check_plan(int ntiles, int nkt, int cus, int max_units) {
   }
 }
 
+// Tail tiles whose K-parts run on more than one XCD (hardware dispatch: workgroup b on XCD b % 8).
+// The split-tail hand-off must not rely on a shared L2 (csrc/tile_plan.h): this counts the tiles for
+// which it could not.
+static int straddling_tiles(int ntiles, int nkt, int cus) {
+  const TailPlan p = plan_tail_c(ntiles, nkt, cus, (long long)cus * 65536, cus, 0);
+  if (p.split < 2) return 0;
+  std::vector<int> xcd(ntiles, -1), straddle(ntiles, 0);
+  for (int b = p.from; b < tail_grid(p, ntiles); ++b) {
+    const TailUnit u = tail_unit_c(p, ntiles, b);
+    if (xcd[u.tile] < 0) xcd[u.tile] = b % 8;
+    else if (xcd[u.tile] != b % 8) straddle[u.tile] = 1;
+  }
+  int n = 0;
+  for (int v : straddle) n += v;
+  return n;
+}
+
 int main() {
+  {
+    const int s = straddling_tiles(591, 48, 256);  // ViT-B/16 fc2 forward: 79 tail tiles x 3 parts
+    std::printf("ViT-B/16 fc2 split tail: %d of 79 tail tiles straddle two XCDs\n", s);
+    CHECK(s > 0);  // documented: same-XCD placement is not an invariant
+  }
   for (int n = 1; n <= 5000; n += (n < 300 ? 1 : 37)) check_remap(n);
   const int shapes[][2] = {{591, 48}, {591, 12}, {591, 36}, {2364, 48}, {2364, 12}, {1285, 40}, {1285, 30}, {1773, 12},
                            {588, 48}, {5140, 10}, {257, 48}, {255, 48}, {512, 48}, {1000, 100}};
