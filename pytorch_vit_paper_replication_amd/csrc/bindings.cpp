@@ -26,7 +26,6 @@ int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
 void pvr_set_attn_fwd_qg(int qg);
 void pvr_set_attn_dbg(void* p);
 void pvr_set_fp8_persistent(int mode);
-void pvr_set_gemm_deferred(int on);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
@@ -1050,9 +1049,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "diagnostic builds (-DPVR_ATTN_STAMPS): int64 buffer for the attention backward's phase stamps "
         "[workgroup * waves + wave][8] (scripts/attn_stamps.py); a no-op otherwise");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");
-  m.def("set_gemm_deferred", &pvr_set_gemm_deferred,
-        "GELU GEMMs on the persistent ping-pong: 1 = deferred-epilogue kernel (epilogue units under the next "
-        "half-tile's MFMAs), 0 = one-pass kernel (A/B)");
   m.def("set_fp8_persistent", &pvr_set_fp8_persistent, "fp8 fwd/dgrad GEMMs on the persistent ping-pong: 1 when the epilogue has no per-row input (default), 0 never (A/B)");
   m.def("set_deterministic", &set_deterministic, "deterministic reductions (partial rows + ordered sum) instead of float atomics");
   m.def("deterministic", &deterministic);

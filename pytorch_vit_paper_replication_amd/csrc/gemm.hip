@@ -1793,264 +1793,6 @@ hipError_t launch_ppp(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ===================================================================================== deferred epilogue
-// Persistent ping-pong whose GELU epilogue runs under the next MFMAs instead of after them. The
-// epilogue of the register-direct persistent kernel is VALU-bound (~21 VALU instructions per
-// element: 22.4k cycles per 256x256 tile against a 32.8k-cycle K loop, profiles/r5/stamps_gelu.log)
-// while the MFMA pipe idles, and 128 accumulator registers per lane leave no room to park a tile.
-// Here each 256x256 tile is computed as two row-half passes (wave rows 0-63 / 64-127 of its 128,
-// acc[0..3] / acc[4..7]): pass h of tile t streams all K-tiles for its half (A rows of that half, B
-// in full: the A half-tile kinds 0 / 3 of the ping-pong layout, B kinds 1 and 2) while the other
-// accumulator half holds a finished half-tile whose epilogue is cut into 8 units (one fragment row
-// x one column pair: 8 values per lane, two 16-B stores) run one per K-tile in the second phase,
-// between its DMA issue and its barrier - on every SIMD while the partner wave issues MFMAs:
-//   pass 0 of tile t: MFMAs -> acc[0..3] | units of tile t-1's half 1 (acc[4..7])
-//   pass 1 of tile t: MFMAs -> acc[4..7] | units of tile t's half 0   (acc[0..3])
-// B is streamed twice per tile (1.5x the DMA bytes of the one-pass kernel). Two phases per K-tile:
-// phase 0 reads the A half + B0 fragments and issues the next K-tile's A half + B0 (4 DMA
-// instructions per wave), phase 1 reads B1 and issues the next K-tile's B1 (2): every half-tile is
-// issued two phases after its buffer's last read (group stagger) and read two phases later. The
-// counted waits: phase 0 leaves its own 4 in flight; phase 1 its 2 plus the unit's 2 stores. Bias
-// columns of a tile come into one of two 1 KiB LDS slots (by tile parity) by one LDS-DMA.
-constexpr int PPD_BIAS = 2 * PP_BUF;
-
-// DMA of stream K-tile `s` = K-tile kk of row half qm of tile index tv (descriptors built here from
-// the tile index: holding them across the loop spilled hundreds of SGPRs), group w: 0 = A half + B0
-// (4 instructions per wave), 1 = B1 (2)
-PVR_DEV void ppd_issue(int tv, int ntiles, int ntn, int qm, int w, char* smem, int s, int kk, const GemmParams& p, int wave, int lane) {
-  const PppTile t = ppp_tile<2>(p, tv, ntiles, ntn);
-  char* buf = smem + (s & 1) * PP_BUF;
-  if (w == 0) {
-    ppp_issue_kind<2>(qm ? 3 : 0, t.ars, t.brs, buf, p.lda, p.ldb, kk * 128, wave, lane);
-    ppp_issue_kind<2>(1, t.ars, t.brs, buf, p.lda, p.ldb, kk * 128, wave, lane);
-  } else {
-    ppp_issue_kind<2>(2, t.ars, t.brs, buf, p.lda, p.ldb, kk * 128, wave, lane);
-  }
-}
-
-PVR_DEV int ppd_n0(int tv, int ntiles, int ntn) { return (xcd_remap(tv, ntiles) % ntn) * 256; }
-PVR_DEV int ppd_m0(int tv, int ntiles, int ntn) { return (xcd_remap(tv, ntiles) / ntn) * 256; }
-
-// GELU epilogue unit U (0..7) of accumulator half H of tile index tv: fragment row i = 4H + U / 2,
-// column pair jp = U % 2 (same math and lane layout as epilogue_direct<EPI_GELU>)
-template <int H, int U>
-PVR_DEV void ppd_unit(const GemmParams& p, v4f (&acc)[8][4], const char* smem, int slot, int tv, int ntiles, int ntn, int wm, int wn,
-                      int lane) {
-  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  constexpr int i = 4 * H + (U >> 1), jp = U & 1;
-  const int li = lane & 15, g = lane >> 4;
-  const int cl = wn * 64 + 32 * jp + ((g & 1) << 4) + ((g & 2) << 2);  // first of the lane's 8 columns in the tile
-  const int c0 = ppd_n0(tv, ntiles, ntn) + cl;
-  const int m = ppd_m0(tv, ntiles, ntn) + wm * 128 + 16 * i + li;
-  const bool ok = m < p.M && c0 < p.N;
-  float v[8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float a = acc[i][2 * jp][r], b = acc[i][2 * jp + 1][r];
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    v[r] = a;
-    v[4 + r] = b;
-  }
-  const float* bl = (const float*)(smem + PPD_BIAS + slot * 1024) + cl;
-  const v4f b0 = *(const __attribute__((address_space(3))) v4f*)bl;
-  const v4f b1 = *(const __attribute__((address_space(3))) v4f*)(bl + 4);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    v[q] += b0[q];
-    v[4 + q] += b1[q];
-  }
-  bool keep[8] = {true, true, true, true, true, true, true, true};
-  if (p.drop_thr) {
-    const uint32_t key = rng_key((*p.seed_ptr) + p.seed_offset);  // wave-uniform (scalar)
-    const uint32_t idx = (uint32_t)m * (uint32_t)p.N + (uint32_t)c0;  // host: M * N + 8 <= 2^32
-    bool k0[4], k1[4];
-    rng_keep4_32(key, idx, p.drop_thr, k0);
-    rng_keep4_32(key, idx + 4, p.drop_thr, k1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { keep[q] = k0[q]; keep[4 + q] = k1[q]; }
-  }
-  v4u out, ax;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const v2f s2 = {keep[2 * q] ? p.drop_scale : 0.f, keep[2 * q + 1] ? p.drop_scale : 0.f};
-    v2f g2, d2;
-    gelu_and_grad2((v2f){v[2 * q], v[2 * q + 1]}, g2, d2);
-    g2 *= s2;
-    d2 *= s2;
-    ax[q] = pack2bf(d2.x, d2.y);
-    out[q] = pack2bf(g2.x, g2.y);
-  }
-  const uint32_t OOB = 0x80000000u;
-  const uint32_t oc = ok ? (uint32_t)(((int64_t)m * p.ldc + c0) * 2) : OOB;
-  const uint32_t ox = ok ? (uint32_t)(((int64_t)m * p.ld_aux + c0) * 2) : OOB;
-  const __amdgpu_buffer_rsrc_t crs = make_rsrc(p.C, p.c_skip ? 0u : (uint32_t)((int64_t)p.M * p.ldc * 2));
-  const __amdgpu_buffer_rsrc_t xrs = make_rsrc(p.aux, p.aux ? (uint32_t)((int64_t)p.M * p.ld_aux * 2) : 0u);
-  __builtin_amdgcn_raw_buffer_store_b128(out, crs, oc, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b128(ax, xrs, ox, 0, 0);
-}
-
-template <int H>
-PVR_DEV void ppd_unit_sw(int u, const GemmParams& p, v4f (&acc)[8][4], const char* smem, int slot, int tv, int ntiles, int ntn, int wm,
-                         int wn, int lane) {
-  switch (u) {
-    case 0: ppd_unit<H, 0>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    case 1: ppd_unit<H, 1>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    case 2: ppd_unit<H, 2>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    case 3: ppd_unit<H, 3>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    case 4: ppd_unit<H, 4>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    case 5: ppd_unit<H, 5>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    case 6: ppd_unit<H, 6>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-    default: ppd_unit<H, 7>(p, acc, smem, slot, tv, ntiles, ntn, wm, wn, lane); break;
-  }
-}
-
-// One row-half pass: MFMAs of half QM of tile index tv over its nk K-tiles (stream K-tiles s0 ..), the
-// DMA of the next pass's first K-tile (tile ntv, half nqm) from its last K-tile, and (uv >= 0) the 8
-// epilogue units of the finished half 1 - QM of tile index uv (bias slot uslot); bias_slot >= 0: the
-// tile's bias columns into that LDS slot (wave 0, first K-tile).
-template <int QM>
-PVR_DEV void ppd_pass(v4f (&acc)[8][4], char* smem, int tv, int ntv, int nqm, int ntiles, int ntn, int s0, int nk, int uv, int uslot,
-                      int bias_slot, const GemmParams& p, int wave, int lane, int wm, int wn) {
-#pragma unroll
-  for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[QM * 4 + ii][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  v8s af[4][2], bf[2][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const int s = s0 + kt;
-    const char* buf = smem + (s & 1) * PP_BUF;
-    const bool same = kt + 1 < nk;
-    const int t = same ? tv : ntv;
-    const int tqm = same ? QM : nqm, tk = same ? kt + 1 : 0;
-    // ---- phase 0: A half QM + B0
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bf[jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + 16 * jj, ks, lane);
-    if (bias_slot >= 0 && kt == 0 && wave == 0) {
-      const int n0 = ppd_n0(tv, ntiles, ntn);
-      const __amdgpu_buffer_rsrc_t brs = make_rsrc(p.bias ? p.bias + n0 : p.bias, p.bias ? (uint32_t)(min(256, p.N - n0) * 4) : 0u);
-      dma16(brs, to_lds(smem + PPD_BIAS + bias_slot * 1024), (uint32_t)lane * 16);
-    }
-    ppd_issue(t, ntiles, ntn, tqm, 0, smem, s + 1, tk, p, wave, lane);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    pp_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[QM * 4 + ii][jj] = mfma16(bf[jj][ks], af[ii][ks], acc[QM * 4 + ii][jj]);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    // ---- phase 1: B1, one epilogue unit
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bf[jj][ks] = read_frag<256, true>(buf + 256 * 128, wn * 64 + 32 + 16 * jj, ks, lane);
-    // the unit's 2 stores go out before this phase's DMA group: the next phase's wait (for that group's
-    // predecessor) then leaves them in flight, and only the wait one K-tile later retires them
-    const bool unit = uv >= 0 && kt < 8;
-    if (unit) ppd_unit_sw<1 - QM>(kt, p, acc, smem, uslot, uv, ntiles, ntn, wm, wn, lane);
-    ppd_issue(t, ntiles, ntn, tqm, 1, smem, s + 1, tk, p, wave, lane);
-    if (unit)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the unit's 2 stores + this phase's 2 DMAs in flight
-    else
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    pp_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[QM * 4 + ii][2 + jj] = mfma16(bf[jj][ks], af[ii][ks], acc[QM * 4 + ii][2 + jj]);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-  }
-  if (uv >= 0)  // K loops shorter than 8 K-tiles: the remaining units after the loop (younger stores only)
-    for (int u = nk; u < 8; ++u) ppd_unit_sw<1 - QM>(u, p, acc, smem, uslot, uv, ntiles, ntn, wm, wn, lane);
-}
-
-template <int EPI, bool UNITS = true>
-__global__ void __launch_bounds__(512, 2) gemm_ppd_kernel(GemmParams p) {
-  static_assert(EPI == EPI_GELU, "deferred epilogue: GELU");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int ntm = (p.M + 255) / 256, ntn = (p.N + 255) / 256, ntiles = ntm * ntn;
-  const int nk = p.K / 64;  // >= 2 (host check)
-  int v = blockIdx.x;
-  if (v >= ntiles) return;
-  const int G = gridDim.x;
-  // prologue: bias of the first tile (slot 0), stream K-tile 0 (half 0 of the first tile)
-  if (wave == 0) {
-    const int n0 = ppd_n0(v, ntiles, ntn);
-    const __amdgpu_buffer_rsrc_t brs = make_rsrc(p.bias ? p.bias + n0 : p.bias, p.bias ? (uint32_t)(min(256, p.N - n0) * 4) : 0u);
-    dma16(brs, to_lds(smem + PPD_BIAS), (uint32_t)lane * 16);
-  }
-  ppd_issue(v, ntiles, ntn, 0, 0, smem, 0, 0, p, wave, lane);
-  ppd_issue(v, ntiles, ntn, 0, 1, smem, 0, 0, p, wave, lane);
-  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  pp_barrier();
-  if (wm == 1) pp_barrier();  // group 1 runs one barrier behind for the whole kernel
-
-  v4f acc[8][4];
-#pragma unroll
-  for (int i = 4; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-  int s0 = 0, slot = 0, pv = -1;
-  for (;;) {
-    // pass 0: half 0 of tile v | units of the previous tile's half 1 (that tile's bias slot)
-    ppd_pass<0>(acc, smem, v, v, 1, ntiles, ntn, s0, nk, UNITS ? pv : -1, slot ^ 1, pv >= 0 ? slot : -1, p, wave, lane, wm, wn);
-    s0 += nk;
-    // pass 1: half 1 of tile v | units of its half 0; the last K-tile issues the next tile's first
-    ppd_pass<1>(acc, smem, v, v + G, 0, ntiles, ntn, s0, nk, UNITS ? v : -1, slot, -1, p, wave, lane, wm, wn);
-    s0 += nk;
-    pv = v;
-    v += G;
-    if (v >= ntiles) break;
-    slot ^= 1;
-  }
-  if (wm == 0) pp_barrier();  // re-align the groups
-  // the last tile's half 1: its units after the stream (the trailing DMAs read out of range)
-#pragma unroll
-  for (int u = 0; u < 8; ++u) ppd_unit_sw<1>(u, p, acc, smem, slot, pv, ntiles, ntn, wm, wn, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-}
-
-// deferred-epilogue GELU GEMM (A/B switch; see gemm_ppd_kernel): 1 = fc1-style GELU GEMMs on tile 13
-// take it, 0 = the one-pass persistent kernel
-static int g_gemm_deferred = 0;
-
-template <int EPI>
-hipError_t launch_ppd(const GemmParams& p, hipStream_t s) {
-  constexpr int SMEM = 2 * PP_BUF + 2048;
-  // g_gemm_deferred == 2: timing-only build of the stream without the epilogue units (diagnostic)
-  auto kern = g_gemm_deferred == 2 ? gemm_ppd_kernel<EPI, false> : gemm_ppd_kernel<EPI, true>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_ppd_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)gemm_ppd_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int ntiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  const int cus = device_cus();
-  const int grid = ntiles < cus ? ntiles : cus;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), SMEM, s, p);
-  return hipGetLastError();
-}
-
 // Tile configs (ops/gemm.py `_tile`): 0 = 128x128 (small GEMMs), 6 = 256x256 BK-32 ring (K % 64 != 0),
 // 12 = 256x256 8-wave ping-pong (one tile per workgroup, split-K tail), 13 = its persistent form.
 template <bool AK, bool BKC, bool SWAP, int EPI>
@@ -2059,13 +1801,8 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     case 6: return launch_v3<256, 256, 2, 4, 4, 2, AK, BKC, SWAP, EPI>(p, s);
     case 13:  // persistent ping-pong (k-contiguous bf16, bf16-output epilogues, no split-K)
       if constexpr (AK && BKC && SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
-        if (p.K % PP_BK == 0 && p.K >= 2 * PP_BK && p.k_split_len >= p.K && !p.addend && !p.row_group && (p.N & 3) == 0) {
-          if constexpr (EPI == EPI_GELU) {
-            if (g_gemm_deferred && !p.epi_staged && direct_ok(p) && !p.resid && (uint64_t)p.M * (uint64_t)p.N + 8 <= 0xFFFFFFFFull)
-              return launch_ppd<EPI_GELU>(p, s);
-          }
+        if (p.K % PP_BK == 0 && p.K >= 2 * PP_BK && p.k_split_len >= p.K && !p.addend && !p.row_group && (p.N & 3) == 0)
           return launch_ppp<SWAP, EPI>(p, s);
-        }
       }
       [[fallthrough]];
     case 12:
@@ -2102,7 +1839,6 @@ extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_
 // epilogues lost on the persistent form and stay one tile per workgroup: profiles/r4/g8b, g8c)
 static int g_fp8_persistent = 1;
 extern "C" void pvr_set_fp8_persistent(int mode) { g_fp8_persistent = mode ? 1 : 0; }
-extern "C" void pvr_set_gemm_deferred(int on) { pvr::g_gemm_deferred = on == 2 ? 2 : (on ? 1 : 0); }
 
 // Host entry. Returns hipSuccess, or hipErrorInvalidValue for an unsupported layout/epilogue pair.
 extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
