@@ -139,7 +139,7 @@ def main():
         os.environ["PVR_DISABLE_FUSED"] = "1"
     import torch
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.environ.get("PVR_PKG_ROOT") or os.path.dirname(os.path.abspath(__file__)))  # PVR_PKG_ROOT: an A/B build
     from pytorch_vit_paper_replication_amd.models import vit
     from pytorch_vit_paper_replication_amd.optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
     from pytorch_vit_paper_replication_amd.ops.fused_vit import backward, cross_entropy

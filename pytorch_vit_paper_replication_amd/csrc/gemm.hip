@@ -36,6 +36,9 @@ enum GemmEpi : int {
 namespace {
 
 PVR_DEV void stamp(const GemmParams& p, int slot) {
+#ifdef PVR_GEMM_PHASE_STAMPS
+  return;  // p.dbg holds the per-wave phase sums instead (PpStamps)
+#endif
   if (p.dbg && threadIdx.x == 0) {
     const int b = blockIdx.x + gridDim.x * blockIdx.z;
     p.dbg[(int64_t)b * 8 + slot] = __builtin_amdgcn_s_memtime();
@@ -779,10 +782,35 @@ PVR_DEV v4f mfma_fp8(const v8s& a0, const v8s& a1, const v8s& b0, const v8s& b1,
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, FA, FB, 0, 127, 0, 127);
 }
 
+// Per-wave phase-segment cycle sums of the ping-pong K loop (diagnostic builds, -DPVR_GEMM_PHASE_STAMPS;
+// scripts/gemm_phase_stamps.py): reads issue | DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait |
+// MFMA issue | barrier 2 | (slot 7: whole K loop), summed over every phase, written once per wave to
+// p.dbg[(workgroup * 8 + wave) * 8 + segment]. Production builds compile the stamps out.
+struct PpStamps {
+#ifdef PVR_GEMM_PHASE_STAMPS
+  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t last = 0;
+#endif
+  PVR_DEV void at(int k) {
+#ifdef PVR_GEMM_PHASE_STAMPS
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    acc[k] += t - last;
+    last = t;
+#else
+    (void)k;
+#endif
+  }
+  PVR_DEV void begin() {
+#ifdef PVR_GEMM_PHASE_STAMPS
+    last = __builtin_amdgcn_s_memtime();
+#endif
+  }
+};
+
 template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool SWAP, int ES = 2, int FA = 0, int FB = 0>
 PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
                       __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
-                      int t_issue, int nk, int wave, int lane, int wm, int wn) {
+                      int t_issue, int nk, int wave, int lane, int wm, int wn, PpStamps& pst) {
   // R: register subtile for this quadrant. mn-contiguous operands are read with the asm transpose
   // read (halves combined after the wait below): the builtin would make hipcc drain the in-flight
   // half-tile DMAs (vmcnt(0)) in front of the read.
@@ -821,9 +849,13 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           read_frag_mn_async<128>(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, ks, lane, blo[jj][ks], bhi[jj][ks]);
       }
   }
+  pst.at(0);
   pp_issue<KIND, AK, BKC, ES>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
+  pst.at(1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  pst.at(2);
   pp_barrier();
+  pst.at(3);
   if constexpr (AK && BKC)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   else
@@ -854,6 +886,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = cat44(blo[jj][ks], bhi[jj][ks]);
   }
+  pst.at(4);
   __builtin_amdgcn_s_setprio(1);
   if constexpr (ES == 1) {
 #pragma unroll
@@ -867,7 +900,9 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           c = mfma_fp8<FA, FB>(af[ii][0], af[ii][1], bf[QN][jj][0], bf[QN][jj][1], c);
       }
     __builtin_amdgcn_s_setprio(0);
+    pst.at(5);
     pp_barrier();
+    pst.at(6);
     return;
   }
 #pragma unroll
@@ -883,7 +918,9 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           c = mfma16(af[ii][ks], bf[QN][jj][ks], c);
       }
   __builtin_amdgcn_s_setprio(0);
+  pst.at(5);
   pp_barrier();
+  pst.at(6);
 }
 
 // Register-direct epilogue of the ping-pong kernels (SWAP layout, bf16-output epilogues, no row
@@ -1451,6 +1488,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   v8s af[4][2], bf[2][2][2];
+  PpStamps pst;
 
   stamp(p, 0);
   // prologue: half-tiles 0..5 = all of K-tile 0, A0/B0 of K-tile 1
@@ -1464,18 +1502,30 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   pp_barrier();
   if (wm == 1) pp_barrier();  // group 1 runs one barrier behind
   stamp(p, 1);
+  pst.begin();
+#ifdef PVR_GEMM_PHASE_STAMPS
+  const uint64_t pst0 = pst.last;
+#endif
 
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * PP_BUF;
     // phase P = 4t + ph issues half-tile P + 6 = 4(t+1) + ph + 2
-    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
-    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn);
-    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
-    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn);
+    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn, pst);
+    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn, pst);
+    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn, pst);
+    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn, pst);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
   stamp(p, 2);
+#ifdef PVR_GEMM_PHASE_STAMPS
+  pst.acc[7] = __builtin_amdgcn_s_memtime() - pst0;
+  if (p.dbg && lane == 0) {
+    const int64_t b = blockIdx.x + (int64_t)gridDim.x * blockIdx.z;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.dbg[(b * 8 + wave) * 8 + k] = pst.acc[k];
+  }
+#endif
   if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU) {
     if (tpart >= 0 && !tail_gather(p, acc, smem, tloc, tpart)) return;  // another part finishes the tile
   }

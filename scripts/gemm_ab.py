@@ -18,7 +18,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("PVR_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # PVR_PKG_ROOT: an A/B build
 from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
 from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
 

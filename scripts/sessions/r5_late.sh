@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5: ping-pong GEMM with each phase's half-tile DMA issued inside its MFMA block (-DPVR_PP_DMA_LATE,
+# ab_late/) vs the in-tree build: kernel checks on the variant, phase stamps of both, the step's GEMMs
+# alternating (gemm_ab.py), then whole-step benches alternating.
+R="${GRAFT_REPO_ROOT:-/root/repo}"; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
+O=gpurun_out/${1:-r5late}; mkdir -p "$O"
+step() { local t=$1 log=$2; shift 2; timeout -k 10 "$t" "$@" > "$O/$log" 2>&1; local rc=$?; echo "[$log] rc=$rc"; tail -n 2 "$O/$log" | cut -c1-200; [ $rc -eq 0 ] || exit $rc; }
+PVR_PKG_ROOT=$R/ab_late step 600 kernels_late.log python -u -m pytest tests/test_gpu_kernels.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+PVR_PKG_ROOT=$R/ab_gst step 120 stamps_base.log python scripts/gemm_phase_stamps.py
+PVR_PKG_ROOT=$R/ab_glate step 120 stamps_late.log python scripts/gemm_phase_stamps.py
+for i in 1 2; do
+  step 300 gemm_base_$i.log python scripts/gemm_ab.py
+  PVR_PKG_ROOT=$R/ab_late step 300 gemm_late_$i.log python scripts/gemm_ab.py
+done
+for i in 1 2; do
+  step 200 b16_base_$i.log python bench.py
+  PVR_PKG_ROOT=$R/ab_late step 200 b16_late_$i.log python bench.py
+done

@@ -6,6 +6,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# PVR_PKG_ROOT: a directory holding another build of the package (same-session A/B of a kernel
+# variant against the same checks); it shadows the tree's own package
+if os.environ.get("PVR_PKG_ROOT"):
+    sys.path.insert(0, os.environ["PVR_PKG_ROOT"])
 
 
 def pytest_configure(config):
