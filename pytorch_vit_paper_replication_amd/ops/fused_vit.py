@@ -345,9 +345,13 @@ class EncoderBlockFn(torch.autograd.Function):
         side_db = False
         db_part = None
         prow = ext.attn_bwd_bias_rows(B, N, H, D, aseed is not None) if gbqkv is not None else 0
-        fp8_qkv = f8d is not None and f8d[0].wgrad_ready(f8d[1], 3, 0) and store.bf16_t(wqkv) is not None
-        # fp8: dQKV's e5m2 copy (grad slot 3: the qkv dgrad and weight-gradient operand) written by the
-        # attention backward's own stores once the slot is calibrated (generic kernels)
+        # the qkv dgrad runs in fp8 (W^T shadow present); its weight gradient too once both slots are
+        # calibrated and fp8 weight gradients are on (enable_fp8(wgrad=True), opt-in)
+        fp8_qkv = f8d is not None and store.bf16_t(wqkv) is not None
+        wgrad8_qkv = fp8_qkv and f8d[0].wgrad_ready(f8d[1], 3, 0)
+        # fp8: dQKV's e5m2 copy (grad slot 3: the qkv dgrad operand, and the weight-gradient operand when
+        # that runs in fp8) written by the attention backward's own stores once the slot is calibrated
+        # (generic kernels) - with bf16 weight gradients too, instead of a separate quantize pass over dQKV
         q8kw, q8res = {}, None
         if fp8_qkv:
             prod = f8d[0].grad_producer(f8d[1], 3)
@@ -355,8 +359,8 @@ class EncoderBlockFn(torch.autograd.Function):
                 meta, slot = prod
                 q8 = torch.empty(T, 3 * D, dtype=torch.uint8, device=do.device)
                 # dQKV's bf16 copy is not stored when every reader takes the e5m2 copy: the qkv dgrad
-                # and weight gradient (fp8_qkv) and the bias gradient (kernel partials, prow > 0)
-                q8_only = prow > 0 and DGRAD_TAP is None and T >= 256
+                # and weight gradient (both fp8) and the bias gradient (kernel partials, prow > 0)
+                q8_only = wgrad8_qkv and prow > 0 and DGRAD_TAP is None and T >= 256
                 q8kw = dict(q_out=q8, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1], q_only=q8_only)
                 q8res = (q8, meta.dscale[slot:slot + 1])
         if prow > 0:

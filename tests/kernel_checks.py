@@ -1076,6 +1076,42 @@ def check_vit_fp8_bf16_skip(B=4, steps=4, image=64, images=None):
             {"grad_l2": 1e-6, "nonfinite": 0, "loss_diff": 1e-2, "param_l2": 1e-3})
 
 
+def check_vit_fp8_default_producers(images=64, steps=8):
+    """The default fp8 recipe (fp8 forward + dgrad, bf16 weight gradients): once the slots are
+    calibrated, every e5m2 gradient operand of the fp8 dgrad GEMMs comes from its producer kernel
+    (LayerNorm backward, dGELU epilogue, bias-gradient pass, attention backward for dQKV) - no separate
+    quantize pass runs in a steady-state step - and training stays finite with a falling loss."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+    from pytorch_vit_paper_replication_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    m = ViT(**_FP8_CFG).to(DEV).enable_fp8()
+    x = torch.rand(images, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (images,), device=DEV)
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    calls = []
+    losses = []
+    for i in range(steps):
+        st = m._fp8  # created by the first forward
+        orig = st.grad_quant if st is not None else None
+        if i == steps - 1:  # steady state: count the quantize passes of the last step
+            st.grad_quant = lambda g, block, which: calls.append((block, which)) or orig(g, block, which)
+        try:
+            loss = cross_entropy(m(x), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step(clip_norm=1.0)
+        finally:
+            if st is not None:
+                st.__dict__.pop("grad_quant", None)  # back to the class method
+        losses.append(loss.item())
+    met = {"quantize_passes": float(len(calls)), "nonfinite": float(not all(math.isfinite(v) for v in losses)),
+           "loss_not_falling": float(not losses[-1] < losses[0])}
+    return (f"vit fp8 default recipe (bf16 wgrad): steady-state quantize passes {sorted(set(calls))}, "
+            f"loss {losses[0]:.3f}->{losses[-1]:.3f}", met, {"quantize_passes": 0, "nonfinite": 0, "loss_not_falling": 0})
+
+
 def check_vit_fp8_dgrad(B=4):
     """fp8 dgrad GEMMs (enable_fp8(dgrad=True): e5m2 gradients x e4m3 W^T) against the bf16 dgrads of the
     same fp8-forward model, PER dgrad output tensor (fc2 / fc1 / out-proj / qkv of every block, tapped
@@ -1565,6 +1601,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_fp8_producer(1030, 768, 1280, True),
         check_vit_fp8,
         check_vit_fp8_dgrad,
+        check_vit_fp8_default_producers,
         check_vit_fp8_wgrad,
         check_vit_fp8_bf16_skip,
         # 257 tokens: the attention backward's lastkey path writes dQKV's e5m2 copy and the in_proj bias
