@@ -325,6 +325,10 @@ def main():
                        "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
                        "dropout": "off (eval)" if args.infer else "0.1 (mlp, embedding)",
                        "final_loss": round(final_loss, 4),
+                       # BASELINE configs 2 / 3: 256 images on one GPU, 512 per GPU on 2-8 (global 4096 at 8);
+                       # efficiency against 1 GPU at 512 (bench.py --batch 512 --force-ddp) keeps per-GPU work fixed
+                       "scaling_note": "per-GPU batch 256 at 1 GPU (config 2), 512 at 2-8 GPUs (config 3)"
+                       if name == "ViT-B/16" and args.batch is None and not args.infer else None,
                        "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2)},
         }
         print(json.dumps(out), flush=True)
