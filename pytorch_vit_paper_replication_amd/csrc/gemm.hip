@@ -786,18 +786,32 @@ PVR_DEV v4f mfma_fp8(const v8s& a0, const v8s& a1, const v8s& b0, const v8s& b1,
 // scripts/gemm_phase_stamps.py): reads issue | DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait |
 // MFMA issue | barrier 2 | (slot 7: whole K loop), summed over every phase, written once per wave to
 // p.dbg[(workgroup * 8 + wave) * 8 + segment]. Production builds compile the stamps out.
+// -DPVR_GEMM_PHASE_BY_TYPE (with -DPVR_GEMM_PHASE_STAMPS): slots 0-3 = whole phase by phase type
+// (quadrant order (0,0) (0,1) (1,1) (1,0)), 4-7 = its reads + DMA issue + vmcnt wait part.
 struct PpStamps {
 #ifdef PVR_GEMM_PHASE_STAMPS
   uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t last = 0;
+  uint64_t t0 = 0;
 #endif
   PVR_DEV void at(int k) {
-#ifdef PVR_GEMM_PHASE_STAMPS
+#if defined(PVR_GEMM_PHASE_STAMPS) && !defined(PVR_GEMM_PHASE_BY_TYPE)
     const uint64_t t = __builtin_amdgcn_s_memtime();
     acc[k] += t - last;
     last = t;
 #else
     (void)k;
+#endif
+  }
+  PVR_DEV void type_mark(int pt, int what) {  // what 0: phase start, 1: R-part end, 2: phase end
+#if defined(PVR_GEMM_PHASE_STAMPS) && defined(PVR_GEMM_PHASE_BY_TYPE)
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (what == 0) t0 = t;
+    else if (what == 1) acc[4 + pt] += t - t0;
+    else acc[pt] += t - t0;
+#else
+    (void)pt;
+    (void)what;
 #endif
   }
   PVR_DEV void begin() {
@@ -811,6 +825,9 @@ template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool 
 PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
                       __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
                       int t_issue, int nk, int wave, int lane, int wm, int wn, PpStamps& pst) {
+  constexpr int PT_ = QM == 0 ? QN : 3 - QN;  // phase type: (0,0) (0,1) (1,1) (1,0)
+  pst.type_mark(PT_, 0);
+
   // R: register subtile for this quadrant. mn-contiguous operands are read with the asm transpose
   // read (halves combined after the wait below): the builtin would make hipcc drain the in-flight
   // half-tile DMAs (vmcnt(0)) in front of the read.
@@ -853,6 +870,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
   pp_issue<KIND, AK, BKC, ES>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
   pst.at(1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  pst.type_mark(PT_, 1);
   pst.at(2);
   pp_barrier();
   pst.at(3);
@@ -903,6 +921,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
     pst.at(5);
     pp_barrier();
     pst.at(6);
+    pst.type_mark(PT_, 2);
     return;
   }
 #pragma unroll
@@ -921,6 +940,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
   pst.at(5);
   pp_barrier();
   pst.at(6);
+  pst.type_mark(PT_, 2);
 }
 
 // Register-direct epilogue of the ping-pong kernels (SWAP layout, bf16-output epilogues, no row

@@ -20,11 +20,22 @@ from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
 from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
 
 SEG = ["reads issue", "DMA issue", "vmcnt wait", "barrier 1", "lgkmcnt wait", "MFMA issue", "barrier 2", "K loop total"]
+if os.environ.get("PPT"):  # build with -DPVR_GEMM_PHASE_BY_TYPE too: per phase type (4 per K-tile)
+    SEG = ["phase (0,0) whole", "phase (0,1) whole", "phase (1,1) whole", "phase (1,0) whole",
+           "phase (0,0) R-part", "phase (0,1) R-part", "phase (1,1) R-part", "phase (1,0) R-part"]
 
 
 def report(name, dbg, nphases):
     d = dbg.view(-1, 8).double()
-    d = d[d[:, 7] > 0]
+    if not os.environ.get("PPT"):
+        d = d[d[:, 7] > 0]
+    if os.environ.get("PPT"):
+        d = d[d[:, 0] > 0]
+        med = d.median(0).values / (nphases / 4)
+        print(f"# {name}: {d.shape[0]} waves, cycles per phase of each type (median over waves)", flush=True)
+        for k, s in enumerate(SEG):
+            print(f"  {s:20s} {med[k].item():8.1f}", flush=True)
+        return
     med = d.median(0).values / nphases
     print(f"# {name}: {d.shape[0]} waves, cycles per phase (median over waves; 16 MFMAs per wave per phase)", flush=True)
     for k, s in enumerate(SEG):
