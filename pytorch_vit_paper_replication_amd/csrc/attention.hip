@@ -1377,6 +1377,13 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
   const int npr = p1 - p0;
   PairOff prv = cur;
   int sl = 0;  // ring slot of block t (t mod 3)
+#ifdef PVR_ATTN_STAMPS
+  // slots: 0 wait + barrier, 1 DMA group issue, 2 pair switch (previous pair's dQ / dK / dV, V
+  // fragments), 3 S / dP, 4 dQ, 5 next table, 6 P / dS + dV / dK, 7 loop total
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+  const uint64_t st_0 = st_last;
+#endif
   // global stores of a block (dQ of the previous block, its bias partials, a pair's dK / dV) are issued
   // after the block's DMA group: the next block's wait retires the group but leaves them in flight
   // (a plain vmcnt(0) there waited for their write acknowledgements, ~1-2 us per block)
@@ -1403,6 +1410,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
         case 19: wait_barrier_lds<19>(); break;
         default: wait_barrier_lds<0>(); break;
       }
+      ASTAMP(0);
       nst = (qb == 0 && pi > 0 ? 17 + pdb : 0) + (qb != 0 ? 1 + pdb : 0);
       const char* qimg = ring + sl * SLOT;
       const char* doimg = qimg + 4096;
@@ -1414,6 +1422,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
         issue_group(cur, qb + 2, ring + sl2 * SLOT, qb >= 1 && has_next, qb - 1, nxt, knext);
       else
         issue_group(has_next ? nxt : cur, has_next ? qb + 2 - NQ : 0, ring + sl2 * SLOT, has_next, qb - 1, nxt, knext);
+      ASTAMP(1);
       if (qb == 0) {
         if (pi > 0) {
           // the previous pair's last block (its K image is the other buffer) and its dK / dV
@@ -1428,6 +1437,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
             for (int ks = 0; ks < 2; ++ks) vf[f][ks] = ds_read_b128(vimg + kw0 * 128 + 2048 * f + (ks ? fr1 : fr0));
         }
       }
+      ASTAMP(2);
       // ---- phase 1a: S[q][key], dP[q][key] of the wave's two key fragments
       v4f s[2][2], dp[2][2];
       if (nf > 0) {
@@ -1455,13 +1465,16 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
               dp[a][f] = mfma16(dA[ks][a], vf[f][ks], dp[a][f]);
             }
       }
+      ASTAMP(3);
       // ---- phase 2 of block t-1 (same pair), while the S / dP products drain
       if (qb != 0) phase2(dsb + ((t - 1) & 1) * DSB, kimg, qb - 1, cur, p0 + pi);
+      ASTAMP(4);
       // ---- table of block t+1 (landed at this block's wait)
       if (qb + 1 < NQ)
         block_table(ring + sl1 * SLOT, qb + 1, (t + 1) & 1);
       else if (has_next)
         block_table(ring + sl1 * SLOT, 0, (t + 1) & 1);
+      ASTAMP(5);
       // ---- phase 1b: P, dS of both key fragments (dS^T -> LDS), then dV^T += dO^T P, dK^T += Q^T dS
       // one dims fragment at a time (transposed Q / dO reads double-buffered)
       if (nf > 0) {
@@ -1528,10 +1541,18 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
           if (li == 0) *(v4f*)(vsb + 16 * e + 4 * g) = cs;
         }
       }
+      ASTAMP(6);
       sl = sl1;
     }
     prv = cur;
   }
+#ifdef PVR_ATTN_STAMPS
+  st_acc[7] = __builtin_amdgcn_s_memtime() - st_0;
+  if (g_attn_dbg && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g_attn_dbg[((int64_t)blockIdx.x * 8 + wave) * 8 + k] = st_acc[k];
+  }
+#endif
   // last block's dQ and the last pair's dK / dV
   wait_barrier_lds<0>();
   phase2(dsb + ((npr * NQ - 1) & 1) * DSB, kimg0 + ((npr - 1) & 1) * IMG, NQ - 1, prv, p1 - 1);
