@@ -1556,13 +1556,15 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
       epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
   } else if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
     if (!p.epi_staged && direct_ok(p)) {
-      if (p.resid)
-        epilogue_direct<EPI, true, ES == 1>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
+      // (one instance per epilogue actually reachable: a residual exists for BF16 only; a second,
+      // identical GELU / dGELU copy doubled the kernel's code, and its hot path's I-cache footprint)
+      if (EPI == EPI_BF16 && p.resid)
+        epilogue_direct<EPI, EPI == EPI_BF16, ES == 1>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
       else
         epilogue_direct<EPI, false, ES == 1>(p, acc, smem, m0 + wm * 128, n0 + wn * 64, wm, wn, lane);
     } else if (!p.addend && !p.row_group && (p.N & 3) == 0) {
-      if (p.resid)
-        epilogue_staged<EPI, 128, true>(p, acc, smem, m0, n0, wm, wn, lane);
+      if (EPI == EPI_BF16 && p.resid)
+        epilogue_staged<EPI, 128, EPI == EPI_BF16>(p, acc, smem, m0, n0, wm, wn, lane);
       else
         epilogue_staged<EPI, 128, false>(p, acc, smem, m0, n0, wm, wn, lane);
     }
@@ -1818,13 +1820,13 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
     // registers (DIRECT; the DGELU column-sum exchange uses the separate region) or stages in the
     // separate region behind them.
     if constexpr (DIRECT) {
-      if (p.resid)
-        epilogue_direct<EPI, true, ES == 1>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
+      if (EPI == EPI_BF16 && p.resid)  // (see gemm_pp_kernel: one instance per reachable epilogue)
+        epilogue_direct<EPI, EPI == EPI_BF16, ES == 1>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
       else
         epilogue_direct<EPI, false, ES == 1>(p, acc, smem + 2 * PP_BUF, cur.m0 + wm * 128, cur.n0 + wn * 64, wm, wn, lane);
     } else if constexpr (ES == 2) {
-      if (p.resid)
-        epilogue_staged<EPI, 32, true>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
+      if (EPI == EPI_BF16 && p.resid)
+        epilogue_staged<EPI, 32, EPI == EPI_BF16>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
       else
         epilogue_staged<EPI, 32, false>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
     }
