@@ -1018,8 +1018,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
 //   written per query (ds_last, added to dQ by the main kernel's dQ epilogue), and dV[kt] = sum p dO,
 //   dK[kt] = scale * sum ds Q reduced here. For ViT's N = 256 + 1 (the CLS token of 224/14) the main
 //   kernel's key blocks are then exactly full.
-// Thread = (row slot, 16-B head-dim chunk): 16 lanes share one query row (coalesced 16-B chunks),
-// 16 row slots per workgroup walk the queries; memory-bound, no MFMA.
+// Thread = (row slot, 1/8 of the head row): 8 lanes share one query row (DH / 8 consecutive elements
+// each: 16 B at dh 64, 20 B at dh 80), 32 row slots per workgroup walk the queries; memory- and
+// latency-bound, no MFMA. (The round-4 form gave each row 16 lanes of 16 B: at dh 80 six of every
+// 16 lanes idled and a pair took 17 dependent trips instead of 9.)
 template <int DH, bool LAST>
 __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                              const uint16_t* __restrict__ dout, int64_t ld_do,
@@ -1028,104 +1030,116 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __re
                                                              float* __restrict__ dsl, float* __restrict__ bpart,
                                                              uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H, int D,
                                                              float scale, AttnQ8 q8) {
-  constexpr int NCH = DH / 8;  // 16-B chunks per head row (<= 16)
-  constexpr int RS = 16;       // row slots
-  static_assert(NCH <= 16, "head dim <= 128");
-  __shared__ float red[3][RS][DH];
+  constexpr int E = DH / 8;   // elements per lane (8 / 10 / 12 / 16)
+  constexpr int W = E / 2;    // dwords per lane and row
+  constexpr int RS = 32;      // row slots (8 per wave)
+  static_assert(DH % 16 == 0 && DH <= 128, "head dim");
+  __shared__ float red[3][4][DH];  // per-wave partial column sums
   const int pr = blockIdx.x;
   const int b = pr / H, h = pr % H;
-  const int tid = threadIdx.x;
-  const int ch = tid & 15, rs = tid >> 4;
-  const bool act = ch < NCH;
-  const int cc = act ? ch : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = lane & 7, rs = tid >> 3;  // this lane's eighth of the row, row slot
   const int kt = N - 1;
-  const uint16_t* qbase = qkv + (int64_t)b * N * ld + h * DH + cc * 8;
-  auto unpack = [](const uint4& w, float (&x)[8]) {
-    const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+  const int col = h * DH + ch * E;
+  auto load_row = [](const uint16_t* p, uint32_t (&w)[W]) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = bf2f(j & 1 ? u[j >> 1] >> 16 : u[j >> 1] & 0xFFFF);
+    for (int j = 0; j < W; ++j) w[j] = ((const uint32_t*)p)[j];
   };
-  float kf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, vf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (LAST && act) {  // this lane's chunk of K and V of key kt
-    unpack(*(const uint4*)(qbase + (int64_t)kt * ld + D), kf);
-    unpack(*(const uint4*)(qbase + (int64_t)kt * ld + 2 * D), vf);
+  auto unpack = [](const uint32_t (&w)[W], float (&x)[E]) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) x[j] = bf2f(j & 1 ? w[j >> 1] >> 16 : w[j >> 1] & 0xFFFF);
+  };
+  auto row8_sum = [](float v) {  // the row's 8 lanes
+#pragma unroll
+    for (int off = 4; off > 0; off >>= 1) v += __shfl_xor(v, off, 8);
+    return v;
+  };
+  const uint16_t* qrow0 = qkv + (int64_t)b * N * ld + col;
+  float kf[E], vf[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) kf[j] = vf[j] = 0.f;
+  if constexpr (LAST) {  // this lane's part of K and V of key kt
+    uint32_t kw[W], vw[W];
+    load_row(qrow0 + (int64_t)kt * ld + D, kw);
+    load_row(qrow0 + (int64_t)kt * ld + 2 * D, vw);
+    unpack(kw, kf);
+    unpack(vw, vf);
   }
   const float c = scale * LOG2E;
-  float av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, ak[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float ov_sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of dO (the v-bias gradient)
-  // U rows per thread per trip with all their loads issued first (the loop is latency-bound:
-  // one row at a time waited a global-load round trip per 16 rows of the head)
-  // (LAST: one row per trip: two rows cost the registers of 4 -> 6 waves per SIMD and measured
-  // 131-136 vs 123-130 us per ViT-H/14 b256 layer; profiles/r4/ab11 vs ab9)
-  constexpr int U = LAST ? 1 : 4;
-  for (int q0 = rs; q0 < N; q0 += RS * U) {
-    uint4 dw[U], ow[U], qw[U];
+  float av[E], ak[E], ov_sum[E];  // dV[kt], dK[kt] partials; column sums of dO (the v-bias gradient)
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int q = min(q0 + u * RS, N - 1);
-      const int64_t row = (int64_t)b * N + q;
-      dw[u] = *(const uint4*)(dout + row * ld_do + h * DH + cc * 8);
-      ow[u] = *(const uint4*)(o + row * ld_o + h * DH + cc * 8);
-      if constexpr (LAST) qw[u] = *(const uint4*)(qbase + (int64_t)q * ld);
+  for (int j = 0; j < E; ++j) av[j] = ak[j] = ov_sum[j] = 0.f;
+  const int trips = (N + RS - 1) / RS;  // every row slot takes the same trips (rows past N: not live)
+  for (int t = 0; t < trips; ++t) {
+    const int q = rs + t * RS;
+    const bool live = q < N;  // (uniform per row slot; the row's 8 lanes agree)
+    const int qc = min(q, N - 1);
+    const int64_t row = (int64_t)b * N + qc;
+    uint32_t dw[W], ow[W], qw[W];
+    load_row(dout + row * ld_do + col, dw);
+    load_row(o + row * ld_o + col, ow);
+    if constexpr (LAST) load_row(qrow0 + (int64_t)qc * ld, qw);
+    const float lq = LAST ? lse[(int64_t)pr * N + qc] : 0.f;
+    float dv[E], ov[E];
+    unpack(dw, dv);
+    unpack(ow, ov);
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < E; ++j) dl = fmaf(dv[j], ov[j], dl);
+    dl = row8_sum(dl);
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) ov_sum[j] += dv[j];
     }
+    if constexpr (LAST) {
+      float qv[E];
+      unpack(qw, qv);
+      float sdot = 0.f, dpdot = 0.f;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int q = q0 + u * RS;
-      const bool live = q < N;  // (uniform per row slot; the row's 16 lanes agree)
-      float dv[8], ov[8];
-      unpack(dw[u], dv);
-      unpack(ow[u], ov);
-      if (live) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ov_sum[j] += dv[j];
+      for (int j = 0; j < E; ++j) {
+        sdot = fmaf(qv[j], kf[j], sdot);
+        dpdot = fmaf(dv[j], vf[j], dpdot);
       }
-      float dl = 0.f;
+      sdot = row8_sum(sdot);
+      dpdot = row8_sum(dpdot);
+      const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -lq * LOG2E));
+      const float ds = live ? p * (dpdot - dl) : 0.f;
+      const float pl = live ? p : 0.f;
+      if (ch == 0 && live) dsl[(int64_t)pr * N + q] = ds;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dl = fmaf(dv[j], ov[j], dl);
-      if (!act) dl = 0.f;
-#pragma unroll
-      for (int off = 8; off > 0; off >>= 1) dl += __shfl_xor(dl, off, 16);  // the row's 16 lanes
-      if constexpr (LAST) {
-        float qv[8];
-        unpack(qw[u], qv);
-        float sdot = 0.f, dpdot = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          sdot = fmaf(qv[j], kf[j], sdot);
-          dpdot = fmaf(dv[j], vf[j], dpdot);
-        }
-#pragma unroll
-        for (int off = 8; off > 0; off >>= 1) {
-          sdot += __shfl_xor(sdot, off, 16);
-          dpdot += __shfl_xor(dpdot, off, 16);
-        }
-        const float p = __builtin_amdgcn_exp2f(fmaf(sdot, c, -lse[(int64_t)pr * N + min(q, N - 1)] * LOG2E));
-        const float ds = live ? p * (dpdot - dl) : 0.f;
-        const float pl = live ? p : 0.f;
-        if (ch == 0 && live) dsl[(int64_t)pr * N + q] = ds;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          av[j] = fmaf(pl, dv[j], av[j]);
-          ak[j] = fmaf(ds, qv[j], ak[j]);
-        }
+      for (int j = 0; j < E; ++j) {
+        av[j] = fmaf(pl, dv[j], av[j]);
+        ak[j] = fmaf(ds, qv[j], ak[j]);
       }
-      if (ch == 0 && live) dlt[(int64_t)pr * N + q] = dl;
     }
+    if (ch == 0 && live) dlt[(int64_t)pr * N + q] = dl;
   }
   if (!LAST && !bpart) return;
-  if (act) {
+  // column sums: the wave's 8 row slots (lanes ch, ch + 8, ..) by shuffles, then the 4 waves via LDS
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[0][rs][cc * 8 + j] = av[j];
-      red[1][rs][cc * 8 + j] = ak[j];
-      red[2][rs][cc * 8 + j] = ov_sum[j];
+  for (int j = 0; j < E; ++j) {
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1) {
+      ov_sum[j] += __shfl_xor(ov_sum[j], off);
+      if constexpr (LAST) {
+        av[j] += __shfl_xor(av[j], off);
+        ak[j] += __shfl_xor(ak[j], off);
+      }
+    }
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      red[0][wave][ch * E + j] = av[j];
+      red[1][wave][ch * E + j] = ak[j];
+      red[2][wave][ch * E + j] = ov_sum[j];
     }
   }
   __syncthreads();
   if (tid < DH) {
     float sv = 0.f, sk = 0.f, so = 0.f;
 #pragma unroll
-    for (int r = 0; r < RS; ++r) {
+    for (int r = 0; r < 4; ++r) {
       sv += red[0][r][tid];
       sk += red[1][r][tid];
       so += red[2][r][tid];
