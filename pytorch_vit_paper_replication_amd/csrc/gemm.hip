@@ -786,6 +786,7 @@ PVR_DEV v4f mfma_fp8(const v8s& a0, const v8s& a1, const v8s& b0, const v8s& b1,
 // scripts/gemm_phase_stamps.py): reads issue | DMA issue | vmcnt wait | barrier 1 | lgkmcnt wait |
 // MFMA issue | barrier 2 | (slot 7: whole K loop), summed over every phase, written once per wave to
 // p.dbg[(workgroup * 8 + wave) * 8 + segment]. Production builds compile the stamps out.
+// -DPVR_GEMM_PHASE_ONLY_TYPE=t (with -DPVR_GEMM_PHASE_STAMPS): the same segments, phases of type t only.
 // -DPVR_GEMM_PHASE_BY_TYPE (with -DPVR_GEMM_PHASE_STAMPS): slots 0-3 = whole phase by phase type
 // (quadrant order (0,0) (0,1) (1,1) (1,0)), 4-7 = its reads + DMA issue + vmcnt wait part.
 struct PpStamps {
@@ -794,13 +795,20 @@ struct PpStamps {
   uint64_t last = 0;
   uint64_t t0 = 0;
 #endif
-  PVR_DEV void at(int k) {
+  // pt: the calling phase's type; -DPVR_GEMM_PHASE_ONLY_TYPE=t sums the segments of type-t phases only
+  PVR_DEV void at(int k, int pt) {
 #if defined(PVR_GEMM_PHASE_STAMPS) && !defined(PVR_GEMM_PHASE_BY_TYPE)
     const uint64_t t = __builtin_amdgcn_s_memtime();
+#ifdef PVR_GEMM_PHASE_ONLY_TYPE
+    if (pt == PVR_GEMM_PHASE_ONLY_TYPE) acc[k] += t - last;
+#else
+    (void)pt;
     acc[k] += t - last;
+#endif
     last = t;
 #else
     (void)k;
+    (void)pt;
 #endif
   }
   PVR_DEV void type_mark(int pt, int what) {  // what 0: phase start, 1: R-part end, 2: phase end
@@ -866,14 +874,14 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           read_frag_mn_async<128>(buf + 256 * 128 + QN * 16384, wn * 32 + 16 * jj, ks, lane, blo[jj][ks], bhi[jj][ks]);
       }
   }
-  pst.at(0);
+  pst.at(0, PT_);
   pp_issue<KIND, AK, BKC, ES>(ars, brs, nul, smem, lda, ldb, t_issue, nk, wave, lane);
-  pst.at(1);
+  pst.at(1, PT_);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pst.type_mark(PT_, 1);
-  pst.at(2);
+  pst.at(2, PT_);
   pp_barrier();
-  pst.at(3);
+  pst.at(3, PT_);
   if constexpr (AK && BKC)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   else
@@ -904,7 +912,7 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) bf[QN][jj][ks] = cat44(blo[jj][ks], bhi[jj][ks]);
   }
-  pst.at(4);
+  pst.at(4, PT_);
   __builtin_amdgcn_s_setprio(1);
   if constexpr (ES == 1) {
 #pragma unroll
@@ -918,9 +926,9 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           c = mfma_fp8<FA, FB>(af[ii][0], af[ii][1], bf[QN][jj][0], bf[QN][jj][1], c);
       }
     __builtin_amdgcn_s_setprio(0);
-    pst.at(5);
+    pst.at(5, PT_);
     pp_barrier();
-    pst.at(6);
+    pst.at(6, PT_);
     pst.type_mark(PT_, 2);
     return;
   }
@@ -937,9 +945,9 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
           c = mfma16(af[ii][ks], bf[QN][jj][ks], c);
       }
   __builtin_amdgcn_s_setprio(0);
-  pst.at(5);
+  pst.at(5, PT_);
   pp_barrier();
-  pst.at(6);
+  pst.at(6, PT_);
   pst.type_mark(PT_, 2);
 }
 

@@ -6,6 +6,7 @@ over waves per phase (4 phases per 64-deep K-tile). Shapes: the ViT-B/16 b256 qk
 form (k-contiguous: tile 12), same FLOPs.
 
   PVR_PKG_ROOT=ab_gst python scripts/gemm_phase_stamps.py
+  ONLY_TYPE=0 PVR_PKG_ROOT=ab_t0 python scripts/gemm_phase_stamps.py   # -DPVR_GEMM_PHASE_ONLY_TYPE=0 build
 """
 from __future__ import annotations
 
@@ -37,6 +38,9 @@ def report(name, dbg, nphases):
             print(f"  {s:20s} {med[k].item():8.1f}", flush=True)
         return
     med = d.median(0).values / nphases
+    if os.environ.get("ONLY_TYPE"):  # build with -DPVR_GEMM_PHASE_ONLY_TYPE=t: a quarter of the phases summed
+        med[:7] *= 4
+        name += f" [phase type {os.environ['ONLY_TYPE']} only]"
     print(f"# {name}: {d.shape[0]} waves, cycles per phase (median over waves; 16 MFMAs per wave per phase)", flush=True)
     for k, s in enumerate(SEG):
         print(f"  {s:14s} {med[k].item():8.1f}", flush=True)
