@@ -1792,8 +1792,15 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pp_barrier();
 
+  // diagnostic stamps (p.dbg set, scripts/gemm_stamps.py --persistent): per workgroup, cycles in the
+  // K loops and in the epilogues summed over its tiles, the whole kernel, and its tile count
+  const bool dstamp = p.dbg != nullptr;
+  const uint64_t ts0 = dstamp ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t ts_loop = 0, ts_epi = 0, ts_a = 0;
+  int ntile_done = 0;
   int G0 = 0;  // global index (in this workgroup's K-tile stream) of the current tile's K-tile 0
   for (;;) {
+    if (dstamp) ts_a = __builtin_amdgcn_s_memtime();
     v4f acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1824,6 +1831,11 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
       ppp_phase<1, 0, 0, 0, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
     }
     if (wm == 0) pp_barrier();  // re-align the groups for the epilogue
+    uint64_t ts_b = 0;
+    if (dstamp) {
+      ts_b = __builtin_amdgcn_s_memtime();
+      ts_loop += ts_b - ts_a;
+    }
     // The next tile's first DMAs are in flight into the K-tile buffers; the epilogue works from
     // registers (DIRECT; the DGELU column-sum exchange uses the separate region) or stages in the
     // separate region behind them.
@@ -1838,6 +1850,10 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
       else
         epilogue_staged<EPI, 32, false>(p, acc, smem + 2 * PP_BUF, cur.m0, cur.n0, wm, wn, lane);
     }
+    if (dstamp) {
+      ts_epi += __builtin_amdgcn_s_memtime() - ts_b;
+      ++ntile_done;
+    }
     v += gridDim.x;
     if (v >= ntiles) break;
     G0 += nk;
@@ -1849,6 +1865,13 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+  if (dstamp && threadIdx.x == 0) {
+    uint64_t* d = p.dbg + (int64_t)blockIdx.x * 8;
+    d[0] = __builtin_amdgcn_s_memtime() - ts0;
+    d[1] = ts_loop;
+    d[2] = ts_epi;
+    d[3] = (uint64_t)ntile_done;
+  }
 }
 
 template <bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>

@@ -21,11 +21,50 @@ from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
 from pytorch_vit_paper_replication_amd.ops import gemm as G  # noqa: E402
 
 
+def persistent(ext, a):
+    """The persistent form (tile 13) at the ViT-B/16 b256 shape: per workgroup, K-loop and epilogue
+    cycles summed over its tiles and the rest of the kernel (tile hand-offs, start, drain)."""
+    T = 50432
+    N, K = {"bias": (2304, 768), "resid": (768, 768), "gelu": (3072, 768), "dgelu": (3072, 768)}[a.epi]
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    out = torch.empty(T, N, device="cuda", dtype=torch.bfloat16)
+    aux = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    seed = torch.tensor([7], dtype=torch.int64, device="cuda")
+    epi, aux_, drop = (1, aux, (seed, 3 << 32, 0.1)) if a.epi == "gelu" else (0, None, (None, 0, 0.0))
+    dbg = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
+    rows = []
+    for it in range(6):
+        dbg.zero_()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        ext.gemm(x, True, w, True, out, T, N, K, epi, b, None, None, 0, aux_, 0, 0, 0, drop[0], drop[1], drop[2], 0, 13, dbg=dbg,
+                 tail_limit=-1)
+        e.record()
+        torch.cuda.synchronize()
+        if it >= 2:
+            d = dbg.view(-1, 8).cpu().double()
+            d = d[d[:, 3] > 0]
+            rows.append((d, s.elapsed_time(e)))
+    med = statistics.median
+    for d, ms in rows[-2:]:
+        nt = d[:, 3]
+        total, loop, epil = d[:, 0], d[:, 1], d[:, 2]
+        print(f"persistent {a.epi} M{T} N{N} K{K}: {d.shape[0]} workgroups, {ms:.3f} ms; per tile (median over workgroups): "
+              f"loop {med((loop / nt).tolist()):7.0f}  epilogue {med((epil / nt).tolist()):7.0f}  other "
+              f"{med(((total - loop - epil) / nt).tolist()):7.0f}  (tiles per workgroup {med(nt.tolist()):.0f}, "
+              f"kernel {med(total.tolist()):.0f} cycles)", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epi", default="bias", choices=["bias", "resid", "gelu", "dgelu"])
     ap.add_argument("--tiles", default="32,64,128,256,512,1024,2304")
+    ap.add_argument("--persistent", action="store_true", help="the persistent form (tile 13), per-workgroup sums")
     a = ap.parse_args()
+    if a.persistent:
+        return persistent(_ext.ext(), a)
     ext = _ext.ext()
     N, K = {"bias": (2304, 768), "resid": (768, 768), "gelu": (3072, 768), "dgelu": (3072, 768)}[a.epi]
     ntn = N // 256
