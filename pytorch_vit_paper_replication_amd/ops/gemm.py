@@ -53,9 +53,11 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
         # K-tiles stream in under the register-direct epilogue, whose stores stay in flight under
         # the next tile's first K-tile (qkv fwd 0.171-0.179 vs 0.183-0.185 ms, fc1 GELU fwd 0.347-0.352
         # vs 0.361-0.367; N = 768 (2.3 tiles per CU) neutral: profiles/r3/ppp_direct_ab.log). The dGELU
-        # dgrad (column-sum exchange at every tile end) stays on 12: 0.300 vs 0.325 ms (profiles/r3/gemm_ab.log)
+        # dgrad (column-sum exchange at every tile end) too since round 5: 0.298-0.303 vs 0.311-0.315 ms
+        # with the column sums (profiles/r5/tiles_12_13/; round 3 measured the opposite before the
+        # register-direct epilogues, profiles/r3/gemm_ab.log)
         # (any K: limiting it to K <= 2048 measured no gain, profiles/r4/pmaxk/)
-        if K >= 128 and not dgelu and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
+        if K >= 128 and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
             return 13
         return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:

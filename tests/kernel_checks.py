@@ -157,6 +157,24 @@ def check_gemm_gelu_drop_paths(M=3000, N=768, p=0.1):
             {"mask_differs": 0, "rate_dev": rate_limit(p, M * N)})
 
 
+def check_gemm_dgelu_tiles(M=5000, N=3072, K=768):
+    """dGELU dgrad + bias-gradient column sums on the one-tile (12) and persistent (13) ping-pong
+    kernels (the persistent one is the default at ViT sizes since round 5) vs fp32."""
+    dy, w, g = bf(rnd(M, K)), bf(rnd(K, N, scale=0.05)), bf(rnd(M, N))
+    wt = w.t().contiguous()
+    ref = (dy.float() @ w.float()) * g.float()
+    m = {}
+    for t in (12, 13):
+        with tile(t):
+            cs = torch.zeros(N, device=DEV)
+            out = G.linear_dgrad(dy, w, dgelu_aux=g, wt=wt, colsum=cs)
+        l2, mx = errs(out, ref)
+        l2c, _ = errs(cs, ref.sum(0))
+        m.update({f"t{t}_l2": l2, f"t{t}_max": mx, f"t{t}_colsum_l2": l2c})
+    return (f"gemm dGELU dgrad + colsum M{M} N{N} K{K}, tiles 12 / 13 vs fp32", m,
+            {"t12_l2": 3.5e-3, "t12_max": 7e-3, "t12_colsum_l2": 1.5e-6, "t13_l2": 3.5e-3, "t13_max": 7e-3, "t13_colsum_l2": 1.5e-6})
+
+
 def check_gemm_small_splitk(M, N, K, resid=False, gelu=False):
     """Serving-size forward GEMM (few output tiles): split-K fp32 partials + the reduction pass with
     bias / exact GELU / residual, vs a PyTorch fp32 reference."""
@@ -1503,6 +1521,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_dropout(3000, 768, 1024, 0.1, 13),  # persistent, 16 K-tiles (1/K exact in bf16)
         lambda: check_gemm_dropout(3000, 768, 1024, 0.1, 12),  # one tile per workgroup, 16 K-tiles
         lambda: check_gemm_gelu_drop_paths(),
+        lambda: check_gemm_dgelu_tiles(),
         lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
         # split-K tail of the last dispatch round (ViT-B/16 b256 shapes: 591 tiles -> 2 rounds + 79
         # tiles as 3 K-parts; 2364 tiles -> 9 rounds + 60 tiles as 4 K-parts; 588 patch-embed tiles)
