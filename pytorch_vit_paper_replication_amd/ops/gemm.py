@@ -56,8 +56,11 @@ def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = F
         # dgrad (column-sum exchange at every tile end) too since round 5: 0.298-0.303 vs 0.311-0.315 ms
         # with the column sums (profiles/r5/tiles_12_13/; round 3 measured the opposite before the
         # register-direct epilogues, profiles/r3/gemm_ab.log)
-        # (any K: limiting it to K <= 2048 measured no gain, profiles/r4/pmaxk/)
-        if K >= 128 and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
+        # K <= 2048 only: at ViT-L/16-384 (T = 73,856, N = 1024: 4.5 tiles per CU) the long-K GEMMs run
+        # faster one tile per workgroup (fc2 fwd K 4096 0.520 vs 0.539 ms, qkv dgrad K 3072 0.380 vs
+        # 0.396, fc1 dgrad 0.503 vs 0.510; profiles/r5/tiles_12_13/l16_ab.log; ViT-B/16 has no such
+        # GEMM above four tiles per CU, hence round 4's "no gain", profiles/r4/pmaxk/)
+        if 128 <= K <= 2048 and math.ceil(M / 256) * math.ceil(N / 256) >= 4 * _n_cus():
             return 13
         return 12
     if kind == "wgrad" and K >= 4096 and M >= 256 and N >= 256:
