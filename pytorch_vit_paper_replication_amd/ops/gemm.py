@@ -160,18 +160,19 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
 # best beside the dgrad chain, scripts/gpu_wgs_ab.sh in round 2)
 _WGRAD_WGS = 256
 _WGRAD_WGS_NARROW = 144
+OVERLAPPED = False  # set by ParamStore.on_side while it launches side-stream weight gradients
 
 
 def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
     """Token splits of a weight-gradient GEMM (each split accumulates into dW with f32 atomics).
     256x256 ping-pong tiles (12): one resident workgroup per CU, so fill the 256 CUs once, except
-    for the narrow weights of a 768-wide model (their 9-36 tiles would take 7-28 splits): ~144
-    workgroups there, leaving CUs to the dgrads they overlap with on the main stream (ViT-B/16 b256
-    +1.0 %; ViT-L/16 and ViT-H/14 lose 1 % with it; profiles/r5/wgrad_width/);
-    128x128 tiles (0): about 1024 workgroups."""
+    for the narrow weights of a 768-wide model (their 9-36 tiles would take 7-28 splits) while they
+    run on the side stream (OVERLAPPED): ~144 workgroups there, leaving CUs to the dgrads they
+    overlap with on the main stream (ViT-B/16 b256 +0.8-1.0 %; ViT-L/16 and ViT-H/14 lose 1 % with
+    it; profiles/r5/wgrad_width/); 128x128 tiles (0): about 1024 workgroups."""
     if tile == 12:
         tiles = math.ceil(N / 256) * math.ceil(K / 256)
-        wgs = _WGRAD_WGS_NARROW if min(N, K) <= 768 else _WGRAD_WGS
+        wgs = _WGRAD_WGS_NARROW if OVERLAPPED and min(N, K) <= 768 else _WGRAD_WGS
         return max(1, min(wgs // tiles, max(1, T // 256)))
     tiles = math.ceil(N / 128) * math.ceil(K / 128)
     target = 1024

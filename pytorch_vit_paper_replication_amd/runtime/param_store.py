@@ -303,10 +303,16 @@ class ParamStore:
         if side is None:
             fn()
             return
+        from ..ops import gemm as _gemm  # (ops imports the runtime: resolved at call time)
+
         main = torch.cuda.current_stream(self.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            fn()
+            prev, _gemm.OVERLAPPED = _gemm.OVERLAPPED, True  # split widths for work beside the main stream
+            try:
+                fn()
+            finally:
+                _gemm.OVERLAPPED = prev
         done = None
         if SIDE_WINDOW > 0 or SIDE_HOLD_BYTES > 0:
             done = torch.cuda.Event()
