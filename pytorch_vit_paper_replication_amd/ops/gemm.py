@@ -34,7 +34,7 @@ FORCE_TILE: Optional[int] = None
 Drop = Optional[Tuple[torch.Tensor, int, float]]  # (int64 seed tensor on device, site offset, p)
 
 
-def _tile(M: int, N: int, K: int, kind: str, gelu: bool = False, dgelu: bool = False) -> int:
+def _tile(M: int, N: int, K: int, kind: str) -> int:
     """Tile config per GEMM kind (measured on MI355X, scripts/bench_kernels.py, profiles/):
     k-contiguous forward/dgrad at ViT sizes -> 256x256 8-wave ping-pong, persistent (13) when there
     are at least four output tiles per CU, one tile per workgroup (12) otherwise (K % 64 != 0: the
@@ -127,7 +127,7 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
         ext.splitk_epilogue(ws, nsplit, out, bias, resid, epi == EPI_GELU)
         return out
     _gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
-          row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, tile=_tile(T, N, K, "fwd", epi == EPI_GELU))
+          row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, tile=_tile(T, N, K, "fwd"))
     return out
 
 
@@ -147,7 +147,7 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
         raise ValueError("colsum is fused only into the GELU-backward epilogue")
     if wt is not None and N % 64 == 0:
         _gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t", dgelu=dgelu_aux is not None), colsum=colsum,
+              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t"), colsum=colsum,
               tail_limit=DGRAD_TAIL_UNITS)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,

@@ -17,8 +17,8 @@ T_B16, T_L16 = 50432, 128 * 577
 
 def test_persistent_kernel_for_short_k_with_four_tiles_per_cu():
     assert G._tile(T_B16, 2304, 768, "fwd") == 13          # qkv forward
-    assert G._tile(T_B16, 3072, 768, "fwd", gelu=True) == 13  # fc1 forward
-    assert G._tile(T_B16, 3072, 768, "dgrad_t", dgelu=True) == 13  # fc2 dgrad (dGELU), since round 5
+    assert G._tile(T_B16, 3072, 768, "fwd") == 13          # fc1 forward (GELU epilogue)
+    assert G._tile(T_B16, 3072, 768, "dgrad_t") == 13      # fc2 dgrad (dGELU epilogue; since round 5)
     assert G._tile(T_B16, 768, 3072, "fwd") == 12          # fc2 forward: 2.3 tiles per CU
     assert G._tile(T_L16, 1024, 1024, "fwd") == 13          # ViT-L/16-384 out-projection
 
