@@ -60,6 +60,9 @@ def parse():
                    help="A/B: GB of weight-gradient inputs held at once (0 = until the end of backward)")
     p.add_argument("--no-gemm-tail", action="store_true",
                    help="A/B: no split-K tail on the last dispatch round of the one-tile-per-workgroup GEMMs")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="process-group transport for --gpus > 1: nccl = RCCL (production); gloo = test-only, every rank "
+                        "on the same GPU (LOCAL_RANK mod device count), to exercise this multi-rank path on a 1-GPU box")
     p.add_argument("--main-prio", type=int, default=-1,
                    help="run the step on a stream of this priority: -1 (default) puts the dgrad chain above the weight-gradient side stream; 0 = default stream")
     return p.parse_args()
@@ -154,7 +157,12 @@ def main():
             param_store.SIDE_WINDOW = args.side_window
         if args.side_hold_gb is not None:
             param_store.SIDE_HOLD_BYTES = int(args.side_hold_gb * 2**30)
-    rank, world, device = init_distributed()
+    if args.backend == "gloo":  # test transport: ranks share the GPU(s); gradients travel over gloo
+        rank, world, _ = init_distributed(backend="gloo")
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+        torch.cuda.set_device(device)
+    else:
+        rank, world, device = init_distributed()
     if args.no_gemm_tail and args.impl == "fused":
         from pytorch_vit_paper_replication_amd import _ext
 
@@ -283,8 +291,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if use_ddp:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if use_ddp:  # the slowest rank's time (CPU tensor on the gloo test transport)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == "nccl" else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item())
@@ -320,7 +328,8 @@ def main():
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,
                        "image_size": args.image_size, "parallelism": desc["parallelism"], "impl": args.impl + ("+hipgraph" if args.graph else ""),
-                       "grad_transport": (net.transport + f" {args.comm_dtype} wire") if use_ddp else "none",
+                       "grad_transport": (net.transport + f" {args.comm_dtype} wire" + (" (gloo test transport, shared GPU)"
+                                          if args.backend == "gloo" else "")) if use_ddp else "none",
                        "optimizer": "none (inference: eval forward under inference_mode)" if args.infer else
                        "Adam(wd=0.03 decay group) + clip 1.0 + warmup/linear-decay LR",
                        "dropout": "off (eval)" if args.infer else "0.1 (mlp, embedding)",

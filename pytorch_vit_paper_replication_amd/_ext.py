@@ -95,7 +95,15 @@ def deterministic() -> bool:
     """Deterministic reductions on the fused path (``set_deterministic`` / ``PVR_DETERMINISTIC=1`` /
     ``torch.use_deterministic_algorithms(True)``): every bias / LayerNorm-parameter gradient and the
     weight gradients are reduced in a fixed order, so a training step produces the same bits on every
-    run. Off by default: the float-atomic reductions are order-dependent in the last bits."""
+    run. Off by default: the float-atomic reductions are order-dependent in the last bits.
+
+    Not covered: the attention backward at sequence lengths with several 256-key blocks that take
+    neither its last-key nor its tail-split slab path (e.g. N = 677) still sums dQ with float atomics
+    (the extension warns once when deterministic mode meets such a shape). Every shape of the
+    BASELINE models (N = 197, 257, 577) is covered.
+
+    Each fused backward entry point calls this, so the native flag follows
+    ``torch.use_deterministic_algorithms`` from the first backward kernel of a step on."""
     m = _C if _TRIED else load()
     on = torch.are_deterministic_algorithms_enabled() or _DETERMINISTIC_ENV
     if m is not None and bool(m.deterministic()) != on:

@@ -984,6 +984,11 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   }
   const int old_db = old_part.defined() ? 1 : 0;
   if (pvr_attn_bwd_needs_dq_acc((int)N, (int)dh, old_db, has_drop)) {
+    // several key blocks per head and neither the lastkey nor the tail-split slab path (e.g. N = 677):
+    // dQ is summed with f32 atomics, which deterministic mode does not replace for this shape
+    if (g_deterministic)
+      TORCH_WARN_ONCE("deterministic mode: the attention backward at N = ", N,
+                      " accumulates dQ with float atomics (several key blocks, no slab path); dQ is not bitwise repeatable");
     dq_acc = dq_workspace(B * N * D, qkv.options());
     dq_rezero = dq_acc.defined() ? 1 : 0;
     if (!dq_acc.defined()) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));

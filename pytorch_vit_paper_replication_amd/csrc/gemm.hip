@@ -47,6 +47,12 @@ PVR_DEV void stamp(const GemmParams& p, int slot) {
 
 constexpr int TK = 64;  // K depth of one LDS stage
 
+// Ping-pong K loops: read the next K-tile's A0 first-k-step fragments in the read-free (1,0) phase
+// (A/B switch while it is measured; 0 = the round-5 phase reads 12 / 4 / 8 / 0)
+#ifndef PVR_PP_PRE
+#define PVR_PP_PRE 1
+#endif
+
 PVR_DEV int swz_k(int row) { return (row >> 1) & 7; }                                // 128-B rows
 PVR_DEV int swz_mn(int row) { return ((row & 3) | (((row >> 3) & 1) << 2)) << 1; }  // 16-B chunk XOR
 // 16-B chunk XOR of the fp8 mn images' 128-B k-rows: the 16 rows a 32-lane half reads with
@@ -829,10 +835,14 @@ struct PpStamps {
   }
 };
 
-template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool SWAP, int ES = 2, int FA = 0, int FB = 0>
-PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, __amdgpu_buffer_rsrc_t ars,
-                      __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda, int64_t ldb,
-                      int t_issue, int nk, int wave, int lane, int wm, int wn, PpStamps& pst) {
+// PR (bf16 k-contiguous A only, see PVR_PP_PRE): 1 = this (0,0) phase takes A0's first k-step
+// fragments from `pre` (read one phase earlier) and reads only the second; 2 = this (1,0) phase
+// reads the NEXT K-tile's A0 first-k-step fragments from `nbuf` into `pre`.
+template <int QM, int QN, int RD_A, int RD_B, int KIND, bool AK, bool BKC, bool SWAP, int ES = 2, int FA = 0, int FB = 0, int PR = 0>
+PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], v8s (&pre)[4], const char* buf, const char* nbuf,
+                      __amdgpu_buffer_rsrc_t ars, __amdgpu_buffer_rsrc_t brs, __amdgpu_buffer_rsrc_t nul, char* smem, int64_t lda,
+                      int64_t ldb, int t_issue, int nk, int wave, int lane, int wm, int wn, PpStamps& pst) {
+  static_assert(PR == 0 || (AK && ES == 2), "A0 read-ahead: bf16 k-contiguous A only");
   constexpr int PT_ = QM == 0 ? QN : 3 - QN;  // phase type: (0,0) (0,1) (1,1) (1,0)
   pst.type_mark(PT_, 0);
 
@@ -852,11 +862,17 @@ PVR_DEV void pp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], con
       for (int ks = 0; ks < 2; ++ks) {
         if constexpr (ES == 1)
           af[ii][ks] = frag_fp8(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+        else if constexpr (AK && PR == 1)
+          af[ii][ks] = ks == 0 ? pre[ii] : read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
         else if constexpr (AK)
           af[ii][ks] = read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
         else
           read_frag_mn_async<128>(buf + QM * 16384, wm * 64 + 16 * ii, ks, lane, alo[ii][ks], ahi[ii][ks]);
       }
+  }
+  if constexpr (PR == 2) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) pre[ii] = read_frag<256, true>(nbuf, wm * 128 + 16 * ii, 0, lane);
   }
   if constexpr (RD_B && MN8B) {
 #pragma unroll
@@ -1535,13 +1551,21 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
   const uint64_t pst0 = pst.last;
 #endif
 
+  // A0 read-ahead (PVR_PP_PRE): K-tile 0's first k-step A0 fragments now (landed: vmcnt(8) above)
+  constexpr int PRE = (PVR_PP_PRE && AK && ES == 2) ? 1 : 0;
+  v8s pre[4];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) pre[ii] = read_frag<256, true>(smem, wm * 128 + 16 * ii, 0, lane);
+  }
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * PP_BUF;
+    const char* nbuf = smem + ((t + 1) & 1) * PP_BUF;  // (the last K-tile's read-ahead reads dead data)
     // phase P = 4t + ph issues half-tile P + 6 = 4(t+1) + ph + 2
-    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn, pst);
-    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn, pst);
-    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn, pst);
-    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, buf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn, pst);
+    pp_phase<0, 0, 1, 1, 2, AK, BKC, SWAP, ES, FA, FB, PRE>(acc, af, bf, pre, buf, nbuf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn, pst);
+    pp_phase<0, 1, 0, 1, 3, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, pre, buf, nbuf, ars, brs, nul, smem, p.lda, p.ldb, t + 1, nk, wave, lane, wm, wn, pst);
+    pp_phase<1, 1, 1, 0, 0, AK, BKC, SWAP, ES, FA, FB>(acc, af, bf, pre, buf, nbuf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn, pst);
+    pp_phase<1, 0, 0, 0, 1, AK, BKC, SWAP, ES, FA, FB, 2 * PRE>(acc, af, bf, pre, buf, nbuf, ars, brs, nul, smem, p.lda, p.ldb, t + 2, nk, wave, lane, wm, wn, pst);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // null stages too: no LDS-DMA may outlive the workgroup
   if (wm == 0) pp_barrier();  // equal barrier counts for both groups
@@ -1700,17 +1724,26 @@ PVR_DEV PppTile ppp_tile(const GemmParams& p, int v, int ntiles, int ntn) {
 
 // Phase of the continuous stream: reads / MFMAs of K-tile (current buffer) and the DMA of global
 // half-tile `h_issue`, which belongs to this tile (K-tile kt_i) or to the next one.
-template <int QM, int QN, int RD_A, int RD_B, bool SWAP, int VM = 8, int ES = 2, int FA = 0, int FB = 0>
-PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], const char* buf, char* smem, const PppTile& cur,
-                       const PppTile& nxt, int G_issue, int kind, int tile_first_G, int nk, const GemmParams& p, int wave, int lane,
-                       int wm, int wn) {
+// PR: the A0 read-ahead of pp_phase (bf16 only); the next K-tile's buffer is the other one, also
+// across a tile boundary (the K-tile stream is continuous).
+template <int QM, int QN, int RD_A, int RD_B, bool SWAP, int VM = 8, int ES = 2, int FA = 0, int FB = 0, int PR = 0>
+PVR_DEV void ppp_phase(v4f (&acc)[8][4], v8s (&af)[4][2], v8s (&bf)[2][2][2], v8s (&pre)[4], const char* buf, char* smem,
+                       const PppTile& cur, const PppTile& nxt, int G_issue, int kind, int tile_first_G, int nk, const GemmParams& p,
+                       int wave, int lane, int wm, int wn) {
+  static_assert(PR == 0 || ES == 2, "A0 read-ahead: bf16 only");
   if constexpr (RD_A) {
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
         af[ii][ks] = ES == 1 ? frag_fp8(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane)
-                             : read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+                     : (PR == 1 && ks == 0) ? pre[ii]
+                                            : read_frag<256, true>(buf, wm * 128 + QM * 64 + 16 * ii, ks, lane);
+  }
+  if constexpr (PR == 2) {
+    const char* nbuf = smem + (((buf - smem) / PP_BUF) ^ 1) * PP_BUF;
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) pre[ii] = read_frag<256, true>(nbuf, wm * 128 + 16 * ii, 0, lane);
   }
   if constexpr (RD_B) {
 #pragma unroll
@@ -1791,6 +1824,12 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
   ppp_issue_kind<ES>(1, cur.ars, cur.brs, smem + PP_BUF, p.lda, p.ldb, 128, wave, lane);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   pp_barrier();
+  constexpr int PRE = (PVR_PP_PRE && ES == 2) ? 1 : 0;
+  v8s pre[4];  // A0 read-ahead: live across each epilogue into the next tile's first phase
+  if constexpr (PRE) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) pre[ii] = read_frag<256, true>(smem, wm * 128 + 16 * ii, 0, lane);
+  }
 
   // diagnostic stamps (p.dbg set, scripts/gemm_stamps.py --persistent): per workgroup, cycles in the
   // K loops and in the epilogues summed over its tiles, the whole kernel, and its tile count
@@ -1815,20 +1854,20 @@ __global__ void __launch_bounds__(512, 2) gemm_ppp_kernel(GemmParams p) {
         // the four half-tiles this K-tile waits for, so every wait leaves them in flight (counted);
         // the first wait for a half-tile issued after them (next K-tile) retires them
         const char* buf = smem + (G0 & 1) * PP_BUF;
-        ppp_phase<0, 0, 1, 1, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 2, G0, nk, p, wave, lane, wm, wn);
-        ppp_phase<0, 1, 0, 1, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 1, 3, G0, nk, p, wave, lane, wm, wn);
-        ppp_phase<1, 1, 1, 0, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 0, G0, nk, p, wave, lane, wm, wn);
-        ppp_phase<1, 0, 0, 0, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G0 + 2, 1, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<0, 0, 1, 1, SWAP, 8 + INFL, ES, FA, FB, PRE>(acc, af, bf, pre, buf, smem, cur, nxt, G0 + 1, 2, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<0, 1, 0, 1, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, pre, buf, smem, cur, nxt, G0 + 1, 3, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<1, 1, 1, 0, SWAP, 8 + INFL, ES, FA, FB>(acc, af, bf, pre, buf, smem, cur, nxt, G0 + 2, 0, G0, nk, p, wave, lane, wm, wn);
+        ppp_phase<1, 0, 0, 0, SWAP, 8 + INFL, ES, FA, FB, 2 * PRE>(acc, af, bf, pre, buf, smem, cur, nxt, G0 + 2, 1, G0, nk, p, wave, lane, wm, wn);
         kt = 1;
       }
     }
     for (; kt < nk; ++kt) {
       const int G = G0 + kt;
       const char* buf = smem + (G & 1) * PP_BUF;
-      ppp_phase<0, 0, 1, 1, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 1, 2, G0, nk, p, wave, lane, wm, wn);
-      ppp_phase<0, 1, 0, 1, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 1, 3, G0, nk, p, wave, lane, wm, wn);
-      ppp_phase<1, 1, 1, 0, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 2, 0, G0, nk, p, wave, lane, wm, wn);
-      ppp_phase<1, 0, 0, 0, SWAP, 8, ES, FA, FB>(acc, af, bf, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<0, 0, 1, 1, SWAP, 8, ES, FA, FB, PRE>(acc, af, bf, pre, buf, smem, cur, nxt, G + 1, 2, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<0, 1, 0, 1, SWAP, 8, ES, FA, FB>(acc, af, bf, pre, buf, smem, cur, nxt, G + 1, 3, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<1, 1, 1, 0, SWAP, 8, ES, FA, FB>(acc, af, bf, pre, buf, smem, cur, nxt, G + 2, 0, G0, nk, p, wave, lane, wm, wn);
+      ppp_phase<1, 0, 0, 0, SWAP, 8, ES, FA, FB, 2 * PRE>(acc, af, bf, pre, buf, smem, cur, nxt, G + 2, 1, G0, nk, p, wave, lane, wm, wn);
     }
     if (wm == 0) pp_barrier();  // re-align the groups for the epilogue
     uint64_t ts_b = 0;
@@ -1943,11 +1982,25 @@ extern "C" int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_
 static int g_fp8_persistent = 1;
 extern "C" void pvr_set_fp8_persistent(int mode) { g_fp8_persistent = mode ? 1 : 0; }
 
+extern "C" int pvr_gemm_ws_ok(const pvr::GemmParams* pp, int cus);
+extern "C" hipError_t pvr_gemm_ws(const pvr::GemmParams* pp, int cus, hipStream_t s);
+
+// 1 if tile config 15 (the wave-specialized kernel, gemm_ws.hip) runs this GEMM as given
+extern "C" int pvr_gemm_ws_takes(const pvr::GemmParams* pp) { return pvr_gemm_ws_ok(pp, pvr::device_cus()); }
+
 // Host entry. Returns hipSuccess, or hipErrorInvalidValue for an unsupported layout/epilogue pair.
 extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
   using namespace pvr;
   const GemmParams& p = *pp;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return hipSuccess;
+  // tile 15: wave-specialized persistent kernel (epilogue waves beside the MFMA waves); shapes it
+  // does not take fall through to the 256x256 ping-pong
+  if (p.tile_cfg == 15) {
+    if (pvr_gemm_ws_ok(pp, device_cus())) return pvr_gemm_ws(pp, device_cus(), s);
+    GemmParams q = p;
+    q.tile_cfg = 13;
+    return pvr_gemm(&q, s);
+  }
   const bool ak = p.a_kcontig, bk = p.b_kcontig;
   if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad / wgrad e5m2 x e4m3)
     const int f = p.fmt_a * 2 + p.fmt_b;

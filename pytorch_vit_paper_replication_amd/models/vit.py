@@ -219,13 +219,23 @@ class ViT(nn.Module):
         P = c["patch_size"]
         return x.shape[2] == x.shape[3] == c["image_size"] and x.shape[2] % P == 0
 
+    @staticmethod
+    def _rank_offset() -> int:
+        # per-rank offset of the dropout counter: DDP ranks draw different masks from one base
+        dist = torch.distributed
+        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        return rank * 40503
+
     def _dropout_seed(self, device) -> torch.Tensor:
         rng = getattr(self, "_pvr_rng", None)
-        if rng is None or rng.device != device:
+        if rng is not None and rng.device != device:
+            with torch.inference_mode(False):  # e.g. restored on the CPU before .cuda(): keep the counter
+                rng = rng.to(device)
+            object.__setattr__(self, "_pvr_rng", rng)
+        if rng is None:
             with torch.inference_mode(False):
                 base = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
-                rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
-                rng = torch.tensor([base * 2654435761 + rank * 40503], dtype=torch.int64, device=device)
+                rng = torch.tensor([base * 2654435761 + self._rank_offset()], dtype=torch.int64, device=device)
             object.__setattr__(self, "_pvr_rng", rng)
         seed = torch.empty_like(rng)
         _ext.ext().rng_next(rng, seed)  # seed = rng; rng += 1 (one device kernel, graph-replay safe)
@@ -324,8 +334,12 @@ class ViT(nn.Module):
             return None
         st = getattr(self, "_fp8", None)
         if st is None or st.device != device:
+            old_sd = st.state_dict() if st is not None else getattr(self, "_fp8_pending", None)
             st = F8.Fp8State(c["num_transformer_layer"], device, history=cfg[0], margin=cfg[1], dgrad=cfg[2], wgrad=cfg[3])
+            if old_sd is not None:  # restored (or built) on another device: carry the scaling state over
+                st.load_state_dict(old_sd)
             object.__setattr__(self, "_fp8", st)
+            object.__setattr__(self, "_fp8_pending", None)
         st.dgrad = cfg[2]
         st.wgrad = cfg[3] and cfg[2]
         return st
@@ -338,7 +352,9 @@ class ViT(nn.Module):
         out = {}
         rng = getattr(self, "_pvr_rng", None)
         if rng is not None:
-            out["dropout_rng"] = rng.detach().cpu().clone()
+            # rank-free: every DDP rank re-adds its own offset on load (rank 0 writes the checkpoint)
+            out["dropout_rng"] = rng.detach().cpu().clone() - self._rank_offset()
+            out["dropout_rng_rank_free"] = torch.ones(1, dtype=torch.int64)
         st = getattr(self, "_fp8", None)
         if st is not None:
             out["fp8"] = st.state_dict()
@@ -349,11 +365,19 @@ class ViT(nn.Module):
         parameters' device). The fp8 state needs ``enable_fp8`` with the same history first."""
         dev = torch.device(device) if device is not None else next(self.parameters()).device
         if "dropout_rng" in sd:
-            object.__setattr__(self, "_pvr_rng", sd["dropout_rng"].to(device=dev, dtype=torch.int64).clone())
+            rng = sd["dropout_rng"].to(dtype=torch.int64).clone()
+            if "dropout_rng_rank_free" in sd:
+                rng += self._rank_offset()
+            object.__setattr__(self, "_pvr_rng", rng.to(dev))  # moved to the forward's device on first use
         if "fp8" in sd:
             cfg = getattr(self, "_fp8_cfg", None)
             if cfg is None:
                 raise RuntimeError("checkpoint holds fp8 scaling state: call enable_fp8(...) before loading it")
+            if dev.type != "cuda":
+                # the fused path builds its fp8 state on the forward's device: apply it there
+                object.__setattr__(self, "_fp8", None)
+                object.__setattr__(self, "_fp8_pending", sd["fp8"])
+                return
             from ..ops import fp8 as F8
 
             st = getattr(self, "_fp8", None)

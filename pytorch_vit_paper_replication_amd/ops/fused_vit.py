@@ -233,6 +233,7 @@ class EncoderBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx2):
         ext = _ext.ext()
+        _ext.deterministic()  # native flag follows torch.use_deterministic_algorithms from this kernel on
         x, xn1, mean1, rstd1, qkv, o, lse, x1, xn2, mean2, rstd2, u, h = ctx.saved_tensors
         B, N, H, scale, store, drop1, drop2, dropa, params = ctx.meta
         ln1w, ln1b, wqkv, bqkv, wo, bo, ln2w, ln2b, w1, b1, w2, b2 = params
@@ -448,6 +449,7 @@ class HeadFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits):
         ext = _ext.ext()
+        _ext.deterministic()  # native flag follows torch.use_deterministic_algorithms from this kernel on
         xhat, rstd = ctx.saved_tensors
         B, N, store, ln_w, ln_b, head_w, head_b = ctx.meta
         g = store.grad_dest
@@ -525,6 +527,7 @@ class TokenLayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         ext = _ext.ext()
+        _ext.deterministic()  # native flag follows torch.use_deterministic_algorithms from this kernel on
         tokens, mean, rstd = ctx.saved_tensors
         store, w, b = ctx.meta
         T, D = tokens.shape

@@ -68,6 +68,24 @@ def _tile(M: int, N: int, K: int, kind: str) -> int:
     return 0
 
 
+# Wave-specialized persistent kernel (tile 15, csrc/gemm_ws.hip: 8 MFMA waves + 8 epilogue waves per
+# CU, the epilogue of tile t - 2 running beside the MFMAs of tile t) for these GEMM kinds of the
+# large-token path: "gelu" (fc1 forward: GELU + dropout + derivative), "dgelu" (fc2 dgrad: x dGELU
+# factor + bias-gradient column sums), "bias" (qkv forward), "resid" (out-proj / fc2 forward: dropout +
+# residual), "dgrad" (plain dgrads). PVR_GEMM_WS=kind,kind overrides (empty: none).
+import os as _os
+
+WS_KINDS = set(k for k in _os.environ.get("PVR_GEMM_WS", "").split(",") if k)
+
+
+def _ws_tile(kind: str, t: int) -> int:
+    """Tile 15 for a GEMM kind routed to the wave-specialized kernel, where the default choice is a
+    256x256 ping-pong one (12 / 13); the kernel itself falls back to tile 13 for shapes it cannot take."""
+    if FORCE_TILE is None and kind in WS_KINDS and t in (12, 13):
+        return 15
+    return t
+
+
 def _small_splitk(T: int, N: int, K: int) -> int:
     """K splits for a forward GEMM on 256x256 tiles (T >= 2048) with fewer than 128 output tiles
     (0: do not split). Each split keeps at least two 64-deep K-tiles; the splits aim at ~256
@@ -126,8 +144,10 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = 
         ext.gemm(x, True, w, True, ws, T, N, K, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0, None, 0, 0.0, ksplit, 14)
         ext.splitk_epilogue(ws, nsplit, out, bias, resid, epi == EPI_GELU)
         return out
+    kind = "gelu" if epi == EPI_GELU else "resid" if resid is not None else "bias"
     _gemm(x, True, w, True, out, T, N, K, epi, bias, resid, addend, addend_period, gelu_aux,
-          row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0, tile=_tile(T, N, K, "fwd"))
+          row_remap[0], row_remap[1], row_remap[2], seed, soff, p, 0,
+          tile=_ws_tile(kind, _tile(T, N, K, "fwd")) if addend is None and row_remap[0] == 0 else _tile(T, N, K, "fwd"))
     return out
 
 
@@ -147,8 +167,8 @@ def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, *, dgelu_aux: Optional[torch
         raise ValueError("colsum is fused only into the GELU-backward epilogue")
     if wt is not None and N % 64 == 0:
         _gemm(dy, True, wt, True, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
-              seed, soff, p, 0, tile=_tile(T, K, N, "dgrad_t"), colsum=colsum,
-              tail_limit=DGRAD_TAIL_UNITS)
+              seed, soff, p, 0, tile=_ws_tile("dgelu" if dgelu_aux is not None else "dgrad", _tile(T, K, N, "dgrad_t")),
+              colsum=colsum, tail_limit=DGRAD_TAIL_UNITS)
     else:
         _ext.ext().gemm(dy, True, w, False, out, T, K, N, epi, None, None, None, 0, dgelu_aux, 0, 0, 0,
                         seed, soff, p, 0, _tile(T, K, N, "dgrad") if tile is None else tile, colsum=colsum,
@@ -225,6 +245,9 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.
                  None, 0, 0.0, ksplit, 14)
         ext.splitk_reduce(ws, nsplit, out, True)
         return out
+    if nsplit > 1 and _ext.deterministic():
+        # the f32-atomic epilogue below adds every token split into the same element: one split only
+        ksplit, nsplit = math.ceil(T / 64) * 64, 1
     if narrow:
         tmp = torch.zeros(N, K, dtype=torch.float32, device=dy.device)
         linear_wgrad(dy, x, tmp)

@@ -144,7 +144,7 @@ def check_gemm_gelu_drop_paths(M=3000, N=768, p=0.1):
     masks, names = [], []
     for K in (256, 1024):
         x, w = bf(torch.ones(M, K, device=DEV)), bf(torch.full((N, K), 1.0 / K, device=DEV))
-        for t in (12, 13):
+        for t in (12, 13, 15):
             with tile(t):
                 u = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
                 h = G.linear_fwd(x, w, b, gelu_aux=u, drop=(seed, 11 << 32, p))
@@ -153,7 +153,7 @@ def check_gemm_gelu_drop_paths(M=3000, N=768, p=0.1):
     differs = sum(int((mk != masks[0]).sum()) for mk in masks[1:])
     rate = masks[0].float().mean().item()
     m = {"mask_differs": float(differs), "rate_dev": abs(rate - p)}
-    return (f"gemm_gelu drop mask: K 256 vs K 1024, tiles 12 / 13 (rate {rate:.4f})", m,
+    return (f"gemm_gelu drop mask: K 256 vs K 1024, tiles 12 / 13 / 15 (rate {rate:.4f})", m,
             {"mask_differs": 0, "rate_dev": rate_limit(p, M * N)})
 
 
@@ -1522,6 +1522,18 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_dropout(3000, 768, 1024, 0.1, 12),  # one tile per workgroup, 16 K-tiles
         lambda: check_gemm_gelu_drop_paths(),
         lambda: check_gemm_dgelu_tiles(),
+        # wave-specialized persistent kernel (tile 15): M / N tails, K = 256 (8 K-steps), several tiles
+        # per workgroup (the epilogue of tile t - 2 beside tile t, the drain of the last two)
+        lambda: check_gemm_fwd(3152, 768, 768, 15),
+        lambda: check_gemm_fwd(197 * 3, 2304, 768, 15, True, True),
+        lambda: check_gemm_fwd(2000, 1000, 256, 15, True, True),
+        lambda: check_gemm_fwd(70000, 768, 512, 15, True, True),
+        lambda: check_gemm_gelu(6000, 3072, 768, 15),
+        lambda: check_gemm_gelu(50432, 3072, 768, 15),
+        lambda: check_gemm_gelu_dropout(5000, 3072, 768, tiles=(13, 15)),
+        lambda: check_gemm_dropout(3000, 768, 1024, 0.1, 15),
+        lambda: check_gemm_dgelu(4096, 768, 3072, True, 15),
+        lambda: check_gemm_dgelu(50432, 768, 3072, True, 15),
         lambda: check_gemm_fwd(300, 256, 64, 12, True, False),
         # split-K tail of the last dispatch round (ViT-B/16 b256 shapes: 591 tiles -> 2 rounds + 79
         # tiles as 3 K-parts; 2364 tiles -> 9 rounds + 60 tiles as 4 K-parts; 588 patch-embed tiles)

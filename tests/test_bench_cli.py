@@ -63,3 +63,41 @@ def test_world1_forced_ddp_and_inference():
     assert _desc(["--force-ddp"], 1)["ddp"]
     d = _desc(["--infer"], 1)
     assert d["metric"] == "inference images/sec (whole node) ViT-B/16 224px bf16"
+
+
+def _run_bench(argv, timeout=420):
+    import subprocess
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)  # the top-level command relaunches itself under torch.distributed.run
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], cwd=ROOT, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout
+
+
+def _json_lines(out):
+    import json
+
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_bench_distributed_branch_two_ranks():
+    """The driver's multi-GPU command path end to end with 2 ranks on one GPU: `bench.py --gpus 2`
+    relaunches itself under torch.distributed.run (127.0.0.1 rendezvous), both ranks build the model,
+    DDP broadcasts rank 0's parameters and all-reduces the bucketed gradients (gloo test transport:
+    RCCL needs one GPU per rank), the timed region's MAX over ranks, rank 0 prints exactly ONE JSON
+    line, and every rank destroys its process group (clean exit)."""
+    out = _run_bench(["--gpus", "2", "--backend", "gloo", "--batch", "16", "--steps", "2", "--warmup", "1"])
+    lines = _json_lines(out)
+    assert len(lines) == 1, out
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["steps"] == 2 and j["warmup"] == 1
+    assert j["config"]["global_batch"] == 2 * j["config"]["per_gpu_batch"] == 32
+    assert j["config"]["parallelism"] == "dp2" and "gloo" in j["config"]["grad_transport"]
+    assert j["metric"] == "images/sec (whole node) ViT-B/16 224px bf16 at 1/2/4/8 MI355X"
+    assert j["value"] > 0 and abs(j["value"] - 32 * 2 / (j["ms_per_step"] * 2 / 1000.0)) < 0.02 * j["value"]
