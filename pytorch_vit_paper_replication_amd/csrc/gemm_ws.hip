@@ -11,29 +11,40 @@
 //   * 8 MFMA waves (two per SIMD, ping-ponging a barrier apart as in gemm.hip) compute 256 x 128
 //     output tiles (each wave 64 x 64: 4 x 4 v_mfma_f32_16x16x32_bf16 fragments) from a 6-slot ring
 //     of 32-deep K-steps that LDS-DMA (buffer_load ... lds) fills 4 steps ahead, continuously across
-//     the workgroup's tiles. Their accumulators start at the bias; at a tile end they store the tile
-//     as bf16 u = A.B^T + bias (64 KiB, register order) to a per-workgroup scratch slot in L2 and go
-//     straight on with the next tile.
-//   * 8 epilogue waves (two per SIMD) turn tile t - 2's u into the outputs while the MFMA waves run
-//     tile t: GELU + dropout + GELU-derivative (fc1 forward), x dGELU-factor + column sums (fc2
-//     dgrad), or dropout + residual. Their VALU work and HBM stores overlap the matrix-core work on
-//     the same SIMDs (an MFMA blocks its SIMD's vector issue for 8 of its 16 cycles).
+//     the workgroup's tiles. At a tile end they hand the accumulators to the epilogue waves through
+//     LDS (the two ring slots just consumed + a 16 KiB spare region = 64 KiB) and go on with the next
+//     tile. They issue no global store: their vmcnt waits count LDS-DMA only.
+//   * 8 epilogue waves (two per SIMD) hold the handed-off tile in registers and turn it into the
+//     outputs while the MFMA waves run the next tile: bias + GELU + dropout + GELU-derivative (fc1
+//     forward), x dGELU-factor + bias-gradient column sums (fc2 dgrad), bias + dropout + residual.
+//     Their VALU work and HBM traffic overlap the matrix-core work on the same SIMDs (an MFMA blocks
+//     its SIMD's vector issue for 8 of its 16 cycles).
 //
 // Both roles execute the same s_barrier sequence (every barrier counts all 16 waves): the epilogue
-// waves spread a tile's work over the barrier intervals of the MFMA waves' next-next tile, so the
-// protocol needs no flags. Register budget: 4 waves per SIMD, <= 128 VGPRs each (__launch_bounds__).
-// LDS: 6 K-step slots x 24 KiB + bias staging + column-sum exchange.
+// waves spread a tile's 8 work units over the barrier intervals of the next tile, so the protocol
+// needs no flags. Register budget: 4 waves per SIMD, <= 128 VGPRs each (__launch_bounds__).
+// An earlier form of this kernel handed u over through an L2 scratch buffer: its stores sat in the
+// MFMA waves' in-order vmcnt queue and every CU's burst at the tile end stalled their next K-steps
+// (+35 % on the qkv forward; profiles/r6/README.md).
 //
-// Numerics: u is rounded to bf16 before the elementwise epilogue, as PyTorch's autocast Linear
-// output is (reference models/vit.py:118-126 under autocast); the epilogue math is gemm.hip's.
+// Numerics: the bf16 hand-off rounds A.B^T to bf16 before the bias and the elementwise epilogue, as
+// PyTorch's autocast Linear output is (reference models/vit.py:118-126 under autocast); the dGELU
+// hand-off stays fp32 (two rounds), so the bias-gradient column sums keep the fp32 accumulator.
 // Reference: /root/reference/models/vit.py:118-126 (MLP block), :166-169; SURVEY.md K9, K10, K11.
 #include "common.h"
 #include "gemm_params.h"
+#include <type_traits>
 
 namespace pvr {
 namespace {
 
 constexpr int EPI_BF16_ = 0, EPI_GELU_ = 1, EPI_DGELU_ = 2;  // = GemmEpi of gemm.hip
+
+// diagnostic ablations (timing only, wrong results): 1 = the epilogue waves only keep the barrier
+// count, 3 = and no hand-off (the MFMA waves alone)
+#ifndef PVR_WS_ABL
+#define PVR_WS_ABL 0
+#endif
 
 constexpr int WS_BM = 256, WS_BN = 128;       // output tile (rows of A x rows of B)
 constexpr int WS_A = WS_BM * 64;              // A image of one K-step: [256 rows][32 k] bf16 = 16 KiB
@@ -43,14 +54,21 @@ constexpr int WS_NSLOT = 6;                   // K-step ring
 constexpr int WS_AHEAD = 4;                   // K-steps of LDS-DMA in flight ahead of the reads
 constexpr int WS_DMA = 3;                     // DMA instructions per MFMA wave per K-step
 constexpr int WS_VM = (WS_AHEAD - 1) * WS_DMA;  // vmcnt that retires the next K-step
-constexpr int WS_USTORES = 8;                 // u stores per MFMA wave at a tile end
-constexpr int WS_BIAS_OFF = WS_NSLOT * WS_SLOT;           // 2 x 128 fp32 bias staging slots
-constexpr int WS_CS_OFF = WS_BIAS_OFF + 2 * WS_BN * 4;    // column-sum exchange [8 waves][64] fp32
-constexpr int WS_LDS = WS_CS_OFF + 8 * 64 * 4;
-constexpr int WS_U_BYTES = WS_BM * WS_BN * 2;  // one scratch slot (bf16 u of a tile)
-constexpr int WS_SC1 = 16;                    // buffer cache policy sc1: L2-served (no stale L1 line)
+constexpr int WS_SPARE = WS_NSLOT * WS_SLOT;  // 16 KiB: hand-off chunks 6, 7; column-sum exchange between hand-offs
+constexpr int WS_LDS = WS_SPARE + 16384;      // 160 KiB
+// hand-off: bf16 (one round, 8 KiB per MFMA wave) or fp32 for the dGELU epilogue (two rounds, one
+// wave group at a time, 16 KiB per wave)
+template <int EPI> constexpr bool ws_f32u() { return EPI == 2; }
 
 PVR_DEV int ws_swz(int row) { return (row >> 1) & 3; }  // 64-B rows: conflict-free ds_read_b128
+
+template <int I, int N, class F>
+PVR_DEV void ws_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    ws_static_for<I + 1, N>(f);
+  }
+}
 
 PVR_DEV void ws_barrier() {
   asm volatile("" ::: "memory");
@@ -123,11 +141,10 @@ PVR_DEV WsTile ws_tile(const GemmParams& p, int v) {
 }
 
 // One K-step of an MFMA wave (a barrier apart from its SIMD partner): read this step's fragments,
-// issue the DMA of step G + WS_AHEAD (this tile's or the next one's), retire step G + 1, MFMAs.
-// infl: the first K-steps after a tile end, whose counted wait leaves the WS_USTORES u stores (younger
-// than the DMAs it retires) in flight.
+// issue the DMA of step G + WS_AHEAD (this tile's or the next one's), retire step G + 1 (the MFMA
+// waves issue no other vector-memory operation, so the count is exact), MFMAs.
 PVR_DEV void ws_step(v4f (&acc)[4][4], char* smem, int G, int G0, int nk, const WsTile& cur, const WsTile& nxt,
-                     const WsDma& d, bool infl, int w, int lane, int wm, int wn) {
+                     const WsDma& d, int w, int lane, int wm, int wn) {
   const char* slot = smem + (G % WS_NSLOT) * WS_SLOT;
   v8s a[4], b[4];
 #pragma unroll
@@ -140,10 +157,7 @@ PVR_DEV void ws_step(v4f (&acc)[4][4], char* smem, int G, int G0, int nk, const 
     ws_issue(same ? cur.ars : nxt.ars, same ? cur.brs : nxt.brs, smem + (Gi % WS_NSLOT) * WS_SLOT, d,
              (same ? rel : rel - nk) * 64, w);
   }
-  if (infl)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WS_VM + WS_USTORES) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WS_VM) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WS_VM) : "memory");
   ws_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_setprio(1);
@@ -155,101 +169,163 @@ PVR_DEV void ws_step(v4f (&acc)[4][4], char* smem, int G, int G0, int nk, const 
   ws_barrier();
 }
 
-// ---------------------------------------------------------------- epilogue waves
-// Epilogue wave e processes MFMA wave e's 64 x 64 block of a tile: fragment rows i = 0..3, column
-// pairs jp = 0..1. Its u words come from the scratch in the MFMA lane order; one v_permlane16_swap
-// per word pair gives every lane 8 contiguous columns c0 = nb + 32 jp + {0, 16, 8, 24}[g] of row
-// mb + 16 i + li (the register-direct layout of gemm.hip's epilogue_direct), so every load / store
-// below is 16 B per lane.
+// ---------------------------------------------------------------- hand-off and epilogue waves
+// The 64 KiB hand-off area of the tile ending at K-step G0 - 1: 8 chunks of 8 KiB, chunks 0-2 in the
+// ring slot of K-step G0 - 2, 3-5 in that of G0 - 1 (both consumed: their next DMAs, of steps G0 + 4
+// and G0 + 5, are issued after the hand-off), 6-7 in the spare region.
+PVR_DEV char* ws_chunk(char* smem, int G0, int c) {
+  const int sa = (G0 + WS_NSLOT - 2) % WS_NSLOT, sb = (G0 + WS_NSLOT - 1) % WS_NSLOT;
+  return c < 3 ? smem + sa * WS_SLOT + c * 8192 : c < 6 ? smem + sb * WS_SLOT + (c - 3) * 8192 : smem + WS_SPARE + (c - 6) * 8192;
+}
+
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-struct WsEpi {
-  int mb, nb, e;                       // block origin, epilogue wave
-  uint32_t vc[2], vx[2];               // per-jp lane offsets in C and in the resid / aux tensor
-  __amdgpu_buffer_rsrc_t crs, xrs, srs;  // C, resid (BF16) or aux (GELU store / DGELU load), scratch
-  int ldx;
-  bool has_in;
-  v4u pu[2], px[2];                    // u / per-row input of units s and s + 1 (ring of 2, by unit & 1)
-  float cs[2][8];                      // column sums (DGELU)
+// A handed-off 64 x 64 block in register order: bf16: word group (2i + jp) = fragments (i, 2 jp),
+// (i, 2 jp + 1) packed (NU = 8); fp32: group (4i + j) = fragment (i, j) (NU = 16).
+template <int NU>
+struct WsBlock {
+  v4u q[NU];
 };
 
-// unit s = (fragment row s >> 1, column pair s & 1): its u words (scratch, MFMA lane order) and input
+// MFMA wave side: write the accumulators (register order, 16 B per lane and instruction)
+template <bool F32>
+PVR_DEV void ws_put(const v4f (&acc)[4][4], char* smem, int G0, int q, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const v4f a0 = acc[i][2 * jp], a1 = acc[i][2 * jp + 1];
+      if constexpr (F32) {  // 16 KiB per wave: chunks 2q, 2q + 1
+        const int o0 = (i * 4 + 2 * jp) * 1024, o1 = o0 + 1024;
+        *(__attribute__((address_space(3))) v4f*)(ws_chunk(smem, G0, 2 * q + (o0 >> 13)) + (o0 & 8191) + lane * 16) = a0;
+        *(__attribute__((address_space(3))) v4f*)(ws_chunk(smem, G0, 2 * q + (o1 >> 13)) + (o1 & 8191) + lane * 16) = a1;
+      } else {  // 8 KiB per wave: chunk q
+        const v4u o = {pack2bf(a0[0], a0[1]), pack2bf(a0[2], a0[3]), pack2bf(a1[0], a1[1]), pack2bf(a1[2], a1[3])};
+        *(__attribute__((address_space(3))) v4u*)(ws_chunk(smem, G0, q) + (i * 2 + jp) * 1024 + lane * 16) = o;
+      }
+    }
+}
+
+// epilogue wave side: the same words back, into registers
+template <bool F32, int NU>
+PVR_DEV void ws_get(WsBlock<NU>& B, char* smem, int G0, int q, int lane) {
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int o = u * 1024;
+    const char* base = F32 ? ws_chunk(smem, G0, 2 * q + (o >> 13)) + (o & 8191) : ws_chunk(smem, G0, q) + o;
+    B.q[u] = *(const __attribute__((address_space(3))) v4u*)(base + lane * 16);
+  }
+}
+
+struct WsEpi {
+  int mb, nb;                             // block origin (rows, columns)
+  uint32_t vc0, vc1, vx0, vx1;            // per-jp lane offsets in C and in the resid / aux tensor
+  __amdgpu_buffer_rsrc_t crs, xrs;        // C, resid (BF16) or aux (GELU store / DGELU load)
+  int ldc2, ldx2;                         // row strides in bytes
+  bool has_in;
+  v4u x[2];                               // per-row inputs of the next even / odd unit (two units ahead)
+  float bias[2][8];                       // this lane's 8 + 8 bias columns (BF16 / GELU)
+  float* red;                             // DGELU: this wave's 64 column sums in the exchange area (LDS)
+};
+
 template <int S>
-PVR_DEV void ws_epi_load(WsEpi& E, int lane) {
+PVR_DEV void ws_epi_load_x(WsEpi& E) {
   constexpr int I = S >> 1, JP = S & 1;
-  E.pu[S & 1] = __builtin_amdgcn_raw_buffer_load_b128(E.srs, (uint32_t)(E.e * 8192 + (I * 2 + JP) * 1024 + lane * 16), 0, WS_SC1);
-  if (E.has_in) E.px[S & 1] = __builtin_amdgcn_raw_buffer_load_b128(E.xrs, E.vx[JP] + (uint32_t)(I * 16 * E.ldx * 2), 0, 0);
+  if (E.has_in) E.x[S & 1] = __builtin_amdgcn_raw_buffer_load_b128(E.xrs, (JP ? E.vx1 : E.vx0) + (uint32_t)(I * 16 * E.ldx2), 0, 0);
 }
 
 template <int EPI>
-PVR_DEV void ws_epi_begin(const GemmParams& p, WsEpi& E, int m0, int n0, const char* scratch, int e, int lane) {
+PVR_DEV void ws_epi_begin(const GemmParams& p, WsEpi& E, int m0, int n0, int e, int lane) {
   const int wm = e >> 1, wn = e & 1, li = lane & 15, g = lane >> 4;
-  E.e = e;
   E.mb = m0 + wm * 64;
   E.nb = n0 + wn * 64;
   const int rows = max(0, min(64, p.M - E.mb));
   const uint32_t OOB = 0x80000000u;
   E.crs = make_rsrc((const uint16_t*)p.C + (int64_t)E.mb * p.ldc, rows ? (uint32_t)(((int64_t)(rows - 1) * p.ldc + p.N) * 2) : 0);
   E.xrs = E.crs;
-  E.ldx = (int)p.ldc;
+  int ldx = (int)p.ldc;
   E.has_in = EPI == EPI_DGELU_;
   if constexpr (EPI == EPI_BF16_) {
     if (p.resid) {
       E.xrs = make_rsrc(p.resid + (int64_t)E.mb * p.ld_resid, rows ? (uint32_t)(((int64_t)(rows - 1) * p.ld_resid + p.N) * 2) : 0);
-      E.ldx = (int)p.ld_resid;
+      ldx = (int)p.ld_resid;
       E.has_in = true;
     }
   } else {
     const bool has = p.aux != nullptr;
     E.xrs = make_rsrc(has ? p.aux + (int64_t)E.mb * p.ld_aux : p.aux, has && rows ? (uint32_t)(((int64_t)(rows - 1) * p.ld_aux + p.N) * 2) : 0);
-    E.ldx = (int)p.ld_aux;
+    ldx = (int)p.ld_aux;
   }
-  E.srs = make_rsrc(scratch, WS_U_BYTES);
+  E.ldc2 = (int)p.ldc * 2;
+  E.ldx2 = ldx * 2;
+  const int cb = E.nb + ((g & 1) << 4) + ((g & 2) << 2);  // this lane's first column (jp = 0)
+  E.vc0 = cb < p.N ? (uint32_t)((li * (int)p.ldc + cb) * 2) : OOB;
+  E.vx0 = cb < p.N ? (uint32_t)((li * ldx + cb) * 2) : OOB;
+  E.vc1 = cb + 32 < p.N ? (uint32_t)((li * (int)p.ldc + cb + 32) * 2) : OOB;
+  E.vx1 = cb + 32 < p.N ? (uint32_t)((li * ldx + cb + 32) * 2) : OOB;
 #pragma unroll
-  for (int jp = 0; jp < 2; ++jp) {
-    const int c0 = E.nb + 32 * jp + ((g & 1) << 4) + ((g & 2) << 2);
-    const bool okc = c0 < p.N;
-    E.vc[jp] = okc ? (uint32_t)((li * (int)p.ldc + c0) * 2) : OOB;
-    E.vx[jp] = okc ? (uint32_t)((li * E.ldx + c0) * 2) : OOB;
+  for (int k = 0; k < 8; ++k) E.bias[0][k] = E.bias[1][k] = 0.f;
+  if constexpr (EPI != EPI_DGELU_) {
+    if (p.bias) {
+      const __amdgpu_buffer_rsrc_t brs = make_rsrc(p.bias, (uint32_t)p.N * 4);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) E.cs[jp][k] = 0.f;
+      for (int jp = 0; jp < 2; ++jp) {
+        const uint32_t vb = cb + 32 * jp < p.N ? (uint32_t)((cb + 32 * jp) * 4) : OOB;
+        const v4f b0 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(brs, vb, 0, 0));
+        const v4f b1 = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(brs, vb + 16, 0, 0));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { E.bias[jp][k] = b0[k]; E.bias[jp][4 + k] = b1[k]; }
+      }
+    }
   }
-  ws_epi_load<0>(E, lane);
-  ws_epi_load<1>(E, lane);
+  ws_epi_load_x<0>(E);
+  ws_epi_load_x<1>(E);
 }
 
 PVR_DEV float bfw_lo(uint32_t w) { return __uint_as_float(w << 16); }
 PVR_DEV float bfw_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
 
-// Unit S: 8 elements per lane. Consumes ring slot S & 1, then refills it with unit S + 2.
-template <int EPI, int S>
-PVR_DEV void ws_epi_unit(const GemmParams& p, WsEpi& E, uint32_t key, uint64_t seed, bool idx32, int lane) {
+// Unit S = (fragment row S >> 1, column pair S & 1): 8 elements per lane. Dropout: the 32-bit element
+// index (host check: M * N < 2^32).
+template <int EPI, int S, int NU>
+PVR_DEV void ws_epi_unit(const GemmParams& p, WsEpi& E, const WsBlock<NU>& B, uint32_t key, int lane) {
   constexpr int I = S >> 1, JP = S & 1;
   const int li = lane & 15, g = lane >> 4;
   const int m = E.mb + 16 * I + li;
   const int c0 = E.nb + 32 * JP + ((g & 1) << 4) + ((g & 2) << 2);
-  const uint32_t so_c = (uint32_t)(I * 16 * (int)p.ldc * 2), so_x = (uint32_t)(I * 16 * E.ldx * 2);
-  // words 0, 1: columns 16 (2 JP) + 4g .. +3 of the pair's first fragment, 2, 3: of the second
-  const v4u uu = E.pu[S & 1], xin = E.px[S & 1];
-  if constexpr (S + 2 < 8) ws_epi_load<S + 2>(E, lane);
-  uint32_t q[4] = {uu[0], uu[1], uu[2], uu[3]};
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(q[0]), "+v"(q[2]));
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(q[1]), "+v"(q[3]));
-  float v[8] = {bfw_lo(q[0]), bfw_hi(q[0]), bfw_lo(q[1]), bfw_hi(q[1]), bfw_lo(q[2]), bfw_hi(q[2]), bfw_lo(q[3]), bfw_hi(q[3])};
+  const uint32_t vc = (JP ? E.vc1 : E.vc0) + (uint32_t)(I * 16 * E.ldc2);
+  const uint32_t vx = (JP ? E.vx1 : E.vx0) + (uint32_t)(I * 16 * E.ldx2);
+  const v4u xin = E.x[S & 1];
+  if constexpr (S + 2 < 8) ws_epi_load_x<S + 2>(E);
+  float v[8];
+  if constexpr (NU == 16) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // the register-direct epilogue's swap, on the fp32 values
+      uint32_t a = B.q[I * 4 + 2 * JP][r], b = B.q[I * 4 + 2 * JP + 1][r];
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+      v[r] = __uint_as_float(a);
+      v[4 + r] = __uint_as_float(b);
+    }
+  } else {  // words 0, 1: columns 16 (2 JP) + 4g .. +3 of the pair's first fragment, 2, 3: of the second
+    uint32_t q0 = B.q[I * 2 + JP][0], q1 = B.q[I * 2 + JP][1], q2 = B.q[I * 2 + JP][2], q3 = B.q[I * 2 + JP][3];
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(q0), "+v"(q2));
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(q1), "+v"(q3));
+    v[0] = bfw_lo(q0); v[1] = bfw_hi(q0); v[2] = bfw_lo(q1); v[3] = bfw_hi(q1);
+    v[4] = bfw_lo(q2); v[5] = bfw_hi(q2); v[6] = bfw_lo(q3); v[7] = bfw_hi(q3);
+  }
+  if constexpr (EPI != EPI_DGELU_) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += E.bias[JP][k];
+  }
   bool keep[8] = {true, true, true, true, true, true, true, true};
   if constexpr (EPI == EPI_BF16_ || EPI == EPI_GELU_) {
     if (p.drop_thr) {
-      const uint64_t idx = (uint64_t)m * p.N + c0;
-      if (idx32) {
-        bool k0[4], k1[4];
-        rng_keep4_32(key, (uint32_t)idx, p.drop_thr, k0);
-        rng_keep4_32(key, (uint32_t)idx + 4, p.drop_thr, k1);
+      const uint32_t idx = (uint32_t)m * (uint32_t)p.N + (uint32_t)c0;
+      bool k0[4], k1[4];
+      rng_keep4_32(key, idx, p.drop_thr, k0);
+      rng_keep4_32(key, idx + 4, p.drop_thr, k1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { keep[k] = k0[k]; keep[4 + k] = k1[k]; }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; k += 2) rng_keep2(seed, idx + k, p.drop_thr, keep[k], keep[k + 1]);
-      }
+      for (int k = 0; k < 4; ++k) { keep[k] = k0[k]; keep[4 + k] = k1[k]; }
     }
   }
   v4u out;
@@ -279,73 +355,61 @@ PVR_DEV void ws_epi_unit(const GemmParams& p, WsEpi& E, uint32_t key, uint64_t s
       ax[k] = pack2bf(d2.x, d2.y);
       out[k] = pack2bf(g2.x, g2.y);
     }
-    __builtin_amdgcn_raw_buffer_store_b128(ax, E.xrs, E.vx[JP] + so_x, 0, 0);  // no aux (inference): 0-byte resource
+    __builtin_amdgcn_raw_buffer_store_b128(ax, E.xrs, vx, 0, 0);  // no aux (inference): 0-byte resource
   } else {  // EPI_DGELU
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       v[2 * k] *= bfw_lo(xin[k]);
       v[2 * k + 1] *= bfw_hi(xin[k]);
     }
+    // bias-gradient column sums: over the unit's 16 rows (lanes li) by DPP, then one LDS float add
+    // per column into this wave's exchange row (no per-lane accumulators: the fp32 hand-off block
+    // already holds 64 registers)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) E.cs[JP][k] += v[k];
+    for (int k = 0; k < 8; ++k) {
+      const float c = row16_sum(v[k]);
+      if (li == 0) atomicAdd(E.red + 32 * JP + ((g & 1) << 4) + ((g & 2) << 2) + k, c);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) out[k] = pack2bf(v[2 * k], v[2 * k + 1]);
   }
-  __builtin_amdgcn_raw_buffer_store_b128(out, E.crs, E.vc[JP] + so_c, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(out, E.crs, vc, 0, 0);
 }
 
-template <int EPI>
-PVR_DEV void ws_epi_stage(const GemmParams& p, WsEpi& E, int s, uint32_t key, uint64_t seed, bool idx32, int lane) {
-  switch (s) {
-    case 0: ws_epi_unit<EPI, 0>(p, E, key, seed, idx32, lane); break;
-    case 1: ws_epi_unit<EPI, 1>(p, E, key, seed, idx32, lane); break;
-    case 2: ws_epi_unit<EPI, 2>(p, E, key, seed, idx32, lane); break;
-    case 3: ws_epi_unit<EPI, 3>(p, E, key, seed, idx32, lane); break;
-    case 4: ws_epi_unit<EPI, 4>(p, E, key, seed, idx32, lane); break;
-    case 5: ws_epi_unit<EPI, 5>(p, E, key, seed, idx32, lane); break;
-    case 6: ws_epi_unit<EPI, 6>(p, E, key, seed, idx32, lane); break;
-    default: ws_epi_unit<EPI, 7>(p, E, key, seed, idx32, lane); break;
-  }
-}
-
-// DGELU column sums, part 1: each wave's 64 column sums (over its 64 rows) into the LDS exchange
-PVR_DEV void ws_cs_put(WsEpi& E, char* smem, int e, int lane) {
-  const int li = lane & 15, g = lane >> 4;
-  float* red = (float*)(smem + WS_CS_OFF) + e * 64;
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float c = row16_sum(E.cs[jp][k]);
-      if (li == 0) red[32 * jp + ((g & 1) << 4) + ((g & 2) << 2) + k] = c;
-    }
+// DGELU column sums, part 1: zero this wave's exchange row (the spare region, free between
+// hand-offs); the units add into it
+PVR_DEV void ws_cs_zero(WsEpi& E, char* smem, int e, int lane) {
+  E.red = (float*)(smem + WS_SPARE) + e * 64;
+  E.red[lane] = 0.f;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 // part 2 (after a barrier): the wm = 0 waves add the four partials of their 64 columns, one atomic
 // per column
 PVR_DEV void ws_cs_add(const GemmParams& p, const WsEpi& E, const char* smem, int e, int lane) {
   if ((e >> 1) != 0 || !p.colsum) return;
-  const float* red = (const float*)(smem + WS_CS_OFF);
+  const float* red = (const float*)(smem + WS_SPARE);
   const int wn = e & 1, c = E.nb + lane;
   const float s = red[(0 + wn) * 64 + lane] + red[(2 + wn) * 64 + lane] + red[(4 + wn) * 64 + lane] + red[(6 + wn) * 64 + lane];
   if (c < p.N) atomicAdd(p.colsum + c, s);
 }
 
-template <int EPI>
+
+template <int EPI, int SPC>
 __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = ws_ntiles(p);
   const int nk = p.K / 32;                   // K-steps per tile (K % 64 == 0, K >= 256: host check)
-  const int nbar = 2 * nk + 1;               // barriers per tile, both roles
-  char* scratch = (char*)p.tail_ws + (int64_t)blockIdx.x * 2 * WS_U_BYTES;
+  const int nbar = 2 * nk + 1;               // barriers of a tile's K loop, both roles
+  constexpr bool F32 = ws_f32u<EPI>();
+  constexpr int R = F32 ? 2 : 1;             // hand-off rounds
+  constexpr int NU = F32 ? 16 : 8;
   if ((int)blockIdx.x >= ntiles) return;
-  constexpr bool HAS_BIAS = EPI != EPI_DGELU_;
 
   if (w < 8) {
     // ============================================================ MFMA waves
     const int grp = w >> 2, wm = w >> 1, wn = w & 1;
-    const int g = lane >> 4;
     int v = blockIdx.x;
     WsTile cur = ws_tile(p, v);
     WsTile nxt = ws_tile(p, v + gridDim.x);
@@ -353,153 +417,144 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
 #pragma unroll
     for (int s = 0; s < WS_AHEAD; ++s) ws_issue(cur.ars, cur.brs, smem + s * WS_SLOT, dma, s * 64, w);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WS_VM) : "memory");  // K-step 0 landed
-    ws_barrier();                                                  // P0 (the epilogue waves staged tile 0's bias)
-    int G0 = 0, k = 0;
+    ws_barrier();                                                  // P0
+    int G0 = 0;
     for (;;) {
       v4f acc[4][4];
-      if (HAS_BIAS && p.bias) {  // accumulators start at the bias (staged in LDS by the epilogue waves)
-        const float* bs = (const float*)(smem + WS_BIAS_OFF + (k & 1) * WS_BN * 4) + wn * 64 + 4 * g;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const v4f b4 = *(const __attribute__((address_space(3))) v4f*)(bs + 16 * j);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][j] = b4;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-      }
+        for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
       if (grp == 1) ws_barrier();  // group 1 runs one barrier behind
-      // first K-steps after a tile end: the u stores are younger than the DMAs these steps wait for;
-      // step 3's plain wait retires them
-      for (int ks = 0; ks < nk; ++ks) ws_step(acc, smem, G0 + ks, G0, nk, cur, nxt, dma, G0 > 0 && ks < 3, w, lane, wm, wn);
+      for (int ks = 0; ks < nk; ++ks) ws_step(acc, smem, G0 + ks, G0, nk, cur, nxt, dma, w, lane, wm, wn);
       if (grp == 0) ws_barrier();  // re-align the groups
-      // u = bf16(acc) to scratch slot k & 1 in register order: 8 x 16 B per lane (fragments j, j + 1)
-      {
-        typedef uint32_t v4u_ __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t srs = make_rsrc(scratch + (k & 1) * WS_U_BYTES, WS_U_BYTES);
+      G0 += nk;
+      // hand-off: round r writes, the epilogue waves read, both barrier-fenced
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int jp = 0; jp < 2; ++jp) {
-            const v4f a0 = acc[i][2 * jp], a1 = acc[i][2 * jp + 1];
-            const v4u_ o = {pack2bf(a0[0], a0[1]), pack2bf(a0[2], a0[3]), pack2bf(a1[0], a1[1]), pack2bf(a1[2], a1[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(o, srs, (uint32_t)(w * 8192 + (i * 2 + jp) * 1024 + lane * 16), 0, 0);
-          }
+      for (int r = 0; r < R; ++r) {
+        if (PVR_WS_ABL != 3 && (R == 1 || grp == r)) ws_put<F32>(acc, smem, G0, R == 1 ? w : w & 3, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ws_barrier();  // H1
+        ws_barrier();  // H2: the epilogue waves hold it
       }
       v += gridDim.x;
-      ++k;
       if (v >= ntiles) break;
-      G0 += nk;
       cur = nxt;
       nxt = ws_tile(p, v + gridDim.x);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // u stores retired; no LDS-DMA outlives the workgroup
-    ws_barrier();                                      // F: the epilogue waves may read the last tiles
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup (null steps)
     return;
   }
 
   // ============================================================== epilogue waves
   const int e = w - 8;
-  const uint64_t seed = (p.drop_thr ? *p.seed_ptr : 0ull) + p.seed_offset;
-  const uint32_t key = p.drop_thr ? rng_key(seed) : 0u;
-  const bool idx32 = (uint64_t)p.M * (uint64_t)p.N + 8 <= 0xFFFFFFFFull;
-  const int tid = threadIdx.x - 512;
-  auto stage_bias = [&](int vt, int kslot) {  // bias of tile vt -> LDS slot kslot & 1 (before the MFMA waves read it)
-    if (!HAS_BIAS || !p.bias || vt >= ntiles) return;
-    int m0, n0;
-    ws_coords(p, vt, m0, n0);
-    if (tid < WS_BN) {
-      const int n = n0 + tid;
-      ((float*)(smem + WS_BIAS_OFF + (kslot & 1) * WS_BN * 4))[tid] = n < p.N ? p.bias[n] : 0.f;
-    }
-  };
-  stage_bias(blockIdx.x, 0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint32_t key = p.drop_thr ? rng_key(*p.seed_ptr + p.seed_offset) : 0u;
   ws_barrier();  // P0
-  WsEpi E;
-  // stage s of the block runs after barrier interval at(s) of the MFMA waves' tile: spread over the
-  // tile's 2 nk + 1 intervals, loads at interval 0
-  auto at = [&](int s) { return 1 + (s * (nbar - 4)) / 8; };
-  int k = 0;
-  for (int v = blockIdx.x; v < ntiles; v += gridDim.x, ++k) {
-    // MFMA tile k is running; process tile k - 2 (its u stores retired during tile k - 1)
-    const bool work = k >= 2;
-    int s = 0;
-    for (int b = 0; b < nbar; ++b) {
-      if (b == 0) {
-        stage_bias(v + gridDim.x, k + 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (work) {
-          int m0, n0;
-          ws_coords(p, v - 2 * gridDim.x, m0, n0);
-          ws_epi_begin<EPI>(p, E, m0, n0, scratch + (k & 1) * WS_U_BYTES, e, lane);
-        }
-      }
-      if (work) {
-        while (s < 8 && b >= at(s)) ws_epi_stage<EPI>(p, E, s++, key, seed, idx32, lane);
-        if constexpr (EPI == EPI_DGELU_) {
-          if (b == nbar - 2) {
-            ws_cs_put(E, smem, e, lane);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          }
-          if (b == nbar - 1) ws_cs_add(p, E, smem, e, lane);
-        }
-      }
+  WsBlock<NU> B;
+  bool have = false;  // B holds a tile (handed off at the end of the previous MFMA tile)
+  int vprev = 0;
+  int G0 = 0;
+  for (int v = blockIdx.x; v < ntiles; v += gridDim.x) {
+    // the MFMA waves run tile v; process tile vprev (if any) over the K loop's barrier intervals:
+    // interval 0 loads its bias and first per-row inputs, unit s runs after barrier SPC (s + 1)
+    if (have && PVR_WS_ABL == 0) {
+      WsEpi E;
+      int m0, n0;
+      ws_coords(p, vprev, m0, n0);
+      ws_epi_begin<EPI>(p, E, m0, n0, e, lane);
+      if constexpr (EPI == EPI_DGELU_) ws_cs_zero(E, smem, e, lane);
       ws_barrier();
+      ws_static_for<0, 8>([&](auto sc) {
+        constexpr int S = decltype(sc)::value;
+#pragma unroll
+        for (int t = 1; t < SPC; ++t) ws_barrier();
+        ws_epi_unit<EPI, S, NU>(p, E, B, key, lane);
+        ws_barrier();
+      });
+      int rest = nbar - 1 - 8 * SPC;
+      if constexpr (EPI == EPI_DGELU_) {  // the exchange area (spare region) is free until the hand-off
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ws_barrier();
+        ws_cs_add(p, E, smem, e, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        rest -= 1;
+      }
+      for (; rest > 0; --rest) ws_barrier();
+    } else {
+      for (int b = 0; b < nbar; ++b) ws_barrier();
     }
+    G0 += nk;
+    // hand-off of tile v
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      ws_barrier();  // H1
+      if (PVR_WS_ABL == 0 && (R == 1 || (e >> 2) == r)) ws_get<F32, NU>(B, smem, G0, R == 1 ? e : e & 3, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ws_barrier();  // H2
+    }
+    have = true;
+    vprev = v;
   }
-  ws_barrier();  // F: every u store of the MFMA waves retired; they have exited
-  // the last one or two tiles: no barriers needed beside the (exited) MFMA waves, except the
+  // the last tile, after the MFMA waves have exited: no barriers needed beside them, except the
   // column-sum exchange between the epilogue waves themselves
-  const int ktot = k;
-  for (int kk = max(0, ktot - 2); kk < ktot; ++kk) {
+  if (have && PVR_WS_ABL == 0) {
+    WsEpi E;
     int m0, n0;
-    ws_coords(p, blockIdx.x + kk * gridDim.x, m0, n0);
-    ws_epi_begin<EPI>(p, E, m0, n0, scratch + (kk & 1) * WS_U_BYTES, e, lane);
-    for (int s = 0; s < 8; ++s) ws_epi_stage<EPI>(p, E, s, key, seed, idx32, lane);
+    ws_coords(p, vprev, m0, n0);
+    ws_epi_begin<EPI>(p, E, m0, n0, e, lane);
+    if constexpr (EPI == EPI_DGELU_) ws_cs_zero(E, smem, e, lane);
+    ws_static_for<0, 8>([&](auto sc) {
+      constexpr int S = decltype(sc)::value;
+      ws_epi_unit<EPI, S, NU>(p, E, B, key, lane);
+    });
     if constexpr (EPI == EPI_DGELU_) {
-      ws_cs_put(E, smem, e, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       ws_barrier();
       ws_cs_add(p, E, smem, e, lane);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      ws_barrier();
     }
   }
 }
 
-template <int EPI>
-hipError_t launch_ws(const GemmParams& p, hipStream_t s, int cus) {
-  auto kern = gemm_ws_kernel<EPI>;
+template <int EPI, int SPC>
+hipError_t launch_ws_spc(const GemmParams& p, hipStream_t s, int grid) {
+  auto kern = gemm_ws_kernel<EPI, SPC>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WS_LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int ntiles = ((p.M + WS_BM - 1) / WS_BM) * ((p.N + WS_BN - 1) / WS_BN);
-  const int grid = ntiles < cus ? ntiles : cus;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), WS_LDS, s, p);
   return hipGetLastError();
+}
+
+// the epilogue waves' unit spacing SPC (barriers per unit): the widest that fits the K loop's
+// 2 nk + 1 barriers (8 units + interval 0 + 2 for the column-sum exchange)
+template <int EPI>
+hipError_t launch_ws(const GemmParams& p, hipStream_t s, int cus) {
+  const int ntiles = ((p.M + WS_BM - 1) / WS_BM) * ((p.N + WS_BN - 1) / WS_BN);
+  const int grid = ntiles < cus ? ntiles : cus;
+  const int nbar = 2 * (p.K / 32) + 1;
+  if (1 + 8 * 4 + 2 <= nbar) return launch_ws_spc<EPI, 4>(p, s, grid);
+  if (1 + 8 * 2 + 2 <= nbar) return launch_ws_spc<EPI, 2>(p, s, grid);
+  return launch_ws_spc<EPI, 1>(p, s, grid);
 }
 
 }  // namespace
 }  // namespace pvr
 
 // 1 if the wave-specialized kernel takes this GEMM (k-contiguous bf16 operands, bf16-output
-// epilogue without row remap / addend / fp8 copy, K a multiple of 64 and >= 256, the per-stream
-// scratch present and large enough)
+// epilogue without row remap / addend / fp8 copy, K a multiple of 64 and >= 256, 32-bit element
+// indices, 31-bit buffer offsets)
 extern "C" int pvr_gemm_ws_ok(const pvr::GemmParams* pp, int cus) {
+  (void)cus;
   const pvr::GemmParams& p = *pp;
   if (p.elem8 || !p.a_kcontig || !p.b_kcontig || p.epi > 2 || p.addend || p.row_group || p.c_skip || p.q_out) return 0;
   if (p.K % 64 || p.K < 256 || p.k_split_len < p.K || (p.N & 7) || p.M <= 0) return 0;
-  if (!p.tail_ws || p.tail_ws_elems * 4 < (int64_t)cus * 2 * pvr::WS_U_BYTES) return 0;
   const int64_t l1 = p.ldc > p.ld_resid ? p.ldc : p.ld_resid;
   const int64_t ld = l1 > p.ld_aux ? l1 : p.ld_aux;
   if ((int64_t)p.M * ld * 2 >= (1ll << 31) || 256ll * p.lda * 2 >= (1ll << 31) || 128ll * p.ldb * 2 >= (1ll << 31)) return 0;
+  if ((uint64_t)p.M * (uint64_t)p.N + 8 > 0xFFFFFFFFull) return 0;  // 32-bit dropout element index
   return 1;
 }
 

@@ -115,8 +115,10 @@ def check_gemm_gelu(M, N, K, t=0):
     return (f"gemm_gelu M{M} N{N} K{K} t{t}", worst((u, gp), (h, F.gelu(uref.detach()))), lim(4e-3, 7e-3))
 
 
-def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13)):
-    """GELU + dropout + aux epilogue: identical masks and values across GEMM structures."""
+def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13), l2_lim=1e-3):
+    """GELU + dropout + aux epilogue: identical masks and values across GEMM structures (tile 15
+    rounds the pre-activation to bf16 before the GELU, as an autocast Linear output is: ``l2_lim``
+    then allows that rounding, the fp32-reference tolerance of check_gemm_gelu)."""
     x, w, b = bf(rnd(M, K)), bf(rnd(N, K, scale=0.05)), rnd(N)
     seed = torch.tensor([777], dtype=torch.int64, device=DEV)
     outs = []
@@ -131,7 +133,7 @@ def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13)):
     m = worst(*[pair for h1, u1 in outs[1:] for pair in ((h1, h0), (u1, u0))])
     m.update(mask_differs=float(not same_mask), rate_dev=abs(rate - 0.1))
     return (f"gemm_gelu+dropout M{M} N{N} K{K} tiles{tiles} (drop rate {rate:.4f})", m,
-            lim(1e-3, 8e-3, mask_differs=0, rate_dev=rate_limit(0.1, M * N)))  # same values (1-ulp flips tolerated)
+            lim(l2_lim, 8e-3, mask_differs=0, rate_dev=rate_limit(0.1, M * N)))  # same values (1-ulp flips tolerated)
 
 
 def check_gemm_gelu_drop_paths(M=3000, N=768, p=0.1):
@@ -1530,7 +1532,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_fwd(70000, 768, 512, 15, True, True),
         lambda: check_gemm_gelu(6000, 3072, 768, 15),
         lambda: check_gemm_gelu(50432, 3072, 768, 15),
-        lambda: check_gemm_gelu_dropout(5000, 3072, 768, tiles=(13, 15)),
+        lambda: check_gemm_gelu_dropout(5000, 3072, 768, tiles=(13, 15), l2_lim=4e-3),
         lambda: check_gemm_dropout(3000, 768, 1024, 0.1, 15),
         lambda: check_gemm_dgelu(4096, 768, 3072, True, 15),
         lambda: check_gemm_dgelu(50432, 768, 3072, True, 15),
