@@ -42,6 +42,10 @@ constexpr int EPI_BF16_ = 0, EPI_GELU_ = 1, EPI_DGELU_ = 2;  // = GemmEpi of gem
 
 // diagnostic ablations (timing only, wrong results): 1 = the epilogue waves only keep the barrier
 // count, 3 = and no hand-off (the MFMA waves alone)
+// 1: the MFMA waves raise their priority over their MFMA bursts (A/B knob)
+#ifndef PVR_WS_PRIO
+#define PVR_WS_PRIO 1
+#endif
 #ifndef PVR_WS_ABL
 #define PVR_WS_ABL 0
 #endif
@@ -160,12 +164,12 @@ PVR_DEV void ws_step(v4f (&acc)[4][4], char* smem, int G, int G0, int nk, const 
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WS_VM) : "memory");
   ws_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_setprio(1);
+  if (PVR_WS_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(b[j], a[i], acc[i][j]);  // lane: C[16i + li][16j + 4g + r]
-  __builtin_amdgcn_s_setprio(0);
+  if (PVR_WS_PRIO) __builtin_amdgcn_s_setprio(0);
   ws_barrier();
 }
 
@@ -226,6 +230,7 @@ struct WsEpi {
   v4u x[2];                               // per-row inputs of the next even / odd unit (two units ahead)
   float bias[2][8];                       // this lane's 8 + 8 bias columns (BF16 / GELU)
   float* red;                             // DGELU: this wave's 64 column sums in the exchange area (LDS)
+  uint32_t ow[4], aw[4];                  // the unit's packed outputs (and GELU aux) until its last pair
 };
 
 template <int S>
@@ -285,95 +290,110 @@ PVR_DEV void ws_epi_begin(const GemmParams& p, WsEpi& E, int m0, int n0, int e, 
 PVR_DEV float bfw_lo(uint32_t w) { return __uint_as_float(w << 16); }
 PVR_DEV float bfw_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
 
-// Unit S = (fragment row S >> 1, column pair S & 1): 8 elements per lane. Dropout: the 32-bit element
-// index (host check: M * N < 2^32).
-template <int EPI, int S, int NU>
-PVR_DEV void ws_epi_unit(const GemmParams& p, WsEpi& E, const WsBlock<NU>& B, uint32_t key, int lane) {
+// Unit S = (fragment row I = S >> 1, column half JP = S & 1): 8 elements per lane, columns c0 .. c0 + 7,
+// in 4 pairs P (columns c0 + 2P, +1) run in the order 0, 2, 1, 3 (one permlane swap serves two pairs).
+// A unit is split into pieces of 1, 2 or 4 pairs, one piece per K-loop barrier interval: a whole
+// unit (~160 VALU incl. 16 transcendentals per wave) is several MFMA intervals of issue time and
+// would hold the MFMA waves at the next barrier. The results collect in E.ow / E.aw and the last pair
+// stores them (16 B per lane). Dropout: one 32-bit hash per pair (the rng_keep4_32 bits; host check
+// M * N < 2^32).
+template <int EPI, int S, int P, int NU>
+PVR_DEV void ws_epi_pair(const GemmParams& p, WsEpi& E, WsBlock<NU>& B, uint32_t key, int lane) {
   constexpr int I = S >> 1, JP = S & 1;
   const int li = lane & 15, g = lane >> 4;
-  const int m = E.mb + 16 * I + li;
-  const int c0 = E.nb + 32 * JP + ((g & 1) << 4) + ((g & 2) << 2);
-  const uint32_t vc = (JP ? E.vc1 : E.vc0) + (uint32_t)(I * 16 * E.ldc2);
-  const uint32_t vx = (JP ? E.vx1 : E.vx0) + (uint32_t)(I * 16 * E.ldx2);
-  const v4u xin = E.x[S & 1];
-  if constexpr (S + 2 < 8) ws_epi_load_x<S + 2>(E);
-  float v[8];
-  if constexpr (NU == 16) {
+  float v0, v1;
+  if constexpr (NU == 16) {  // fp32 words: a = group 4I + 2JP, b = a + 1; swap r pairs (0, 1) / (2, 3)
+    constexpr int ga = I * 4 + 2 * JP, r0 = (P & 1) * 2;
+    if constexpr (P < 2) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {  // the register-direct epilogue's swap, on the fp32 values
-      uint32_t a = B.q[I * 4 + 2 * JP][r], b = B.q[I * 4 + 2 * JP + 1][r];
-      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-      v[r] = __uint_as_float(a);
-      v[4 + r] = __uint_as_float(b);
-    }
-  } else {  // words 0, 1: columns 16 (2 JP) + 4g .. +3 of the pair's first fragment, 2, 3: of the second
-    uint32_t q0 = B.q[I * 2 + JP][0], q1 = B.q[I * 2 + JP][1], q2 = B.q[I * 2 + JP][2], q3 = B.q[I * 2 + JP][3];
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(q0), "+v"(q2));
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(q1), "+v"(q3));
-    v[0] = bfw_lo(q0); v[1] = bfw_hi(q0); v[2] = bfw_lo(q1); v[3] = bfw_hi(q1);
-    v[4] = bfw_lo(q2); v[5] = bfw_hi(q2); v[6] = bfw_lo(q3); v[7] = bfw_hi(q3);
-  }
-  if constexpr (EPI != EPI_DGELU_) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += E.bias[JP][k];
-  }
-  bool keep[8] = {true, true, true, true, true, true, true, true};
-  if constexpr (EPI == EPI_BF16_ || EPI == EPI_GELU_) {
-    if (p.drop_thr) {
-      const uint32_t idx = (uint32_t)m * (uint32_t)p.N + (uint32_t)c0;
-      bool k0[4], k1[4];
-      rng_keep4_32(key, idx, p.drop_thr, k0);
-      rng_keep4_32(key, idx + 4, p.drop_thr, k1);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) { keep[k] = k0[k]; keep[4 + k] = k1[k]; }
-    }
-  }
-  v4u out;
-  if constexpr (EPI == EPI_BF16_) {
-    if (p.drop_thr) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = keep[k] ? v[k] * p.drop_scale : 0.f;
-    }
-    if (E.has_in) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[2 * k] += bfw_lo(xin[k]);
-        v[2 * k + 1] += bfw_hi(xin[k]);
+      for (int r = r0; r < r0 + 2; ++r) {
+        uint32_t x = B.q[ga][r], y = B.q[ga + 1][r];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+        B.q[ga][r] = x;
+        B.q[ga + 1][r] = y;
       }
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = pack2bf(v[2 * k], v[2 * k + 1]);
-  } else if constexpr (EPI == EPI_GELU_) {
-    v4u ax;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const v2f s2 = {keep[2 * k] ? p.drop_scale : 0.f, keep[2 * k + 1] ? p.drop_scale : 0.f};
-      v2f g2, d2;
-      gelu_and_grad2((v2f){v[2 * k], v[2 * k + 1]}, g2, d2);
-      g2 *= s2;
-      d2 *= s2;
-      ax[k] = pack2bf(d2.x, d2.y);
-      out[k] = pack2bf(g2.x, g2.y);
+    constexpr int src = P < 2 ? ga : ga + 1;
+    v0 = __uint_as_float(B.q[src][r0]);
+    v1 = __uint_as_float(B.q[src][r0 + 1]);
+  } else {  // bf16 words 0, 1: the pair's first fragment, 2, 3: its second; swaps (0, 2), (1, 3)
+    constexpr int gw = I * 2 + JP;
+    if constexpr (P < 2) {
+      uint32_t x = B.q[gw][P], y = B.q[gw][P + 2];
+      asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+      B.q[gw][P] = x;
+      B.q[gw][P + 2] = y;
     }
-    __builtin_amdgcn_raw_buffer_store_b128(ax, E.xrs, vx, 0, 0);  // no aux (inference): 0-byte resource
-  } else {  // EPI_DGELU
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[2 * k] *= bfw_lo(xin[k]);
-      v[2 * k + 1] *= bfw_hi(xin[k]);
-    }
-    // bias-gradient column sums: over the unit's 16 rows (lanes li) by DPP, then one LDS float add
-    // per column into this wave's exchange row (no per-lane accumulators: the fp32 hand-off block
-    // already holds 64 registers)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float c = row16_sum(v[k]);
-      if (li == 0) atomicAdd(E.red + 32 * JP + ((g & 1) << 4) + ((g & 2) << 2) + k, c);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = pack2bf(v[2 * k], v[2 * k + 1]);
+    v0 = bfw_lo(B.q[gw][P]);
+    v1 = bfw_hi(B.q[gw][P]);
   }
-  __builtin_amdgcn_raw_buffer_store_b128(out, E.crs, vc, 0, 0);
+  const uint32_t xw = E.x[S & 1][P];
+  if constexpr (EPI != EPI_DGELU_) {
+    v0 += E.bias[JP][2 * P];
+    v1 += E.bias[JP][2 * P + 1];
+  }
+  bool k0 = true, k1 = true;
+  if constexpr (EPI == EPI_BF16_ || EPI == EPI_GELU_) {
+    if (p.drop_thr) {
+      const int m = E.mb + 16 * I + li;
+      const int c = E.nb + 32 * JP + ((g & 1) << 4) + ((g & 2) << 2) + 2 * P;
+      const uint32_t h = rng_mix32((((uint32_t)m * (uint32_t)p.N + (uint32_t)c) >> 1) ^ key);
+      k0 = (h & 0xFFFFu) >= p.drop_thr;
+      k1 = (h >> 16) >= p.drop_thr;
+    }
+  }
+  if constexpr (EPI == EPI_BF16_) {
+    if (p.drop_thr) {
+      v0 = k0 ? v0 * p.drop_scale : 0.f;
+      v1 = k1 ? v1 * p.drop_scale : 0.f;
+    }
+    if (E.has_in) {
+      v0 += bfw_lo(xw);
+      v1 += bfw_hi(xw);
+    }
+    E.ow[P] = pack2bf(v0, v1);
+  } else if constexpr (EPI == EPI_GELU_) {
+    const v2f s2 = {k0 ? p.drop_scale : 0.f, k1 ? p.drop_scale : 0.f};
+    v2f g2, d2;
+    gelu_and_grad2((v2f){v0, v1}, g2, d2);
+    g2 *= s2;
+    d2 *= s2;
+    E.aw[P] = pack2bf(d2.x, d2.y);
+    E.ow[P] = pack2bf(g2.x, g2.y);
+  } else {  // EPI_DGELU: bias-gradient column sums over the unit's 16 rows by DPP, one LDS add per column
+    v0 *= bfw_lo(xw);
+    v1 *= bfw_hi(xw);
+    const float c0s = row16_sum(v0), c1s = row16_sum(v1);
+    float* r = E.red + 32 * JP + ((g & 1) << 4) + ((g & 2) << 2) + 2 * P;
+    if (li == 0) {
+      atomicAdd(r, c0s);
+      atomicAdd(r + 1, c1s);
+    }
+    E.ow[P] = pack2bf(v0, v1);
+  }
+  // pin the pair's results here: without it the compiler sinks the arithmetic across the barriers
+  // to the unit's store, re-forming one interval-sized lump
+  asm volatile("" : "+v"(E.ow[P]));
+  if constexpr (EPI == EPI_GELU_) asm volatile("" : "+v"(E.aw[P]));
+  if constexpr (P == 3) {
+    const uint32_t vc = (JP ? E.vc1 : E.vc0) + (uint32_t)(I * 16 * E.ldc2);
+    if constexpr (EPI == EPI_GELU_) {  // no aux (inference): 0-byte resource
+      const uint32_t vx = (JP ? E.vx1 : E.vx0) + (uint32_t)(I * 16 * E.ldx2);
+      __builtin_amdgcn_raw_buffer_store_b128((v4u){E.aw[0], E.aw[1], E.aw[2], E.aw[3]}, E.xrs, vx, 0, 0);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128((v4u){E.ow[0], E.ow[1], E.ow[2], E.ow[3]}, E.crs, vc, 0, 0);
+    if constexpr (S + 2 < 8) ws_epi_load_x<S + 2>(E);  // the ring slot of unit S is free now
+  }
+}
+
+// piece H of NQ of unit S: pairs 4H / NQ .. 4(H + 1) / NQ - 1 of the order 0, 2, 1, 3
+template <int EPI, int S, int H, int NQ, int NU>
+PVR_DEV void ws_epi_piece(const GemmParams& p, WsEpi& E, WsBlock<NU>& B, uint32_t key, int lane) {
+  constexpr int PER = 4 / NQ;
+  ws_static_for<0, PER>([&](auto pc) {
+    constexpr int k = H * PER + decltype(pc)::value;
+    ws_epi_pair<EPI, S, (k == 0 ? 0 : k == 1 ? 2 : k == 2 ? 1 : 3), NU>(p, E, B, key, lane);
+  });
 }
 
 // DGELU column sums, part 1: zero this wave's exchange row (the spare region, free between
@@ -394,7 +414,7 @@ PVR_DEV void ws_cs_add(const GemmParams& p, const WsEpi& E, const char* smem, in
 }
 
 
-template <int EPI, int SPC>
+template <int EPI, int NQ, int SPC>
 __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -456,7 +476,7 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
   int G0 = 0;
   for (int v = blockIdx.x; v < ntiles; v += gridDim.x) {
     // the MFMA waves run tile v; process tile vprev (if any) over the K loop's barrier intervals:
-    // interval 0 loads its bias and first per-row inputs, unit s runs after barrier SPC (s + 1)
+    // interval 0 loads its bias and first per-row inputs, piece x runs after barrier SPC (x + 1)
     if (have && PVR_WS_ABL == 0) {
       WsEpi E;
       int m0, n0;
@@ -464,14 +484,14 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
       ws_epi_begin<EPI>(p, E, m0, n0, e, lane);
       if constexpr (EPI == EPI_DGELU_) ws_cs_zero(E, smem, e, lane);
       ws_barrier();
-      ws_static_for<0, 8>([&](auto sc) {
-        constexpr int S = decltype(sc)::value;
+      ws_static_for<0, 8 * NQ>([&](auto sc) {
+        constexpr int X = decltype(sc)::value;
 #pragma unroll
         for (int t = 1; t < SPC; ++t) ws_barrier();
-        ws_epi_unit<EPI, S, NU>(p, E, B, key, lane);
+        ws_epi_piece<EPI, X / NQ, X % NQ, NQ, NU>(p, E, B, key, lane);
         ws_barrier();
       });
-      int rest = nbar - 1 - 8 * SPC;
+      int rest = nbar - 1 - 8 * NQ * SPC;
       if constexpr (EPI == EPI_DGELU_) {  // the exchange area (spare region) is free until the hand-off
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         ws_barrier();
@@ -505,7 +525,7 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
     if constexpr (EPI == EPI_DGELU_) ws_cs_zero(E, smem, e, lane);
     ws_static_for<0, 8>([&](auto sc) {
       constexpr int S = decltype(sc)::value;
-      ws_epi_unit<EPI, S, NU>(p, E, B, key, lane);
+      ws_epi_piece<EPI, S, 0, 1, NU>(p, E, B, key, lane);
     });
     if constexpr (EPI == EPI_DGELU_) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -515,9 +535,9 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
   }
 }
 
-template <int EPI, int SPC>
+template <int EPI, int NQ, int SPC>
 hipError_t launch_ws_spc(const GemmParams& p, hipStream_t s, int grid) {
-  auto kern = gemm_ws_kernel<EPI, SPC>;
+  auto kern = gemm_ws_kernel<EPI, NQ, SPC>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, WS_LDS);
@@ -528,16 +548,19 @@ hipError_t launch_ws_spc(const GemmParams& p, hipStream_t s, int grid) {
   return hipGetLastError();
 }
 
-// the epilogue waves' unit spacing SPC (barriers per unit): the widest that fits the K loop's
-// 2 nk + 1 barriers (8 units + interval 0 + 2 for the column-sum exchange)
+// the epilogue waves' pieces: one pair per piece (NQ = 4) spaced SPC barriers apart, the widest
+// spacing that fits the K loop's 2 nk + 1 barriers (32 pieces + interval 0 + 2 for the column-sum
+// exchange); short K loops take 2- or 4-pair pieces
 template <int EPI>
 hipError_t launch_ws(const GemmParams& p, hipStream_t s, int cus) {
   const int ntiles = ((p.M + WS_BM - 1) / WS_BM) * ((p.N + WS_BN - 1) / WS_BN);
   const int grid = ntiles < cus ? ntiles : cus;
   const int nbar = 2 * (p.K / 32) + 1;
-  if (1 + 8 * 4 + 2 <= nbar) return launch_ws_spc<EPI, 4>(p, s, grid);
-  if (1 + 8 * 2 + 2 <= nbar) return launch_ws_spc<EPI, 2>(p, s, grid);
-  return launch_ws_spc<EPI, 1>(p, s, grid);
+  if (3 + 32 * 4 <= nbar) return launch_ws_spc<EPI, 4, 4>(p, s, grid);
+  if (3 + 32 * 2 <= nbar) return launch_ws_spc<EPI, 4, 2>(p, s, grid);
+  if (3 + 32 <= nbar) return launch_ws_spc<EPI, 4, 1>(p, s, grid);
+  if (3 + 16 <= nbar) return launch_ws_spc<EPI, 2, 1>(p, s, grid);
+  return launch_ws_spc<EPI, 1, 1>(p, s, grid);
 }
 
 }  // namespace
