@@ -110,9 +110,14 @@ def check_gemm_gelu(M, N, K, t=0):
     u = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
     with tile(t):
         h = G.linear_fwd(x, w, b, gelu_aux=u)
-    uref = (x.float() @ w.float().t() + b).requires_grad_(True)
+    prod = x.float() @ w.float().t()
+    if t == 15:  # tile 15 hands the product to its epilogue waves in bf16 (autocast Linear rounding)
+        prod = prod.bfloat16().float()
+    uref = (prod + b).requires_grad_(True)
     gp = torch.autograd.grad(F.gelu(uref), uref, torch.ones_like(uref))[0]
-    return (f"gemm_gelu M{M} N{N} K{K} t{t}", worst((u, gp), (h, F.gelu(uref.detach()))), lim(4e-3, 7e-3))
+    # tile 15: a bf16 ulp of max deviation on top (the rounded product and the rounded outputs can
+    # land on opposite sides of the reference)
+    return (f"gemm_gelu M{M} N{N} K{K} t{t}", worst((u, gp), (h, F.gelu(uref.detach()))), lim(4e-3, 7e-3 if t != 15 else 1.6e-2))
 
 
 def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13), l2_lim=1e-3):
@@ -133,7 +138,7 @@ def check_gemm_gelu_dropout(M, N, K, tiles=(12, 13), l2_lim=1e-3):
     m = worst(*[pair for h1, u1 in outs[1:] for pair in ((h1, h0), (u1, u0))])
     m.update(mask_differs=float(not same_mask), rate_dev=abs(rate - 0.1))
     return (f"gemm_gelu+dropout M{M} N{N} K{K} tiles{tiles} (drop rate {rate:.4f})", m,
-            lim(l2_lim, 8e-3, mask_differs=0, rate_dev=rate_limit(0.1, M * N)))  # same values (1-ulp flips tolerated)
+            lim(l2_lim, 8e-3 if 15 not in tiles else 1.6e-2, mask_differs=0, rate_dev=rate_limit(0.1, M * N)))  # same values (1-ulp flips tolerated)
 
 
 def check_gemm_gelu_drop_paths(M=3000, N=768, p=0.1):
