@@ -157,6 +157,25 @@ void attach_tail(pvr::GemmParams& p, const torch::Tensor& like) {
   p.tail_cnt_elems = (int)it->second.cnt.numel();
 }
 void set_gemm_tail(bool on) { g_gemm_tail = on; }
+
+// Counters of the in-launch split-K reduction (GemmParams::sk_*): per (device, stream) two words
+// per output tile plus a timeout count, zeroed once; every launch leaves the tile words zero.
+constexpr int g_sk_tiles = 4096;
+torch::Tensor& splitk_counters(const torch::Tensor& like) {
+  static std::map<std::pair<int, hipStream_t>, torch::Tensor> bufs;
+  const auto key = std::make_pair((int)like.get_device(), stream());
+  auto it = bufs.find(key);
+  if (it == bufs.end()) it = bufs.emplace(key, torch::zeros({2 * g_sk_tiles + 4}, like.options().dtype(torch::kInt32))).first;
+  return it->second;
+}
+// spin timeouts of the in-launch split-K reduction on the current stream (0 unless a split's
+// workgroups were not co-resident); reset = true zeroes the count
+int64_t splitk_timeouts(torch::Tensor like, bool reset) {
+  torch::Tensor& c = splitk_counters(like);
+  const int64_t v = c[2 * g_sk_tiles].item<int32_t>();
+  if (reset) c[2 * g_sk_tiles].zero_();
+  return v;
+}
 // fewest K-tiles per split-tail part: 12 (6 / 4 / 3 measured no better or worse on the short-K
 // GEMMs, profiles/r4/ab14/tail_kt.log)
 constexpr int g_tail_min_kt = 12;
@@ -188,7 +207,7 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
           int64_t addend_period, c10::optional<torch::Tensor> aux, int64_t row_group, int64_t row_stride_group,
           int64_t row_offset, c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, int64_t k_split,
           int64_t tile_cfg, c10::optional<torch::Tensor> dbg, c10::optional<torch::Tensor> colsum,
-          int64_t epi_staged, int64_t tail_limit) {
+          int64_t epi_staged, int64_t tail_limit, c10::optional<torch::Tensor> reduce_out, bool reduce_acc) {
   pvr::GemmParams p{};
   p.epi_staged = (int)epi_staged;
   if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
@@ -244,6 +263,26 @@ void gemm(torch::Tensor A, bool a_kcontig, torch::Tensor B, bool b_kcontig, torc
     attach_tail(p, C);
     p.tail_max_units = (int)tail_limit;
     p.tail_min_kt = g_tail_min_kt;
+  }
+  if (reduce_out.has_value() && reduce_out->defined()) {
+    // in-launch reduction of the K splits into reduce_out [M, N] fp32 (GemmParams::sk_*): the
+    // ping-pong weight-gradient kernel, every workgroup co-resident
+    const torch::Tensor& o = *reduce_out;
+    TORCH_CHECK(C.dim() == 3 && epi == 4 && tile_cfg == 14, "gemm: reduce_out needs the split-K workspace form");
+    TORCH_CHECK(o.is_cuda() && o.scalar_type() == torch::kFloat32 && o.dim() == 2 && o.stride(1) == 1 && o.size(0) >= M && o.size(1) >= N &&
+                    o.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0,
+                "gemm: reduce_out must be a 16-B aligned fp32 [M, N] tensor with unit column stride");
+    const int64_t splits = (K + p.k_split_len - 1) / p.k_split_len;
+    const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+    TORCH_CHECK(N % 4 == 0 && tiles <= g_sk_tiles && tiles * splits <= num_cus(), "gemm: reduce_out: too many workgroups to be co-resident");
+    TORCH_CHECK(p.split_stride * 4 * (2 * splits + 16) < (int64_t(1) << 32) && M * p.ldc * 4 < (int64_t(1) << 31),
+                "gemm: reduce_out: workspace too large for 32-bit buffer offsets");
+    torch::Tensor& cnt = splitk_counters(o);
+    p.sk_out = o.data_ptr<float>();
+    p.sk_ldo = o.stride(0);
+    p.sk_acc = reduce_acc ? 1 : 0;
+    p.sk_cnt = reinterpret_cast<unsigned*>(cnt.data_ptr<int32_t>());
+    p.sk_cnt_tiles = g_sk_tiles;
   }
   check(pvr_gemm(&p, stream()), "gemm");
 }
@@ -1063,7 +1102,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("addend_period"), py::arg("aux"), py::arg("row_group"), py::arg("row_stride_group"),
         py::arg("row_offset"), py::arg("seed"), py::arg("seed_offset"), py::arg("drop_p"), py::arg("k_split"),
         py::arg("tile_cfg"), py::arg("dbg") = py::none(), py::arg("colsum") = py::none(),
-        py::arg("epi_staged") = 0, py::arg("tail_limit") = 0);
+        py::arg("epi_staged") = 0, py::arg("tail_limit") = 0, py::arg("reduce_out") = py::none(), py::arg("reduce_acc") = true);
+  m.def("splitk_timeouts", &splitk_timeouts, py::arg("like"), py::arg("reset") = false);
   m.def("num_cus", &num_cus);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_fwd_q8", &layernorm_fwd_q8);

@@ -1217,6 +1217,8 @@ PVR_DEV void epilogue_direct(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
   }
 }
 
+constexpr int CPOL_SC1 = 16;  // buffer-instruction cache policy: sc1 (write-through / L2-bypassing read)
+
 // LDS-staged epilogue of the ping-pong kernel (SWAP layout, bf16-output epilogues): the fp32
 // accumulators cross LDS in two 128-row halves (the 128 KiB of K-tile buffers are free by then),
 // and every thread then owns 4 consecutive columns of rows t/64 + 8k, so each wave instruction
@@ -1363,7 +1365,15 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
         }
       }
       if constexpr (EPI == EPI_F32_STORE) {
-        if (ok) *(float4*)((float*)p.C + (int64_t)blockIdx.z * p.split_stride + (int64_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        if (p.sk_out) {  // in-launch reduction: write-through (sc1) slab stores, read by other CUs
+          typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+          const __amdgpu_buffer_rsrc_t srs = make_rsrc((float*)p.C + (int64_t)blockIdx.z * p.split_stride, (uint32_t)(p.split_stride * 4));
+          if (ok)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_t, make_float4(v[0], v[1], v[2], v[3])), srs,
+                                                   (uint32_t)(((int64_t)m * p.ldc + n) * 4), 0, CPOL_SC1);
+        } else if (ok) {
+          *(float4*)((float*)p.C + (int64_t)blockIdx.z * p.split_stride + (int64_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        }
       } else {
         uint2 o; o.x = pack2bf(v[0], v[1]); o.y = pack2bf(v[2], v[3]);
         if (ok) *(uint2*)(c0 + (int64_t)k * (8 * p.ldc)) = o;
@@ -1400,7 +1410,6 @@ PVR_DEV void epilogue_staged(const GemmParams& p, v4f (&acc)[8][4], char* smem, 
 // arrival counter (agent scope), and the last arriver's waves read every slab with sc1 loads. No
 // release / acquire fences: a release writes back the XCD's whole L2, which with the GEMM's own
 // output dirty in it measured ~30 us per tail tile (profiles/r4/tail_ab.md).
-constexpr int CPOL_SC1 = 16;  // buffer-instruction cache policy: sc1 (write-through / L2-bypassing read)
 
 template <int S>
 PVR_DEV void tail_sum(v4f (&acc)[8][4], __amdgpu_buffer_rsrc_t rs, int tid) {
@@ -1451,6 +1460,92 @@ PVR_DEV bool tail_gather(const GemmParams& p, v4f (&acc)[8][4], char* smem, int 
   }
   __syncthreads();  // the flag word is LDS the epilogue may reuse
   return true;
+}
+
+// The rows [rb, rb + nrow) of one tile of the in-launch split-K reduction: thread t owns columns
+// n0 + 4 (t % 64) .. + 3 of rows rb + t / 64 + 8 i (i < RPT), and sums the S slabs in the order
+// 0..S-1. U slabs x RPT rows of sc1 loads are issued before their adds (16 in flight per thread: one
+// dependent load at a time left the reduction latency-bound, ~25 us per tile at S = 28). Slabs past
+// S and rows past the slice read zero through the resource's range check.
+template <int RPT, int U>
+PVR_DEV void splitk_rows(const GemmParams& p, __amdgpu_buffer_rsrc_t wrs, int S, int rb, int nrow, int n0, int tid) {
+  const int n = n0 + 4 * (tid & 63);
+  const uint32_t far = (uint32_t)(p.split_stride * 4 * S);  // past the resource (host: 2 S + 16 slabs < 4 GiB)
+  uint32_t off[RPT];
+  v4f a[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = (tid >> 6) + 8 * i, m = rb + r;
+    off[i] = r < nrow && m < p.M && n < p.N ? (uint32_t)(((int64_t)m * p.ldc + n) * 4) : far;
+    a[i] = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int q0 = 0; q0 < S; q0 += U) {
+    v4f l[U][RPT];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RPT; ++i)
+        l[u][i] = __builtin_bit_cast(v4f, __builtin_amdgcn_raw_buffer_load_b128(wrs, off[i], (uint32_t)((q0 + u) * p.split_stride * 4), CPOL_SC1));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) a[i] += l[u][i];
+  }
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    if (off[i] == far) continue;
+    const int m = rb + (tid >> 6) + 8 * i;
+    float4* dst = (float4*)(p.sk_out + (int64_t)m * p.sk_ldo + n);
+    const v4f prev = p.sk_acc ? __builtin_bit_cast(v4f, *dst) : v4f{0.f, 0.f, 0.f, 0.f};
+    *dst = __builtin_bit_cast(float4, prev + a[i]);
+  }
+}
+
+// In-launch split-K reduction (GemmParams::sk_*), after this split's slab is stored write-through.
+// The hand-off is the sc1 form of the agent-scope publish: every storing wave drains, one lane adds
+// to the tile's arrival counter, one lane polls it relaxed (s_sleep between polls, bounded), and
+// every slab byte is then read with sc1 loads, so no release / acquire fence (a release writes back
+// the XCD's whole L2). Unlike the split tail's last-arriver gather, every split reduces 1/S of the
+// tile: each workgroup reads 256 KiB in total whatever S is, instead of one workgroup reading S x
+// 256 KiB. The second counter re-arms both once every split has finished reading.
+PVR_DEV void splitk_fixup(const GemmParams& p, char* smem, int tile, int m0, int n0) {
+  typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+  const int S = gridDim.z, z = blockIdx.z, tid = threadIdx.x;
+  unsigned* arrive = p.sk_cnt + 2 * tile;
+  unsigned* done = arrive + 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)S) {
+      __builtin_amdgcn_s_sleep(4);
+      if (++spins == (1u << 24)) {  // ~1 s: a split never arrived (not co-resident); give up
+        __hip_atomic_fetch_add(p.sk_cnt + 2 * p.sk_cnt_tiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(p.C, (uint32_t)(p.split_stride * 4 * S));
+  const int r0 = 256 * z / S, nrow = 256 * (z + 1) / S - r0;
+  const int rpt = (nrow + 7) / 8;  // rows per thread
+  if (rpt <= 1) splitk_rows<1, 16>(p, wrs, S, m0 + r0, nrow, n0, tid);
+  else if (rpt <= 2) splitk_rows<2, 8>(p, wrs, S, m0 + r0, nrow, n0, tid);
+  else if (rpt <= 4) splitk_rows<4, 4>(p, wrs, S, m0 + r0, nrow, n0, tid);
+  else if (rpt <= 8) splitk_rows<8, 2>(p, wrs, S, m0 + r0, nrow, n0, tid);
+  else splitk_rows<16, 1>(p, wrs, S, m0 + r0, nrow, n0, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)(S - 1)) {  // every split has read: re-arm for the next launch
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  (void)smem;
 }
 
 template <bool AK, bool BKC, bool SWAP, int EPI, int ES = 2, int FA = 0, int FB = 0>
@@ -1586,6 +1681,9 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(GemmParams p) {
       epilogue_staged<EPI, 128, false>(p, acc, smem, m0, n0, wm, wn, lane);
     else
       epilogue<8, 4, SWAP, EPI>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
+    if constexpr (EPI == EPI_F32_STORE) {
+      if (p.sk_out) splitk_fixup(p, smem, tt, m0, n0);  // host: staged path (N % 4 == 0, no row groups)
+    }
   } else if constexpr (SWAP && (EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU)) {
     if (!p.epi_staged && direct_ok(p)) {
       // (one instance per epilogue actually reachable: a residual exists for BF16 only; a second,

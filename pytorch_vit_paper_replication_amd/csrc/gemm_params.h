@@ -49,6 +49,13 @@ struct GemmParams {
   int tail_max_units;
   // fewest K-tiles a split part may keep (default 12: measured on the K = 768 bf16 GEMMs)
   int tail_min_kt;
+  // in-launch split-K reduction of EPI_F32_STORE (weight gradients): with sk_out set, every split
+  // stores its partial slab write-through, arrives on its tile's counter (sk_cnt[2 tile], zero
+  // between launches), waits for the tile's other splits and then adds rows [256 z / S, 256 (z+1) / S)
+  // of the tile, summed over the S slabs in order 0..S-1, into sk_out (row stride sk_ldo; sk_acc = 0:
+  // overwrite). Needs every workgroup of the launch co-resident (host: tiles x splits <= CUs).
+  // sk_cnt[2 * sk_cnt_tiles] counts spin timeouts (0 in a healthy run).
+  float* sk_out; int64_t sk_ldo; unsigned* sk_cnt; int sk_acc; int sk_cnt_tiles;
 };
 
 }  // namespace pvr

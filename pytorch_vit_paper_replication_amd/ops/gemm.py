@@ -201,6 +201,22 @@ def wgrad_splits(T: int, N: int, K: int, tile: int = 0) -> int:
     return s
 
 
+# in-launch split-K reduction of the weight gradients (GemmParams::sk_*), opt-in (PVR_SPLITK_FIXUP=1):
+# measured slower than the separate splitk_reduce pass at every ViT-B/16 shape (fc1 0.253 vs 0.239 ms,
+# out 0.100 vs 0.084; b256 step 7384 vs 7439 img/s; profiles/r6/splitk/): each split's write-through
+# slab drain, the wait for its siblings and its 256 KiB of sc1 reads run at one CU's bandwidth,
+# while the separate pass streams every slab at full-chip bandwidth
+SPLITK_FIXUP = _os.environ.get("PVR_SPLITK_FIXUP", "0") != "0"
+_cus = None
+
+
+def _num_cus() -> int:
+    global _cus
+    if _cus is None:
+        _cus = int(_ext.ext().num_cus())
+    return _cus
+
+
 _workspaces = {}  # (device index, stream id) -> flat f32 split-K workspace
 
 
@@ -241,6 +257,12 @@ def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> torch.
     # patch sizes, kc = 3 * P * P odd, take the temporary below)
     if tile == 12 and nsplit > 1 and out.is_contiguous() and N % 4 == 0 and out.shape[-1] % 4 == 0:
         ws = _workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
+        if SPLITK_FIXUP and not narrow and math.ceil(N / 256) * math.ceil(K / 256) * nsplit <= _num_cus():
+            # in-launch reduction: each split adds 1/nsplit of its tile, summed over the slabs in a
+            # fixed order, into out (no separate reduce pass; deterministic)
+            ext.gemm(dy, False, x, False, ws, N, K, T, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0,
+                     None, 0, 0.0, ksplit, 14, reduce_out=out, reduce_acc=True)
+            return out
         ext.gemm(dy, False, x, False, ws, N, K, T, EPI_F32_STORE, None, None, None, 0, None, 0, 0, 0,
                  None, 0, 0.0, ksplit, 14)
         ext.splitk_reduce(ws, nsplit, out, True)

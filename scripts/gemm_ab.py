@@ -5,6 +5,7 @@ optionally A/B'd over a switch of ours, interleaved in one process (rounds x var
 
   python scripts/gemm_ab.py                     # ViT-B/16 batch 256 (T = 50432)
   python scripts/gemm_ab.py --ab tail           # split-K tail of the last dispatch round on / off
+  python scripts/gemm_ab.py --ab skfix --only wgrad   # weight gradients: in-launch split-K reduction on / off
   python scripts/gemm_ab.py --model vit_h14 --batch 256
 
 Prints one line per (GEMM, variant): median / min ms over the rounds, TFLOP/s, ratio vs hipBLASLt.
@@ -94,6 +95,9 @@ def main():
     variants = [("", lambda: None)]
     if a.ab == "tail":
         variants = [("tail on ", lambda: ext.set_gemm_tail(True)), ("tail off", lambda: ext.set_gemm_tail(False))]
+    elif a.ab == "skfix":
+        # weight gradients: in-launch split-K reduction vs the separate reduce pass
+        variants = [("skfix on", lambda: setattr(G, "SPLITK_FIXUP", True)), ("skfixoff", lambda: setattr(G, "SPLITK_FIXUP", False))]
     elif a.ab.startswith("tiles:"):
         # tiles:def,7,8 - the default tile selection vs forced tile configs (every case)
         def force(t):

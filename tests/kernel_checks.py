@@ -372,6 +372,33 @@ def check_gemm_wgrad(T, N, K, t=0):
     return (f"gemm_wgrad T{T} N{N} K{K} t{t}", worst((out, ref)), lim(1e-6, 4e-6))
 
 
+def check_gemm_wgrad_fixup(T, N, K):
+    """Weight gradient with the in-launch split-K reduction (each split adds 1/S of its tile, the
+    slabs summed in a fixed order): vs the fp32 product, accumulating into a non-zero out, bitwise
+    repeatable, no spin timeout; and vs the separate-reduce-pass path."""
+    ext = _ext.ext()
+    dy, x = bf(rnd(T, N)), bf(rnd(T, K))
+    init = rnd(N, K)
+    outs = []
+    prev = G.SPLITK_FIXUP
+    for fix in (True, True, False):
+        G.SPLITK_FIXUP = fix
+        try:
+            out = init.clone()
+            with tile(12):
+                G.linear_wgrad(dy, x, out)
+            outs.append(out)
+        finally:
+            G.SPLITK_FIXUP = prev
+    torch.cuda.synchronize()
+    timeouts = ext.splitk_timeouts(dy, True)
+    ref = init + dy.float().t() @ x.float()
+    m = worst((outs[0], ref), (outs[0], outs[2]))
+    m.update(repeat_differs=float(not torch.equal(outs[0], outs[1])), timeouts=float(timeouts))
+    # fp32 sums over 12k-50k tokens: the accumulation error of either order grows past the short-T 1e-6
+    return (f"gemm_wgrad in-launch split-K T{T} N{N} K{K}", m, lim(3e-6, 1e-5, repeat_differs=0, timeouts=0))
+
+
 def check_gemm_dropout(M=512, N=256, K=128, p=0.1, t=None):
     x, w = bf(torch.ones(M, K, device=DEV)), bf(torch.full((N, K), 1.0 / K, device=DEV))
     seed = torch.tensor([12345], dtype=torch.int64, device=DEV)
@@ -1557,6 +1584,10 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_gemm_dgelu(1000, 3072, 768, False, 12),
         lambda: check_gemm_wgrad(17, 64, 128),
         lambda: check_gemm_wgrad(3000, 768, 2304, 12),
+        lambda: check_gemm_wgrad_fixup(50432, 2304, 768),
+        lambda: check_gemm_wgrad_fixup(12000, 768, 768),
+        lambda: check_gemm_wgrad_fixup(5000, 3072, 768),
+        lambda: check_gemm_wgrad_fixup(3000, 1000, 200),
         lambda: check_gemm_wgrad(1000, 304, 200, 12),
         lambda: check_gemm_dropout(),
         lambda: check_gemm_dropout(1000, 768, 128, 0.1, 12),
