@@ -40,15 +40,17 @@ namespace {
 
 constexpr int EPI_BF16_ = 0, EPI_GELU_ = 1, EPI_DGELU_ = 2;  // = GemmEpi of gemm.hip
 
-// diagnostic ablations (timing only, wrong results): 1 = the epilogue waves only keep the barrier
-// count, 3 = and no hand-off (the MFMA waves alone)
 // 1: the MFMA waves raise their priority over their MFMA bursts (A/B knob)
 #ifndef PVR_WS_PRIO
 #define PVR_WS_PRIO 1
 #endif
+// diagnostic ablations (timing only, wrong results): 1 = the epilogue waves only keep the barrier
+// count, 3 = and no hand-off (the compiler then deletes the MFMAs too: DMA + barriers only), 4 = the
+// full epilogue math without its stores, 5 = the stores without the math
 #ifndef PVR_WS_ABL
 #define PVR_WS_ABL 0
 #endif
+constexpr bool WS_EPI_ON = PVR_WS_ABL == 0 || PVR_WS_ABL >= 4;
 
 constexpr int WS_BM = 256, WS_BN = 128;       // output tile (rows of A x rows of B)
 constexpr int WS_A = WS_BM * 64;              // A image of one K-step: [256 rows][32 k] bf16 = 16 KiB
@@ -342,7 +344,10 @@ PVR_DEV void ws_epi_pair(const GemmParams& p, WsEpi& E, WsBlock<NU>& B, uint32_t
       k1 = (h >> 16) >= p.drop_thr;
     }
   }
-  if constexpr (EPI == EPI_BF16_) {
+  if constexpr (PVR_WS_ABL == 5) {  // ablation: no epilogue math, the raw words stored
+    E.ow[P] = __float_as_uint(v0) ^ __float_as_uint(v1);
+    E.aw[P] = E.ow[P];
+  } else if constexpr (EPI == EPI_BF16_) {
     if (p.drop_thr) {
       v0 = k0 ? v0 * p.drop_scale : 0.f;
       v1 = k1 ? v1 * p.drop_scale : 0.f;
@@ -375,6 +380,7 @@ PVR_DEV void ws_epi_pair(const GemmParams& p, WsEpi& E, WsBlock<NU>& B, uint32_t
   // to the unit's store, re-forming one interval-sized lump
   asm volatile("" : "+v"(E.ow[P]));
   if constexpr (EPI == EPI_GELU_) asm volatile("" : "+v"(E.aw[P]));
+  if (PVR_WS_ABL == 4 && p.M > 0) return;  // ablation: all the math, no stores (runtime-opaque skip)
   if constexpr (P == 3) {
     const uint32_t vc = (JP ? E.vc1 : E.vc0) + (uint32_t)(I * 16 * E.ldc2);
     if constexpr (EPI == EPI_GELU_) {  // no aux (inference): 0-byte resource
@@ -477,7 +483,7 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
   for (int v = blockIdx.x; v < ntiles; v += gridDim.x) {
     // the MFMA waves run tile v; process tile vprev (if any) over the K loop's barrier intervals:
     // interval 0 loads its bias and first per-row inputs, piece x runs after barrier SPC (x + 1)
-    if (have && PVR_WS_ABL == 0) {
+    if (have && WS_EPI_ON) {
       WsEpi E;
       int m0, n0;
       ws_coords(p, vprev, m0, n0);
@@ -508,7 +514,7 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       ws_barrier();  // H1
-      if (PVR_WS_ABL == 0 && (R == 1 || (e >> 2) == r)) ws_get<F32, NU>(B, smem, G0, R == 1 ? e : e & 3, lane);
+      if (WS_EPI_ON && (R == 1 || (e >> 2) == r)) ws_get<F32, NU>(B, smem, G0, R == 1 ? e : e & 3, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       ws_barrier();  // H2
     }
@@ -517,7 +523,7 @@ __global__ void __launch_bounds__(1024, 1) gemm_ws_kernel(GemmParams p) {
   }
   // the last tile, after the MFMA waves have exited: no barriers needed beside them, except the
   // column-sum exchange between the epilogue waves themselves
-  if (have && PVR_WS_ABL == 0) {
+  if (have && WS_EPI_ON) {
     WsEpi E;
     int m0, n0;
     ws_coords(p, vprev, m0, n0);
