@@ -55,7 +55,8 @@ def run(path, args, init_sd, data):
     losses = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for s in range(args.steps):
+    # --stop-at: train only the first steps of the --steps schedule (mid-training comparisons)
+    for s in range(min(args.steps, getattr(args, "stop_at", 0) or args.steps)):
         lo = (s * args.batch) % xtr.shape[0]
         x, y = xtr[lo:lo + args.batch], ytr[lo:lo + args.batch]
         model.train()
@@ -126,6 +127,11 @@ def main():
     p.add_argument("--fp8-study", type=int, default=0, metavar="SEEDS",
                    help="seed study: SEEDS inits x {fused bf16, fp8 fwd+dgrad, fp8 fwd+dgrad+wgrad}; prints the "
                         "per-variant mean / spread of the final loss and held-out accuracy")
+    p.add_argument("--seed-start", type=int, default=0, help="seed study: first seed (studies split over runs)")
+    p.add_argument("--stop-at", type=int, default=0, help="train only this many steps of the --steps schedule")
+    p.add_argument("--checkpoints", default="", help="seed study: comma-separated steps whose windowed mean loss "
+                   "(the --window steps ending there) is recorded per run (JSON line '[ckpt] ...')")
+    p.add_argument("--window", type=int, default=20)
     args = p.parse_args()
     if args.fp8_study:
         return fp8_study(args)
@@ -181,7 +187,8 @@ def fp8_study(args):
     te = make_data(args.test_size, args.classes, args.image_size, gen, dev, templates)
     k = max(1, args.steps // 10)
     res = {v: [] for v in ("fused", "fused_fp8", "fused_fp8w")}
-    for seed in range(args.fp8_study):
+    ckpts = [int(c) for c in args.checkpoints.split(",") if c]
+    for seed in range(args.seed_start, args.seed_start + args.fp8_study):
         torch.manual_seed(seed)
         init_sd = {n: t.clone() for n, t in vit(args.model, image_size=args.image_size, num_classes=args.classes,
                                                mlp_dropout=args.dropout, embedding_dropout=args.dropout).state_dict().items()}
@@ -190,6 +197,10 @@ def fp8_study(args):
         for v in res:
             r = run(v, args, init_sd, data)
             res[v].append({"final_loss": sum(r["losses"][-k:]) / k, "test_acc": r["test_acc"], "test_loss": r["test_loss"]})
+            if ckpts:  # windowed mean loss ending at each checkpoint step (1-based)
+                w = {c: sum(r["losses"][c - args.window:c]) / args.window for c in ckpts if c <= len(r["losses"])}
+                print("[ckpt] " + json.dumps({"seed": seed, "variant": v, "window": args.window, "loss": w,
+                                              "train_s": r["train_s"]}), flush=True)
             print(f"[study] seed {seed} {v}: final loss {res[v][-1]['final_loss']:.4f} test acc {r['test_acc']:.3f} "
                   f"test loss {r['test_loss']:.4f}", flush=True)
 
