@@ -38,8 +38,10 @@ def parse():
     p.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                    help="fp8: encoder forward GEMMs in e4m3 with delayed scaling (ViT-H/14 fp8 config)")
     p.add_argument("--fp8-bf16-dgrad", action="store_true", help="fp8 mode: keep the dgrad GEMMs bf16 (A/B)")
+    p.add_argument("--fp8-bf16-wgrad", action="store_true",
+                   help="fp8 mode: keep the weight-gradient GEMMs bf16 (fp8 weight gradients are the default)")
     p.add_argument("--fp8-wgrad", action="store_true",
-                   help="fp8 mode: also the weight-gradient GEMMs in fp8 (opt-in: behind bf16 in the learning-phase study)")
+                   help="fp8 mode: fp8 weight gradients (the default since round 6; kept so older command lines parse)")
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
     p.add_argument("--force-ddp", action="store_true", help="wrap in DDP even with one process (exercises the comm path)")
     p.add_argument("--pg-only", action="store_true", help="initialise a world-1 RCCL process group but do not wrap in DDP (A/B)")
@@ -187,7 +189,7 @@ def main():
 
     model = vit(args.model, image_size=args.image_size, num_classes=args.num_classes).to(device)
     if args.dtype == "fp8":
-        model.enable_fp8(dgrad=not args.fp8_bf16_dgrad, wgrad=args.fp8_wgrad and not args.fp8_bf16_dgrad)
+        model.enable_fp8(dgrad=not args.fp8_bf16_dgrad, wgrad=not args.fp8_bf16_wgrad and not args.fp8_bf16_dgrad)
     groups = param_groups_weight_decay(model, 0.03)
     total_steps = args.warmup + args.steps
     if args.impl == "fused":
@@ -322,7 +324,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if args.dtype == "bf16" else (
                 "fp8 (e4m3 forward GEMMs; bf16 backward/attention/norms)" if args.fp8_bf16_dgrad else
-                "fp8 (e4m3 forward GEMMs, e5m2-gradient dgrad and wgrad GEMMs; bf16 attention/norms)" if args.fp8_wgrad else
+                "fp8 (e4m3 forward GEMMs, e5m2-gradient dgrad and wgrad GEMMs; bf16 attention/norms)" if not args.fp8_bf16_wgrad else
                 "fp8 (e4m3 forward GEMMs, e5m2-gradient dgrad GEMMs; bf16 wgrad/attention/norms)"),
             "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
                     "random-init weights)",

@@ -45,7 +45,7 @@ def run(path, args, init_sd, data):
                 mlp_dropout=args.dropout, embedding_dropout=args.dropout).to(dev)
     model.load_state_dict(init_sd)
     if path == "fused_fp8":
-        model.enable_fp8()  # e4m3 forward, e5m2-gradient dgrad GEMMs, delayed scaling (wgrad bf16)
+        model.enable_fp8(wgrad=False)  # e4m3 forward, e5m2-gradient dgrad GEMMs, delayed scaling (wgrad bf16)
     elif path == "fused_fp8w":
         model.enable_fp8(dgrad=True, wgrad=True)  # + e5m2 x e4m3 weight-gradient GEMMs
     groups = param_groups_weight_decay(model, 0.03)

@@ -43,7 +43,7 @@ def main():
             p = float(stats.ttest_rel(x, bb).pvalue) if len(x) > 1 else float("nan")
             within = abs(m - bm) <= bs
             out["rows"].append({"step": st, "variant": v, "mean": m, "std": sd, "bf16_mean": bm, "bf16_std": bs,
-                                "diff_mean": dm, "diff_std": dsd, "p_paired": p, "within_1sd": within})
+                                "diff_mean": dm, "diff_std": dsd, "p_paired": p, "within_1sd": bool(within)})
             print(f"| {st} | {v} | {m:.4f} +- {sd:.4f} | {bm:.4f} +- {bs:.4f} | {dm:+.4f} +- {dsd:.4f} | {p:.3f} | {'yes' if within else 'no'} |")
     print(json.dumps(out))
 

@@ -1096,7 +1096,7 @@ def check_vit_fp8(B=4):
     from pytorch_vit_paper_replication_amd.models import ViT
 
     torch.manual_seed(0)
-    mf = ViT(**_FP8_CFG).to(DEV).enable_fp8()
+    mf = ViT(**_FP8_CFG).to(DEV).enable_fp8(wgrad=False)
     mr = ViT(**_FP8_CFG).to(DEV)
     mr.load_state_dict(mf.state_dict())
     x = torch.rand(B * 4, 3, 64, 64, device=DEV)
@@ -1126,7 +1126,7 @@ def check_vit_fp8_bf16_skip(B=4, steps=4, image=64, images=None):
     res = []
     for skip in (True, False):
         torch.manual_seed(0)
-        m = ViT(**dict(_FP8_CFG, mlp_dropout=0.1, image_size=image)).to(DEV).enable_fp8()
+        m = ViT(**dict(_FP8_CFG, mlp_dropout=0.1, image_size=image)).to(DEV).enable_fp8(wgrad=False)
         opt = FusedAdam(m.parameters(), lr=1e-3)
         nimg = images or B * 64
         x = torch.rand(nimg, 3, image, image, device=DEV)
@@ -1167,7 +1167,7 @@ def check_vit_fp8_default_producers(images=64, steps=8):
     from pytorch_vit_paper_replication_amd.optim import FusedAdam
 
     torch.manual_seed(0)
-    m = ViT(**_FP8_CFG).to(DEV).enable_fp8()
+    m = ViT(**_FP8_CFG).to(DEV).enable_fp8(wgrad=False)
     x = torch.rand(images, 3, 64, 64, device=DEV)
     y = torch.randint(0, 10, (images,), device=DEV)
     opt = FusedAdam(m.parameters(), lr=1e-3)
@@ -1203,12 +1203,12 @@ def check_vit_fp8_dgrad(B=4):
     from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
 
     torch.manual_seed(0)
-    m = ViT(**_FP8_CFG).to(DEV).enable_fp8(dgrad=True)
+    m = ViT(**_FP8_CFG).to(DEV).enable_fp8(dgrad=True, wgrad=False)
     x = torch.rand(B * 64, 3, 64, 64, device=DEV)
     y = torch.randint(0, 10, (B * 64,), device=DEV)
 
     def run(dgrad_fp8: bool):
-        m.enable_fp8(dgrad=dgrad_fp8)  # same history / margin: keeps the calibrated scaling state
+        m.enable_fp8(dgrad=dgrad_fp8, wgrad=False)  # same history / margin: keeps the calibrated scaling state
         out = []
         fused_vit.DGRAD_TAP = lambda which, t: out.append((which, t.float().clone()))
         try:
@@ -1227,7 +1227,7 @@ def check_vit_fp8_dgrad(B=4):
         assert w == w2
         per.append((f"b{_FP8_CFG['num_transformer_layer'] - 1 - i // 4}.{names[w]}", errs(t, r)[0]))
     print("fp8 dgrad per-tensor rel-L2 vs bf16 dgrad: " + ", ".join(f"{n} {e:.3e}" for n, e in per))
-    m.enable_fp8(dgrad=True)
+    m.enable_fp8(dgrad=True, wgrad=False)
     losses, ok = _train_losses(m, x, y)
     met = {"l2": max(e for _, e in per), "loss_not_falling": float(not ok or len(per) != 4 * _FP8_CFG["num_transformer_layer"])}
     return (f"vit fp8 dgrad per-tensor vs bf16 dgrad, loss {losses[0]:.3f}->{losses[-1]:.3f}", met,
