@@ -170,3 +170,20 @@ def use_fused(t: torch.Tensor) -> bool:
         return False
     ext()  # raises with the load error
     return False
+
+
+def free_scratch() -> None:
+    """Return the extension's per-(device, stream) scratch buffers to the caching allocator: the
+    split-K GEMM workspaces and tail slabs, the deterministic-mode partial rows, the attention
+    backward's dQ accumulator and scratch (up to ~0.9 GB per layer size at ViT-L/16 384 px). Waits
+    for the device first; the next fused call re-creates what it needs. Call it before
+    ``torch.cuda.empty_cache()`` when switching model sizes in one process."""
+    m = _C if _TRIED else load()
+    if m is None:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    m.free_scratch()
+    from .ops import gemm as _gemm
+
+    _gemm._workspaces.clear()

@@ -87,6 +87,20 @@ int pvr_attn_bwd_q8_ok(int, int);
 namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// Per-(device, stream) scratch caches are keyed by the stream's id (a pooled raw handle can be
+// reused by a different stream) and live in heap maps that free_scratch() empties (never in
+// static-storage destructors, which would run after the HIP runtime's teardown).
+using ScratchKey = std::pair<int, int64_t>;
+ScratchKey scratch_key(int dev) { return std::make_pair(dev, (int64_t)c10::hip::getCurrentHIPStream().id()); }
+template <class T>
+std::map<ScratchKey, T>& scratch_map() {
+  static auto* m = new std::map<ScratchKey, T>();
+  return *m;
+}
+struct SkCounters { torch::Tensor t; };
+struct DetWs { torch::Tensor t; };
+struct DqWs { torch::Tensor t; };
+struct AttnWs { torch::Tensor t; };
 
 // compute units of the current device (the persistent kernels' grid)
 int num_cus() {
@@ -141,8 +155,8 @@ struct TailBufs {
 };
 void attach_tail(pvr::GemmParams& p, const torch::Tensor& like) {
   if (!g_gemm_tail) return;
-  static std::map<std::pair<int, hipStream_t>, TailBufs> bufs;
-  const auto key = std::make_pair((int)like.get_device(), stream());
+  auto& bufs = scratch_map<TailBufs>();
+  const auto key = scratch_key((int)like.get_device());
   auto it = bufs.find(key);
   if (it == bufs.end()) {
     const int64_t cus = num_cus();
@@ -162,11 +176,11 @@ void set_gemm_tail(bool on) { g_gemm_tail = on; }
 // per output tile plus a timeout count, zeroed once; every launch leaves the tile words zero.
 constexpr int g_sk_tiles = 4096;
 torch::Tensor& splitk_counters(const torch::Tensor& like) {
-  static std::map<std::pair<int, hipStream_t>, torch::Tensor> bufs;
-  const auto key = std::make_pair((int)like.get_device(), stream());
+  auto& bufs = scratch_map<SkCounters>();
+  const auto key = scratch_key((int)like.get_device());
   auto it = bufs.find(key);
-  if (it == bufs.end()) it = bufs.emplace(key, torch::zeros({2 * g_sk_tiles + 4}, like.options().dtype(torch::kInt32))).first;
-  return it->second;
+  if (it == bufs.end()) it = bufs.emplace(key, SkCounters{torch::zeros({2 * g_sk_tiles + 4}, like.options().dtype(torch::kInt32))}).first;
+  return it->second.t;
 }
 // spin timeouts of the in-launch split-K reduction on the current stream (0 unless a split's
 // workgroups were not co-resident); reset = true zeroes the count
@@ -192,13 +206,9 @@ void set_deterministic(bool on) { g_deterministic = on; }
 bool deterministic() { return g_deterministic; }
 // partial-row scratch of the deterministic reductions, one per (device, stream), grown on demand
 float* det_scratch(int64_t numel, const torch::TensorOptions& opts) {
-  static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
-  torch::Tensor*& t = cache[std::make_pair((int)opts.device().index(), stream())];
-  if (!t || t->numel() < numel) {
-    delete t;
-    t = new torch::Tensor(torch::empty({numel}, opts.dtype(torch::kFloat32)));
-  }
-  return t->data_ptr<float>();
+  DetWs& d = scratch_map<DetWs>()[scratch_key((int)opts.device().index())];
+  if (!d.t.defined() || d.t.numel() < numel) d.t = torch::empty({numel}, opts.dtype(torch::kFloat32));
+  return d.t.data_ptr<float>();
 }
 
 // C = A . B^T with the given operand layouts; see csrc/gemm.hip for the epilogue contract.
@@ -945,31 +955,34 @@ void attn_dbias_reduce(torch::Tensor part, int64_t B, int64_t H, torch::Tensor d
 // drop = true: forget the cached accumulator of this (device, stream) (after a failed backward, whose
 // partial sums it may still hold); the next call re-creates it with torch::zeros.
 torch::Tensor dq_workspace(int64_t numel, const torch::TensorOptions& opts, bool drop = false) {
-  static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
-  const auto key = std::make_pair((int)opts.device().index(), stream());
-  torch::Tensor*& t = cache[key];
+  DqWs& d = scratch_map<DqWs>()[scratch_key((int)opts.device().index())];
   if (drop) {
-    delete t;
-    t = nullptr;
+    d.t = torch::Tensor();
     return torch::Tensor();
   }
-  if (!t || t->numel() < numel) {
-    delete t;  // stream-ordered reuse of its memory by the caching allocator
-    t = new torch::Tensor(torch::zeros({numel}, opts.dtype(torch::kFloat32)));
-  }
-  return *t;
+  // (a replaced tensor's memory returns to the caching allocator, stream-ordered)
+  if (!d.t.defined() || d.t.numel() < numel) d.t = torch::zeros({numel}, opts.dtype(torch::kFloat32));
+  return d.t;
 }
 
 // Scratch of the generic attention backward, one per (device, stream), grown to the largest request
 // (never freed: see dq_workspace). Calls on one stream are serialised, so they share it.
 torch::Tensor attn_scratch(int64_t numel, const torch::TensorOptions& opts) {
-  static std::map<std::pair<int, hipStream_t>, torch::Tensor*> cache;
-  torch::Tensor*& t = cache[std::make_pair((int)opts.device().index(), stream())];
-  if (!t || t->numel() < numel) {
-    delete t;
-    t = new torch::Tensor(torch::empty({numel}, opts.dtype(torch::kFloat32)));
-  }
-  return *t;
+  AttnWs& d = scratch_map<AttnWs>()[scratch_key((int)opts.device().index())];
+  if (!d.t.defined() || d.t.numel() < numel) d.t = torch::empty({numel}, opts.dtype(torch::kFloat32));
+  return d.t;
+}
+
+// Release every per-(device, stream) scratch buffer above (split tails, split-K counters,
+// deterministic partial rows, the attention backward's dQ accumulator and scratch) to the caching
+// allocator. The caller makes sure no kernel still uses them (ops: _ext.free_scratch synchronizes
+// first); the next call on a stream re-creates what it needs (counters zeroed again).
+void free_scratch() {
+  scratch_map<TailBufs>().clear();
+  scratch_map<SkCounters>().clear();
+  scratch_map<DetWs>().clear();
+  scratch_map<DqWs>().clear();
+  scratch_map<AttnWs>().clear();
 }
 
 // R > 0: for the standard layouts of this shape (qkv [T][3D], dO / O [T][D]) the backward emits the
@@ -1106,6 +1119,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_timeouts", &splitk_timeouts, py::arg("like"), py::arg("reset") = false);
   m.def("num_cus", &num_cus);
   m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("free_scratch", &free_scratch);
   m.def("layernorm_fwd_q8", &layernorm_fwd_q8);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("dy_stride"), py::arg("x"), py::arg("x_stride"),
         py::arg("mean"), py::arg("rstd"), py::arg("w"), py::arg("dres"), py::arg("dres_stride"), py::arg("dx"),

@@ -630,3 +630,59 @@ def test_deterministic_mode_gradients_bitwise_repeatable():
     assert not _ext.ext().deterministic()
     for (n, _), a, b in zip(m.named_parameters(), g1, g2):
         assert torch.equal(a, b), n
+
+
+def _det_model_and_batch():
+    from pytorch_vit_paper_replication_amd.models import ViT
+
+    torch.manual_seed(0)
+    m = ViT(**dict(CFG, image_size=128, embedding_dim=256, num_heads=4, mlp_size=1024, mlp_dropout=0.0,
+                   embedding_dropout=0.0)).cuda()
+    x = torch.rand(64, 3, 128, 128, device="cuda")
+    y = torch.randint(0, 10, (64,), device="cuda")
+    return m, x, y
+
+
+def _grads(m, x, y):
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+
+    m.zero_grad(set_to_none=False)
+    cross_entropy(m(x), y).backward()
+    torch.cuda.synchronize()
+    return [p.grad.detach().clone() for p in m.parameters()]
+
+
+def test_torch_deterministic_algorithms_covers_the_first_step():
+    """torch.use_deterministic_algorithms(True) switched on before any fused backward (no
+    deterministic_mode(), no env var): the native flag is synced at the first backward kernel
+    (HeadFn.backward), so already the first step's gradients are bitwise repeatable."""
+    from pytorch_vit_paper_replication_amd import _ext
+
+    _ext.ext().set_deterministic(False)
+    m, x, y = _det_model_and_batch()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        g1 = _grads(m, x, y)
+        assert _ext.ext().deterministic()
+        g2 = _grads(m, x, y)
+    finally:
+        torch.use_deterministic_algorithms(False)
+    _grads(m, x, y)  # the next backward syncs the flag back off
+    assert not _ext.ext().deterministic()
+    for (n, _), a, b in zip(m.named_parameters(), g1, g2):
+        assert torch.equal(a, b), n
+
+
+def test_free_scratch_releases_and_recreates():
+    """_ext.free_scratch() drops every per-stream scratch buffer (split-K workspaces, tail slabs,
+    deterministic partial rows, attention scratch); the next step re-creates them and, in
+    deterministic mode, reproduces the gradients bit for bit."""
+    from pytorch_vit_paper_replication_amd import _ext
+
+    m, x, y = _det_model_and_batch()
+    with _ext.deterministic_mode():
+        g1 = _grads(m, x, y)
+        _ext.free_scratch()
+        g2 = _grads(m, x, y)
+    for (n, _), a, b in zip(m.named_parameters(), g1, g2):
+        assert torch.equal(a, b), n
