@@ -13,7 +13,13 @@
 //   4: mode 1 issued by the 4 waves of group 0 only (4 DMAs each), group 1 none;
 //   5: mode 1 with every workgroup reading the same 64 KiB (cache-hot: the issue / TA cost alone);
 //   6: mode 1 with 4 phases in flight (vmcnt 8, 5-slot ring);
-//   7: mode 1 with each workgroup streaming its own contiguous range (sequential 16 KiB per phase).
+//   7: mode 1 with each workgroup streaming its own contiguous range (sequential 16 KiB per phase);
+//   8: the GEMM's own operand pattern: per K-tile (4 phases) 256 A rows then 256 B rows of 128 B
+//      (K = 768: 1536-B row stride), A tile = the workgroup's 256-row block of a 50432 x 768 matrix,
+//      B tile = one of 3 256-row blocks of a 768 x 768 matrix, every workgroup at the same K-tile;
+//   9: mode 8 with each workgroup starting its K loop at K-tile (id mod 12) (rotated start);
+//  10: mode 8 with the ping-pong's uneven fragment reads: 12 / 4 / 8 / 0 per phase (A0 + B0, B1,
+//      A1, none) instead of 6 each.
 // Prints TFLOP/s of the MFMAs and the DMA bandwidth.
 #include <hip/hip_runtime.h>
 
@@ -60,6 +66,20 @@ __global__ void __launch_bounds__(512, 1) probe(const uint16_t* src, unsigned sr
   const bool issuer = MODE != 4 || grp == 0;
   auto issue = [&](int it) {
     if (!issuer) return;
+    if constexpr (MODE == 8 || MODE == 9 || MODE == 10) {  // GEMM operand pattern (see the header)
+      const int kt = ((it >> 2) + (MODE == 9 ? (int)blockIdx.x : 0)) % 12, ph = it & 3;
+      const unsigned rowb = ph < 2 ? (unsigned)(blockIdx.x % 197) * 256u + (unsigned)ph * 128u
+                                   : (unsigned)(blockIdx.x % 3) * 256u + (unsigned)(ph - 2) * 128u;
+      const unsigned base = ph < 2 ? 0u : (96u << 20);
+#pragma unroll
+      for (int i = 0; i < NDMA; ++i) {
+        const unsigned row = rowb + (unsigned)(2 * wave + i) * 8u + (unsigned)(lane >> 3);
+        const unsigned off = base + row * 1536u + (unsigned)kt * 128u + (unsigned)(lane & 7) * 16u;
+        char* dst = smem + RING + (it % NSLOT) * SLOT + (2 * wave + i) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)dst, 16, off, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) {
       const unsigned piece = (unsigned)(it * 16 + (MODE == 4 ? 4 * wave + i : 2 * wave + i));  // 1 KiB pieces, 16 per phase
@@ -71,10 +91,34 @@ __global__ void __launch_bounds__(512, 1) probe(const uint16_t* src, unsigned sr
   };
   for (int it = 0; it < iters; ++it) {
     const char* fr = smem + FRAG + (it & 3) * 12288;  // 4 x 12 KiB: [0, 48 KiB)
+    if constexpr (MODE == 10) {  // 12 / 4 / 8 / 0 reads (a: 4 x 2 k-steps, b: 2 x 2 in phase 0)
+      const int ph = it & 3;
+      if (ph == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *(const __attribute__((address_space(3))) v8s*)(fr + i * 1024 + lane * 16);
+        for (int i = 0; i < 4; ++i) a[i] = *(const __attribute__((address_space(3))) v8s*)(fr + i * 1024 + lane * 16);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = *(const __attribute__((address_space(3))) v8s*)(fr + 4096 + j * 1024 + lane * 16);
+        for (int i = 0; i < 4; ++i) a[i] ^= *(const __attribute__((address_space(3))) v8s*)(fr + 6144 + i * 1024 + lane * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = *(const __attribute__((address_space(3))) v8s*)(fr + 4096 + j * 1024 + lane * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] ^= *(const __attribute__((address_space(3))) v8s*)(fr + 10240 + j * 1024 + lane * 16);
+      } else if (ph == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = *(const __attribute__((address_space(3))) v8s*)(fr + 4096 + j * 1024 + lane * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] ^= *(const __attribute__((address_space(3))) v8s*)(fr + 10240 + j * 1024 + lane * 16);
+      } else if (ph == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const __attribute__((address_space(3))) v8s*)(fr + i * 1024 + lane * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] ^= *(const __attribute__((address_space(3))) v8s*)(fr + 6144 + i * 1024 + lane * 16);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *(const __attribute__((address_space(3))) v8s*)(fr + i * 1024 + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = *(const __attribute__((address_space(3))) v8s*)(fr + 4096 + j * 1024 + lane * 16);
+    }
     if constexpr (MODE != 0 && MODE != 3) issue(it);
     if constexpr (MODE != 0) {
       if (issuer) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH * NDMA) : "memory");  // the group DEPTH phases ago landed
@@ -148,6 +192,9 @@ int main() {
     if (run<5>("5 DMA 2/wave, one shared 64 KiB (hot)", cus, src, bytes, iters, sink)) return 1;
     if (run<6>("6 DMA 2/wave, 4 phases in flight", cus, src, bytes, iters, sink)) return 1;
     if (run<7>("7 DMA 2/wave, sequential per workgroup", cus, src, bytes, iters, sink)) return 1;
+    if (run<8>("8 GEMM operand pattern (K 768)", cus, src, bytes, iters, sink)) return 1;
+    if (run<9>("9 GEMM operand pattern, rotated K start", cus, src, bytes, iters, sink)) return 1;
+    if (run<10>("10 GEMM pattern, reads 12/4/8/0 per phase", cus, src, bytes, iters, sink)) return 1;
   }
   CHECK(hipFree(src));
   CHECK(hipFree(sink));
