@@ -319,33 +319,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
 
 // ------------------------------------------------------------- forward: whole head in LDS
 // N <= 256 and dh = 64 (ViT-B/16 and ViT-L/16 at 224 px: N = 197). One persistent workgroup per
-// CU walks a contiguous range of (batch, head) pairs with ceil(N/16) waves of 16 queries. Every
-// key of a head fits in LDS, so
+// CU walks a contiguous range of (batch, head) pairs; wave w owns QF 16-query fragments (queries
+// 16 QF w .. 16 QF w + 16 QF - 1) against every key of the head. Every key of a head fits in LDS, so
 //   * each query row's softmax is exact in one pass (no running max, no rescaling of O);
 //   * the head's K/V are staged once instead of once per 64-query workgroup;
 //   * the next pair's K/V LDS-DMA (second buffer) and Q fragments are in flight under this pair's
 //     math, and its O rows are stored one pair late, so no store sits in front of a DMA wait.
+// Every wave reads the whole K and V^T images (54 KiB at N = 197) per pair. QF = 2 feeds each
+// fragment read to two MFMAs, halving that LDS read traffic, but with 7 instead of 13 waves it
+// measured slower (0.086 vs 0.079 ms at ViT-B/16 b256, step unchanged: profiles/r6/attn_hqf/): the
+// kernel is latency-, not LDS-bound. QF = 1 is the default; PVR_ATTN_HEAD_QF / set_attn_fwd_head_qf.
 // Key rows past N (padding to a multiple of 32 for the P.V k-steps) read as zero.
-template <int NF>
-__global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
-                                                              uint16_t* __restrict__ out, int64_t ld_o,
-                                                              float* __restrict__ lse, int N, int H, int D,
-                                                              int npairs, float scale) {
+template <int NF, int QF>
+__global__ void __launch_bounds__(((NF + QF - 1) / QF) * 64) attn_fwd_head_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
+                                                                                uint16_t* __restrict__ out, int64_t ld_o,
+                                                                                float* __restrict__ lse, int N, int H, int D,
+                                                                                int npairs, float scale) {
   constexpr int DH = 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NP = 32 * ((NF + 1) / 2);  // staged key rows
   constexpr int BUF = 2 * NP * 128;         // K | V images of one (batch, head)
-  constexpr int NW = NF;
+  constexpr int NW = (NF + QF - 1) / QF;    // waves
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, li = lane & 15;
-  constexpr int nf = NF;  // 16-key fragments holding a valid key, one wave each
-  PVR_ASSERT((N + 15) / 16 == NF && blockDim.x == NF * 64 && (int)gridDim.x <= npairs);
+  constexpr int nf = NF;  // 16-key fragments holding a valid key
+  PVR_ASSERT((N + 15) / 16 == NF && blockDim.x == NW * 64 && (int)gridDim.x <= npairs);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int per = npairs / gridDim.x, rem = npairs % gridDim.x;
   const int p0 = L * per + min(L, rem);
   const int p1 = p0 + per + (L < rem ? 1 : 0);
-  const int qrow = min(wave * 16 + li, N - 1);
+  int qrow[QF];
+#pragma unroll
+  for (int j = 0; j < QF; ++j) qrow[j] = min((QF * wave + j) * 16 + li, N - 1);
   const uint32_t extent = clamp_bytes(((int64_t)(N - 1) * ld + DH) * 2);
   const float c = scale * LOG2E;
 
@@ -354,20 +360,23 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
     dma_rows<1>(make_rsrc(base + D, extent), buf, NP, ld, 0, wave, NW, lane);
     dma_rows<1>(make_rsrc(base + 2 * D, extent), buf + NP * 128, NP, ld, 0, wave, NW, lane);
   };
-  auto load_q = [&](int pr, v8s (&qf)[2]) {
-    const uint16_t* qp = qkv + ((int64_t)(pr / H) * N + qrow) * ld + (pr % H) * DH + 8 * g;
-    qf[0] = *(const v8s*)qp;
-    qf[1] = *(const v8s*)(qp + 32);
+  auto load_q = [&](int pr, v8s (&qf)[QF][2]) {
+#pragma unroll
+    for (int j = 0; j < QF; ++j) {
+      const uint16_t* qp = qkv + ((int64_t)(pr / H) * N + qrow[j]) * ld + (pr % H) * DH + 8 * g;
+      qf[j][0] = *(const v8s*)qp;
+      qf[j][1] = *(const v8s*)(qp + 32);
+    }
   };
-  // O^T layout: lane holds O[q = 16 wave + li][d = 16e + 4g + r]. Stores go through range-checked
-  // buffer resources: a lane with nothing to write gets an offset past the extent and its store is
-  // dropped, so every wave issues exactly STORES store instructions per pair and the loop's wait
-  // below can retire the DMAs issued before them without waiting for the stores.
-  constexpr int STORES = 5;
+  // O^T layout: lane holds O[q = 16 (QF wave + j) + li][d = 16e + 4g + r]. Stores go through
+  // range-checked buffer resources: a lane with nothing to write gets an offset past the extent and
+  // its store is dropped, so every wave issues exactly STORES store instructions per pair and the
+  // loop's wait below can retire the DMAs issued before them without waiting for the stores.
+  constexpr int STORES = 5 * QF;
   const uint32_t o_extent = clamp_bytes(((int64_t)(N - 1) * ld_o + DH) * 2);
-  auto store_o = [&](int pr, const v4f (&o)[4], float m, float l) {
+  auto store_o = [&](int pr, int j, const v4f (&o)[4], float m, float l) {
     typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-    const int q = wave * 16 + li;
+    const int q = (QF * wave + j) * 16 + li;
     const bool ok = q < N;
     const float inv = 1.f / l;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(out + (int64_t)(pr / H) * N * ld_o + (pr % H) * DH, o_extent);
@@ -383,12 +392,13 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
   };
 
   if (p0 >= p1) return;  // uniform: the host launches at most npairs workgroups
-  v8s qf[2], qn[2];
+  v8s qf[QF][2], qn[QF][2];
   issue(p0, smem);
   load_q(p0, qf);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  asm volatile("" : "+v"(qf[0]), "+v"(qf[1]));
+#pragma unroll
+  for (int j = 0; j < QF; ++j) asm volatile("" : "+v"(qf[j][0]), "+v"(qf[j][1]));
   for (int pr = p0; pr < p1; ++pr) {
     const int it = pr - p0;
     const char* kimg = smem + (it & 1) * BUF;
@@ -397,37 +407,49 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
       issue(pr + 1, smem + ((it + 1) & 1) * BUF);
       load_q(pr + 1, qn);
     }
-    // S^T[key][q] = K . Q^T: the query on the MFMA lane, keys down the accumulator rows
-    v4f s[16];
+    // S^T[key][q] = K . Q^T: the query on the MFMA lane, keys down the accumulator rows; each K
+    // fragment read feeds the wave's QF query fragments
+    v4f s[QF][16];
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
-      s[f] = v4f{0.f, 0.f, 0.f, 0.f};
-      if (f < nf) {
-        s[f] = mfma16(frag_rows(kimg, NP, 16 * f, 0, lane), qf[0], s[f]);
-        s[f] = mfma16(frag_rows(kimg, NP, 16 * f, 1, lane), qf[1], s[f]);
-      }
-    }
-    float mx = -INFINITY;
 #pragma unroll
-    for (int f = 0; f < 16; ++f) {
-      if (f == nf - 1) {  // keys >= N live only in the last valid fragment
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (16 * f + 4 * g + r >= N) s[f][r] = -INFINITY;
-      }
+      for (int j = 0; j < QF; ++j) s[j][f] = v4f{0.f, 0.f, 0.f, 0.f};
       if (f < nf) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[f][r]);
+        for (int ks = 0; ks < 2; ++ks) {
+          const v8s kf = frag_rows(kimg, NP, 16 * f, ks, lane);
+#pragma unroll
+          for (int j = 0; j < QF; ++j) s[j][f] = mfma16(kf, qf[j][ks], s[j][f]);
+        }
       }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m = mx * c;  // scaled log2 units (c > 0)
-    float l = 0.f;
-    v4f o[4];
+    float m[QF], l[QF];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = v4f{0.f, 0.f, 0.f, 0.f};
-    // O^T[d][q] += V^T[d][key] P^T[key][q], 32 keys per k-step
+    for (int j = 0; j < QF; ++j) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int f = 0; f < 16; ++f) {
+        if (f == nf - 1) {  // keys >= N live only in the last valid fragment
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (16 * f + 4 * g + r >= N) s[j][f][r] = -INFINITY;
+        }
+        if (f < nf) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[j][f][r]);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      m[j] = mx * c;  // scaled log2 units (c > 0)
+      l[j] = 0.f;
+    }
+    v4f o[QF][4];
+#pragma unroll
+    for (int j = 0; j < QF; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[j][e] = v4f{0.f, 0.f, 0.f, 0.f};
+    // O^T[d][q] += V^T[d][key] P^T[key][q], 32 keys per k-step; each V^T fragment read feeds QF MFMAs
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       if (2 * kk < nf) {
@@ -435,39 +457,56 @@ __global__ void __launch_bounds__(NF * 64) attn_fwd_head_kernel(const uint16_t* 
         v4s vlo[4], vhi[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) frag_tr_async(vimg, NP, 32 * kk + 4 * g, 32 * kk + 16 + 4 * g, 16 * e, lane, vlo[e], vhi[e]);
-        v4f pa, pb = v4f{0.f, 0.f, 0.f, 0.f};
+        v8s pf[QF];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pa[r] = __builtin_amdgcn_exp2f(fmaf(s[2 * kk][r], c, -m));
-          l += pa[r];
-        }
-        if (2 * kk + 1 < nf) {
+        for (int j = 0; j < QF; ++j) {
+          v4f pa, pb = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            pb[r] = __builtin_amdgcn_exp2f(fmaf(s[2 * kk + 1][r], c, -m));
-            l += pb[r];
+            pa[r] = __builtin_amdgcn_exp2f(fmaf(s[j][2 * kk][r], c, -m[j]));
+            l[j] += pa[r];
           }
+          if (2 * kk + 1 < nf) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              pb[r] = __builtin_amdgcn_exp2f(fmaf(s[j][2 * kk + 1][r], c, -m[j]));
+              l[j] += pb[r];
+            }
+          }
+          pf[j] = pack_p(pa, pb);
         }
-        const v8s pf = pack_p(pa, pb);
         lds_wait();
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = mfma16(cat44(vlo[e], vhi[e]), pf, o[e]);
+        for (int e = 0; e < 4; ++e) {
+          const v8s vf = cat44(vlo[e], vhi[e]);
+#pragma unroll
+          for (int j = 0; j < QF; ++j) o[j][e] = mfma16(vf, pf[j], o[j][e]);
+        }
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    store_o(pr, o, m, l);
+#pragma unroll
+    for (int j = 0; j < QF; ++j) {
+      l[j] += __shfl_xor(l[j], 16, 64);
+      l[j] += __shfl_xor(l[j], 32, 64);
+      store_o(pr, j, o[j], m[j], l[j]);
+    }
     // everything but this pair's stores has landed (the next pair's K/V images and Q fragments),
     // and every wave is done reading this buffer before the pair after next restages it
-    static_assert(STORES == 5, "the vmcnt below counts store_o's store instructions");
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    static_assert(STORES == 5 * QF && (QF == 1 || QF == 2), "the vmcnt below counts store_o's store instructions");
+    if constexpr (QF == 1)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     __syncthreads();
-    qf[0] = qn[0];
-    qf[1] = qn[1];
-    // re-define qf through an empty asm: the compiler's own wait for these loads then sits here
-    // (already satisfied) instead of in front of the next pair's first MFMA, where it would also
-    // wait for that pair's K/V prefetch
-    asm volatile("" : "+v"(qf[0]), "+v"(qf[1]));
+#pragma unroll
+    for (int j = 0; j < QF; ++j) {
+      qf[j][0] = qn[j][0];
+      qf[j][1] = qn[j][1];
+      // re-define qf through an empty asm: the compiler's own wait for these loads then sits here
+      // (already satisfied) instead of in front of the next pair's first MFMA, where it would also
+      // wait for that pair's K/V prefetch
+      asm volatile("" : "+v"(qf[j][0]), "+v"(qf[j][1]));
+    }
   }
 }
 
@@ -1657,22 +1696,34 @@ static int device_cus() {
 }
 
 // whole-head kernel: one persistent workgroup per CU (its double-buffered K/V images take up to
-// 128 KiB of LDS), ceil(N/16) waves
-template <int NF>
-static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
-                                       int H, int D, float scale, hipStream_t s) {
+// 128 KiB of LDS), ceil(N / (16 QF)) waves. g_attn_fwd_head_qf: query fragments per wave (A/B,
+// default 1).
+#ifndef PVR_ATTN_HEAD_QF
+#define PVR_ATTN_HEAD_QF 1
+#endif
+int g_attn_fwd_head_qf = PVR_ATTN_HEAD_QF;
+template <int NF, int QF>
+static hipError_t attn_fwd_head_launch_qf(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
+                                          int H, int D, float scale, hipStream_t s) {
   using namespace pvr;
   constexpr int SMEM = 2 * 2 * 32 * ((NF + 1) / 2) * 128;
+  constexpr int NW = (NF + QF - 1) / QF;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)attn_fwd_head_kernel<NF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
+    const hipError_t e = hipFuncSetAttribute((const void*)attn_fwd_head_kernel<NF, QF>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int npairs = B * H;
   const int grid = npairs < device_cus() ? npairs : device_cus();
-  hipLaunchKernelGGL(attn_fwd_head_kernel<NF>, dim3(grid), dim3(NF * 64), SMEM, s, qkv, ld, out, ld_o, lse, N, H, D, npairs, scale);
+  hipLaunchKernelGGL((attn_fwd_head_kernel<NF, QF>), dim3(grid), dim3(NW * 64), SMEM, s, qkv, ld, out, ld_o, lse, N, H, D, npairs, scale);
   return hipGetLastError();
+}
+template <int NF>
+static hipError_t attn_fwd_head_launch(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
+                                       int H, int D, float scale, hipStream_t s) {
+  return g_attn_fwd_head_qf == 2 ? attn_fwd_head_launch_qf<NF, 2>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s)
+                                 : attn_fwd_head_launch_qf<NF, 1>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, s);
 }
 
 // Tiled forward launch: QG query groups per wave, KT keys per tile, dynamic LDS for two K/V stages.
@@ -1747,6 +1798,7 @@ extern "C" void pvr_set_attn_dbg(void* p) {
 }
 
 extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg == 1 || qg == 2 ? qg : 0; }
+extern "C" void pvr_set_attn_fwd_head_qf(int qf) { g_attn_fwd_head_qf = qf == 2 ? 2 : 1; }
 
 // seed (optional): attention-probability dropout with keep threshold thr16 (see AttnDrop); the
 // backward must get the same seed / seed_off / thr16

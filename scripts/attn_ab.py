@@ -44,6 +44,8 @@ def main():
     variants = [("", lambda: None)]
     if a.ab == "fwd_qg":
         variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1))]
+    elif a.ab == "hqf":
+        variants = [("hqf2", lambda: ext.set_attn_fwd_head_qf(2)), ("hqf1", lambda: ext.set_attn_fwd_head_qf(1))]
     res = {}
     data = {}
     for name in a.shapes.split(","):
@@ -62,6 +64,7 @@ def main():
             if a.bwd:
                 res.setdefault((name, "bwd", ""), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
     ext.set_attn_fwd_qg(0)
+    ext.set_attn_fwd_head_qf(1)
     for name in a.shapes.split(","):
         B, N, H, dh = SHAPES[name]
         fl = 4.0 * B * H * N * N * dh

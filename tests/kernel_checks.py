@@ -602,6 +602,26 @@ def check_attn_fwd(B, N, H, dh=64):
     return (f"attn_fwd B{B} N{N} H{H} dh{dh}", m, lim(4.5e-3, 6e-3, lse_l2=1.5e-7, lse_max=3e-7))
 
 
+def check_attn_fwd_head_qf(B, N, H):
+    """Whole-head forward (dh 64, N <= 256) with 2 query fragments per wave (the A/B form) vs 1 (the
+    default): per query the same MFMA sequence, so bitwise equal outputs; and vs fp32."""
+    ext = _ext.ext()
+    D = H * 64
+    qkv = bf(rnd(B * N, 3 * D))
+    try:
+        ext.set_attn_fwd_head_qf(1)
+        o1, l1 = ext.attn_fwd(qkv, B, N, H, 0.125)
+        ext.set_attn_fwd_head_qf(2)
+        o2, l2 = ext.attn_fwd(qkv, B, N, H, 0.125)
+    finally:
+        ext.set_attn_fwd_head_qf(1)
+    oref, lref = _attn_ref(qkv, B, N, H)
+    m = worst((o2, oref))
+    m["lse_l2"], m["lse_max"] = errs(l2, lref)
+    m["qf_differs"] = float(not (torch.equal(o1, o2) and torch.equal(l1, l2)))
+    return (f"attn_fwd whole-head QF 2 vs 1, B{B} N{N} H{H}", m, lim(4.5e-3, 6e-3, lse_l2=1.5e-7, lse_max=3e-7, qf_differs=0))
+
+
 def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
     """dQ|dK|dV (and the fused in_proj bias gradient) vs autograd of the fp32 reference."""
     ext = _ext.ext()
@@ -1606,6 +1626,9 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_layernorm_linked(5000, 768),
         lambda: check_layernorm_linked(777, 1280),
         lambda: check_layernorm_linked(1000, 1024),
+        lambda: check_attn_fwd_head_qf(4, 197, 12),
+        lambda: check_attn_fwd_head_qf(3, 17, 2),
+        lambda: check_attn_fwd_head_qf(2, 256, 4),
         lambda: check_attn_fwd(2, 197, 3),
         lambda: check_attn_fwd(1, 17, 2),
         lambda: check_attn_fwd(1, 577, 2),
