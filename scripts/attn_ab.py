@@ -17,7 +17,8 @@ import torch
 sys.path.insert(0, os.environ.get("PVR_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # PVR_PKG_ROOT: an A/B build
 from pytorch_vit_paper_replication_amd import _ext  # noqa: E402
 
-SHAPES = {"l16_384": (128, 577, 16, 64), "h14": (256, 257, 16, 80), "b16": (256, 197, 12, 64)}
+SHAPES = {"l16_384": (128, 577, 16, 64), "h14": (256, 257, 16, 80), "b16": (256, 197, 12, 64),
+          "h14_dh64": (256, 257, 20, 64), "h14_dh96": (256, 257, 13, 96), "h14_dh128": (256, 257, 10, 128)}  # D ~ 1280 at other head dims
 
 
 def timeit(fn, iters=10, warmup=3):
