@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--fp8-bf16-dgrad", action="store_true", help="fp8 mode: keep the dgrad GEMMs bf16 (A/B)")
     p.add_argument("--fp8-bf16-wgrad", action="store_true",
                    help="fp8 mode: keep the weight-gradient GEMMs bf16 (fp8 weight gradients are the default)")
+    p.add_argument("--fp8-grad", choices=["e5m2", "e4m3"], default="e5m2",
+                   help="fp8 mode: the gradients' format in the dgrad / wgrad GEMMs (e4m3: ~40 %% lower weight-gradient error, same speed)")
     p.add_argument("--fp8-wgrad", action="store_true",
                    help="fp8 mode: fp8 weight gradients (the default since round 6; kept so older command lines parse)")
     p.add_argument("--profile-out", default=None, help="write a torch.profiler kernel table here")
@@ -189,7 +191,8 @@ def main():
 
     model = vit(args.model, image_size=args.image_size, num_classes=args.num_classes).to(device)
     if args.dtype == "fp8":
-        model.enable_fp8(dgrad=not args.fp8_bf16_dgrad, wgrad=not args.fp8_bf16_wgrad and not args.fp8_bf16_dgrad)
+        model.enable_fp8(dgrad=not args.fp8_bf16_dgrad, wgrad=not args.fp8_bf16_wgrad and not args.fp8_bf16_dgrad,
+                         grad_fmt=args.fp8_grad)
     groups = param_groups_weight_decay(model, 0.03)
     total_steps = args.warmup + args.steps
     if args.impl == "fused":
@@ -324,8 +327,9 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if args.dtype == "bf16" else (
                 "fp8 (e4m3 forward GEMMs; bf16 backward/attention/norms)" if args.fp8_bf16_dgrad else
-                "fp8 (e4m3 forward GEMMs, e5m2-gradient dgrad and wgrad GEMMs; bf16 attention/norms)" if not args.fp8_bf16_wgrad else
-                "fp8 (e4m3 forward GEMMs, e5m2-gradient dgrad GEMMs; bf16 wgrad/attention/norms)"),
+                f"fp8 (e4m3 forward GEMMs, {args.fp8_grad}-gradient dgrad and wgrad GEMMs; bf16 attention/norms)"
+                if not args.fp8_bf16_wgrad else
+                f"fp8 (e4m3 forward GEMMs, {args.fp8_grad}-gradient dgrad GEMMs; bf16 wgrad/attention/norms)"),
             "data": f"synthetic (random [B,3,{args.image_size},{args.image_size}] in [0,1), {args.num_classes} classes, "
                     "random-init weights)",
             "config": {"model": name, "global_batch": global_batch, "per_gpu_batch": per_gpu, "seq_len": seq,

@@ -23,7 +23,7 @@
 // (dQ of block t-1 beside S/dP of block t, one barrier per block). A pre-pass per (batch, head)
 // supplies delta = rowsum(dO * O), the dO column sums (v-bias gradient) and, for N = 256 + 1, the
 // last key's dS / dK / dV. Heads with more keys accumulate dQ in f32 slabs (or atomics) that the
-// tail launch's final pass turns into bf16 dQ, its optional e5m2 copy and the q-bias partials.
+// tail launch's final pass turns into bf16 dQ, its optional fp8 (e5m2 / e4m3) copy and the q-bias partials.
 #include "attn_common.h"
 
 namespace pvr {
@@ -585,7 +585,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   // final pass at the end sums the nslab + 1 slabs of the pair in fixed order into bf16 dQ;
   // otherwise the bf16 gradient rows directly.
   const bool slab_w = dq_mode == 3 || dq_mode == 4;
-  // optional e5m2 copy of dQKV (the fp8 recipe's grad slot: dgrad and weight-gradient operand) with
+  // optional fp8 copy (e5m2, or e4m3: AttnQ8::fmt) of dQKV (the fp8 recipe's grad slot: dgrad and weight-gradient operand) with
   // the slot's delayed scale, written next to every final bf16 value, amax recorded per wave
   const bool q8kv = q8.out != nullptr;  // dK / dV: every launch writes final values
   const bool q8on = q8kv && !dq_acc;     // dQ here: only a launch whose fragments are the final dQ
@@ -712,7 +712,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
           __builtin_amdgcn_raw_buffer_store_b16(f2bf(val), dqrs, ((vq + r) * (uint32_t)ld_dq + col) * 2, 0, 0);
         if (q8on) {
           q8am = nan_max(q8am, fabsf(val));
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(pack2_fp8<1, false>(val * q8s, 0.f, 0) & 0xFF), q8rs,
+          __builtin_amdgcn_raw_buffer_store_b8(pack1_fp8_rt(q8.fmt, val * q8s), q8rs,
                                                (vq + r) * (uint32_t)q8.ld + col, 0, 0);
         }
       }
@@ -961,9 +961,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
           q8am = nan_max(q8am, nan_max(fabsf(k4[r]), fabsf(v4[r])));
         }
         uint8_t* qrow = q8.out + ((int64_t)b * N + key) * q8.ld + h * DH + 16 * e + 4 * g;
-        *(uint32_t*)(qrow + D) = (uint32_t)pack2_fp8<1, true>(k4[2] * q8s, k4[3] * q8s, pack2_fp8<1, false>(k4[0] * q8s, k4[1] * q8s, 0));
+        *(uint32_t*)(qrow + D) = pack4_fp8_rt(q8.fmt, k4[0] * q8s, k4[1] * q8s, k4[2] * q8s, k4[3] * q8s);
         *(uint32_t*)(qrow + 2 * D) =
-            (uint32_t)pack2_fp8<1, true>(v4[2] * q8s, v4[3] * q8s, pack2_fp8<1, false>(v4[0] * q8s, v4[1] * q8s, 0));
+            pack4_fp8_rt(q8.fmt, v4[0] * q8s, v4[1] * q8s, v4[2] * q8s, v4[3] * q8s);
       }
     }
   }
@@ -974,7 +974,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
   // Final dQ pass of the last launch of a multi-block head (one workgroup per (batch, head)):
   //   dq_mode 4: every key block stored its partial dQ as an f32 slab (the body launch before this
   //     one, this workgroup's own just now): sum the nslab + 1 slabs in slab order (deterministic).
-  // Coalesced 16-B loads; writes the final dQ: bf16 (unless only the fp8 copy is wanted), its e5m2
+  // Coalesced 16-B loads; writes the final dQ: bf16 (unless only the fp8 copy is wanted), its fp8
   // copy, and the q-bias partials (column sums in a fixed order).
   // (no agent-scope fence: it would write back the whole L2. The body launch completed before this
   // one started; this workgroup's own stores / atomics performed in its XCD's L2, which the loads
@@ -1025,7 +1025,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const uint16_t* __restric
                                                 ((uint32_t)qrow * (uint32_t)ld_dq + 4 * chunk) * 2, 0, 0);
         if (q8kv)
           *(uint32_t*)(q8.out + ((int64_t)b * N + qrow) * q8.ld + h * DH + 4 * chunk) =
-              (uint32_t)pack2_fp8<1, true>(sv[2] * q8s, sv[3] * q8s, pack2_fp8<1, false>(sv[0] * q8s, sv[1] * q8s, 0));
+              pack4_fp8_rt(q8.fmt, sv[0] * q8s, sv[1] * q8s, sv[2] * q8s, sv[3] * q8s);
       }
     }
     if (q8kv) {
@@ -1189,11 +1189,11 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __re
         krow[D + tid] = f2bf(sk * scale);
         krow[2 * D + tid] = f2bf(sv);
       }
-      if (q8.out) {  // e5m2 copy of key kt's dK / dV (amax of the two values: the rest come from the main kernel)
+      if (q8.out) {  // fp8 copy of key kt's dK / dV (amax of the two values: the rest come from the main kernel)
         const float qs = *q8.qs;
         uint8_t* qrow = q8.out + ((int64_t)b * N + kt) * q8.ld + h * DH;
-        qrow[D + tid] = (uint8_t)(pack2_fp8<1, false>(sk * scale * qs, 0.f, 0) & 0xFF);
-        qrow[2 * D + tid] = (uint8_t)(pack2_fp8<1, false>(sv * qs, 0.f, 0) & 0xFF);
+        qrow[D + tid] = pack1_fp8_rt(q8.fmt, sk * scale * qs);
+        qrow[2 * D + tid] = pack1_fp8_rt(q8.fmt, sv * qs);
         amax_record(q8.amax, nan_max(fabsf(sk * scale), fabsf(sv)));
       }
     }
@@ -1960,7 +1960,7 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
     // CLS token of 224/14) takes the lastkey path above instead.
     // The tail launch, one workgroup per (batch, head) running after the body, ends with a final
     // dQ pass over the pair's rows: every key block's f32 slab summed there in slab order; the
-    // final pass also writes the e5m2 copy and the q-bias partials.
+    // final pass also writes the fp8 copy and the q-bias partials.
     const int nslab = (N - rem) / KB;
     const int64_t sstride = (int64_t)B * N * D;
     launch(NW, 0, N - rem, 3, slab, sstride, nslab, nullptr);
@@ -2030,12 +2030,13 @@ extern "C" hipError_t pvr_attn_bwd(const uint16_t* qkv, int64_t ld, const uint16
                                    int64_t ld_do, const float* lse, uint16_t* dqkv, int64_t ld_dq, float* dq_acc,
                                    int dq_rezero, float* dbias, float* bpart, float* ws, int B, int N, int H, int D, float scale,
                                    const uint64_t* seed, uint64_t seed_off, uint32_t thr16, float keep_scale, uint8_t* q8_out,
-                                   int64_t q8_ld, const float* q8_qs, unsigned* q8_amax, int q8_only, hipStream_t s) {
+                                   int64_t q8_ld, const float* q8_qs, unsigned* q8_amax, int q8_only, int q8_fmt, hipStream_t s) {
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
+  if (q8_fmt != 0 && q8_fmt != 1) return hipErrorInvalidValue;
   if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
   const pvr::AttnDrop drop{seed, seed_off, thr16, keep_scale};
   if (q8_only && !q8_out) return hipErrorInvalidValue;
-  const pvr::AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, q8_only};
+  const pvr::AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, q8_only, q8_fmt};
   switch (D / H) {
 #define PVR_BWD_DH(DH) \
   case DH:             \

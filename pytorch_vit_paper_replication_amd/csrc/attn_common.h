@@ -118,6 +118,7 @@ struct AttnQ8 {
   const float* qs;
   unsigned* amax;
   int only;  // backward: store only the fp8 copy, not the bf16 gradient (every reader takes the copy)
+  int fmt;   // backward copies: 1 e5m2 (default), 0 e4m3 (enable_fp8(grad_fmt="e4m3")); forward: 0
 };
 // max|x| record with few same-address atomics: most waves find the running amax already larger
 PVR_DEV void amax_record(unsigned* amax, float m) {

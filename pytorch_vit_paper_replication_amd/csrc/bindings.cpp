@@ -30,7 +30,7 @@ void pvr_set_fp8_persistent(int mode);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
 hipError_t pvr_layernorm_fwd_q8(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, uint8_t*, int64_t, const float*,
                                 unsigned*, float*, float*, int, int, float, hipStream_t);
-hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, uint8_t*, int64_t, const float*, unsigned*, int, int, float*, hipStream_t);
+hipError_t pvr_layernorm_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, const float*, const float*, const uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, int, uint8_t*, int64_t, const float*, unsigned*, int, int, int, float*, hipStream_t);
 int pvr_layernorm_bwd_blocks(int, int);
 int pvr_colsum_part_rows(int);
 hipError_t pvr_cast_f32_bf16(const float*, uint16_t*, int64_t, hipStream_t);
@@ -38,7 +38,7 @@ hipError_t pvr_splitk_reduce(const float*, int, int64_t, float*, int64_t, int, i
 hipError_t pvr_pad_cols_bf16(const uint16_t*, int, int, uint16_t*, int, hipStream_t);
 hipError_t pvr_transpose_batched(const uint16_t*, uint16_t*, const int64_t*, int, int, hipStream_t);
 hipError_t pvr_colsum(const uint16_t*, int64_t, int, int, float*, uint16_t*, int64_t, const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t,
-                      const float*, unsigned*, float*, hipStream_t);
+                      const float*, unsigned*, int, float*, hipStream_t);
 hipError_t pvr_im2col(const float*, uint16_t*, int, int, int, int, int, int, hipStream_t);
 hipError_t pvr_cls_rows(const float*, const float*, uint16_t*, int, int, int64_t, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
 hipError_t pvr_patch_bwd(const uint16_t*, int, int, int, float*, float*, float*, uint16_t*, float*, const uint64_t*, uint64_t, uint32_t, float, hipStream_t);
@@ -80,7 +80,7 @@ hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float
 hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, int, hipStream_t);
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, float*, float*, int, int, int, int, float,
                         const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t, const float*, unsigned*,
-                        int, hipStream_t);
+                        int, int, hipStream_t);
 int64_t pvr_attn_bwd_ws_floats(int, int, int, int, int, int);
 int pvr_attn_bwd_q8_ok(int, int);
 }
@@ -361,7 +361,8 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
                    c10::optional<torch::Tensor> dw, c10::optional<torch::Tensor> db, int64_t rows,
                    c10::optional<torch::Tensor> dsum, c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> seed,
                    int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
-                   c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool dz_nostore) {
+                   c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool dz_nostore,
+                   int64_t q_fmt) {
   const int64_t D = w.numel();
   // optional e5m2 copy of the last-written gradient (dz if given, else dx) with a delayed scale
   // and an amax record: the producer-side quantization for the next fp8 dgrad GEMM
@@ -394,7 +395,7 @@ void layernorm_bwd(torch::Tensor dy, int64_t dy_stride, torch::Tensor x, int64_t
   check(pvr_layernorm_bwd(bf(dy, "dy"), dy_stride, bf(x, "x"), x_stride, f32(mean, "mean"), f32(rstd, "rstd"), f32(w, "w"),
                           opt_ptr<const uint16_t>(dres), dres_stride, bf_mut(dx, "dx"), dx_stride, opt_ptr<float>(dw),
                           opt_ptr<float>(db), opt_ptr<float>(dsum), dzp, ldz, d.seed, (uint64_t)seed_offset, d.thr, d.scale,
-                          dz_nostore ? 1 : 0, qp, ldq, qs, qa, (int)rows, (int)D,
+                          dz_nostore ? 1 : 0, qp, ldq, qs, qa, (int)q_fmt, (int)rows, (int)D,
                           g_deterministic && (opt_ptr<float>(dw) || opt_ptr<float>(db) || opt_ptr<float>(dsum)) ? det_scratch((int64_t)pvr_layernorm_bwd_blocks((int)rows, (int)D) * 3 * D, x.options()) : nullptr,
                           stream()),
         "layernorm_bwd");
@@ -464,12 +465,12 @@ void transpose_batched(torch::Tensor src, torch::Tensor dst, torch::Tensor meta,
 
 void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tensor> db, c10::optional<torch::Tensor> dz,
             c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
-            c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax) {
+            c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, int64_t q_fmt) {
   const DropArgs d = drop_args(seed, drop_p, "colsum");
   int64_t ldz = 0;
   uint16_t* dzp = nullptr;
   if (dz.has_value() && dz->defined()) { dzp = const_cast<uint16_t*>(bf(*dz, "dz")); ldz = ld_of(*dz, "dz"); }
-  // optional e5m2 copy of the (masked) gradient + amax record (the fp8 dgrad operand)
+  // optional fp8 copy (q_fmt 1 e5m2, 0 e4m3) of the (masked) gradient + amax record (the fp8 dgrad operand)
   uint8_t* qp = nullptr;
   int64_t ldq = 0;
   const float* qs = nullptr;
@@ -488,7 +489,7 @@ void colsum(torch::Tensor dy, int64_t rows, int64_t N, c10::optional<torch::Tens
     qa = reinterpret_cast<unsigned*>(q_amax->data_ptr());
   }
   check(pvr_colsum(bf(dy, "dy"), ld_of(dy, "dy"), (int)rows, (int)N, opt_ptr<float>(db), dzp, ldz, d.seed, (uint64_t)seed_offset,
-                   d.thr, d.scale, qp, ldq, qs, qa,
+                   d.thr, d.scale, qp, ldq, qs, qa, (int)q_fmt,
                    g_deterministic && opt_ptr<float>(db) ? det_scratch((int64_t)pvr_colsum_part_rows((int)rows) * N, dy.options()) : nullptr, stream()),
         "colsum");
 }
@@ -798,9 +799,11 @@ void fp8_transpose(torch::Tensor x8, torch::Tensor yt) {
 
 // fp8 weight gradient partials straight from the row-major fp8 copies: ws[s][N][K] = dscale_a *
 // dscale_b * dy8[Ts][N]^T . x8[Ts][K] over token split s (ksplit tokens, a multiple of 128), dy8 e5m2
+// (fmt_a 1) or e4m3 (fmt_a 0)
 // and x8 e4m3 [T][features] (mn-contiguous operands: transposed LDS reads, no transposed copies)
 void gemm_fp8_wgrad_mn(torch::Tensor dy8, torch::Tensor x8, torch::Tensor ws, int64_t N, int64_t K, int64_t T, torch::Tensor scale_a,
-                       torch::Tensor scale_b, int64_t ksplit) {
+                       torch::Tensor scale_b, int64_t ksplit, int64_t fmt_a) {
+  TORCH_CHECK((fmt_a == 0 || fmt_a == 1), "gemm_fp8_wgrad_mn: fmt_a 0 (e4m3) / 1 (e5m2)");
   TORCH_CHECK(dy8.dim() == 2 && x8.dim() == 2 && dy8.size(0) >= T && x8.size(0) >= T && dy8.size(1) >= N && x8.size(1) >= K &&
                   dy8.stride(1) == 1 && x8.stride(1) == 1,
               "gemm_fp8_wgrad_mn: dy8 [T][N], x8 [T][K] row-major");
@@ -818,7 +821,7 @@ void gemm_fp8_wgrad_mn(torch::Tensor dy8, torch::Tensor x8, torch::Tensor ws, in
   p.B = reinterpret_cast<const uint16_t*>(u8(x8, "x8")); p.ldb = x8.stride(0); p.b_kcontig = 0;
   p.C = ws.data_ptr(); p.ldc = ws.stride(1); p.split_stride = ws.stride(0);
   p.scale_a = f32(scale_a, "scale_a"); p.scale_b = f32(scale_b, "scale_b");
-  p.elem8 = 1; p.fmt_a = 1; p.fmt_b = 0;
+  p.elem8 = 1; p.fmt_a = (int)fmt_a; p.fmt_b = 0;
   p.k_split_len = (int)ksplit;
   p.epi = 4;  // EPI_F32_STORE
   p.tile_cfg = 14;
@@ -826,9 +829,10 @@ void gemm_fp8_wgrad_mn(torch::Tensor dy8, torch::Tensor x8, torch::Tensor ws, in
 }
 
 // fp8 weight gradient partials: ws[s][N][K] = dscale_a * dscale_b * A8[N][Ks] . B8[K][Ks]^T over split s
-// of the (padded) token dim, A e5m2 (gradient^T), B e4m3 (activation^T)
+// of the (padded) token dim, A e5m2 / e4m3 (fmt_a 1 / 0; gradient^T), B e4m3 (activation^T)
 void gemm_fp8_wgrad(torch::Tensor A8, torch::Tensor B8, torch::Tensor ws, int64_t N, int64_t K, int64_t Tp, torch::Tensor scale_a,
-                    torch::Tensor scale_b, int64_t ksplit) {
+                    torch::Tensor scale_b, int64_t ksplit, int64_t fmt_a) {
+  TORCH_CHECK((fmt_a == 0 || fmt_a == 1), "gemm_fp8_wgrad: fmt_a 0 (e4m3) / 1 (e5m2)");
   pvr::GemmParams p{};
   p.drop_scale = 1.f;
   p.M = (int)N; p.N = (int)K; p.K = (int)Tp;
@@ -841,7 +845,7 @@ void gemm_fp8_wgrad(torch::Tensor A8, torch::Tensor B8, torch::Tensor ws, int64_
               "gemm_fp8_wgrad: workspace [splits][N][K] f32");
   p.C = ws.data_ptr(); p.ldc = ws.stride(1); p.split_stride = ws.stride(0);
   p.scale_a = f32(scale_a, "scale_a"); p.scale_b = f32(scale_b, "scale_b");
-  p.elem8 = 1; p.fmt_a = 1; p.fmt_b = 0;
+  p.elem8 = 1; p.fmt_a = (int)fmt_a; p.fmt_b = 0;
   p.k_split_len = (int)ksplit;
   p.epi = 4;  // EPI_F32_STORE
   p.tile_cfg = 14;
@@ -1004,7 +1008,8 @@ bool attn_bwd_q8_ok(int64_t B, int64_t N, int64_t H, int64_t D, bool drop) {
 torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out, torch::Tensor lse, int64_t B, int64_t N, int64_t H,
                        double scale, c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> dbias_part_out,
                        c10::optional<torch::Tensor> seed, int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
-                       c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool q_only) {
+                       c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool q_only,
+                       int64_t q_fmt) {
   const int64_t D = qkv.size(1) / 3;
   auto dqkv = torch::empty_like(qkv);
   torch::Tensor dq_acc;
@@ -1075,7 +1080,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
                                       bf_mut(dqkv, "dqkv"), lds[3], dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
                                       dbias_arg, bpart_arg, ws.data_ptr<float>(), (int)B, (int)N, (int)H, (int)D, (float)scale,
                                       drop.seed, (uint64_t)seed_offset, drop.thr, drop.scale, qp, ldq, qs, qa, q_only && qp ? 1 : 0,
-                                      stream());
+                                      (int)q_fmt, stream());
   // a persistent accumulator is re-zeroed only by a completed backward: after a failed launch it
   // may hold stale partial sums, so it is dropped (re-created zeroed by the next call)
   if (err != hipSuccess && dq_rezero) dq_workspace(0, qkv.options(), true);
@@ -1128,7 +1133,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dx_stride"), py::arg("dw"), py::arg("db"), py::arg("rows"), py::arg("dsum") = py::none(),
         py::arg("dz") = py::none(), py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0,
         py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none(),
-        py::arg("dz_nostore") = false);
+        py::arg("dz_nostore") = false, py::arg("q_fmt") = 1);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("splitk_epilogue", &splitk_epilogue);
   m.def("attn_bwd_bias_rows", &attn_bwd_bias_rows, py::arg("B"), py::arg("N"), py::arg("H"), py::arg("D"), py::arg("drop") = false);
@@ -1138,7 +1143,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_batched", &transpose_batched);
   m.def("colsum", &colsum, py::arg("dy"), py::arg("rows"), py::arg("N"), py::arg("db"), py::arg("dz"), py::arg("seed"),
         py::arg("seed_offset"), py::arg("drop_p"), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
-        py::arg("q_amax") = py::none());
+        py::arg("q_amax") = py::none(), py::arg("q_fmt") = 1);
   m.def("im2col", &im2col);
   m.def("cls_rows", &cls_rows);
   m.def("patch_bwd", &patch_bwd);
@@ -1163,12 +1168,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("drop_p") = 0.0, py::arg("colsum") = py::none(), py::arg("q_out") = py::none(), py::arg("q_scale") = py::none(),
         py::arg("q_amax") = py::none(), py::arg("q_fmt") = 0, py::arg("c_skip") = false, py::arg("tail_limit") = 0);
   m.def("fp8_transpose", &fp8_transpose);
-  m.def("gemm_fp8_wgrad_mn", &gemm_fp8_wgrad_mn);
+  m.def("gemm_fp8_wgrad_mn", &gemm_fp8_wgrad_mn, py::arg("dy8"), py::arg("x8"), py::arg("ws"), py::arg("N"), py::arg("K"),
+        py::arg("T"), py::arg("scale_a"), py::arg("scale_b"), py::arg("ksplit"), py::arg("fmt_a") = 1);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("y"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"));
   m.def("fp8_dequant", &fp8_dequant, py::arg("x"), py::arg("dscale") = py::none(), py::arg("fmt") = 0);
   m.def("fp8_scale_update", &fp8_scale_update);
   m.def("fp8_quant_t", &fp8_quant_t);
-  m.def("gemm_fp8_wgrad", &gemm_fp8_wgrad);
+  m.def("gemm_fp8_wgrad", &gemm_fp8_wgrad, py::arg("A8"), py::arg("B8"), py::arg("ws"), py::arg("N"), py::arg("K"), py::arg("Tp"),
+        py::arg("scale_a"), py::arg("scale_b"), py::arg("ksplit"), py::arg("fmt_a") = 1);
   m.def("fp8_quant_multi", &fp8_quant_multi, py::arg("segs"), py::arg("nchunks"), py::arg("qscale"), py::arg("amax"), py::arg("fmt"),
         py::arg("amax_only"));
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("B"), py::arg("N"), py::arg("H"), py::arg("scale"),
@@ -1177,7 +1184,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
         py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none(),
         py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0, py::arg("q_out") = py::none(),
-        py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none(), py::arg("q_only") = false);
+        py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none(), py::arg("q_only") = false,
+        py::arg("q_fmt") = 1);
   m.def("attn_bwd_q8_ok", &attn_bwd_q8_ok, "attn_bwd can write dQKV's e5m2 copy for this shape");
   m.def("arch", []() { return std::string("gfx950"); });
 }

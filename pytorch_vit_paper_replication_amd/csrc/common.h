@@ -331,4 +331,17 @@ PVR_DEV uint2 pack8_fp8_fast(const float (&v)[8], float qs, float vmax) {
   return r;
 }
 
+// Runtime-format forms for the gradient copies (fmt 1 e5m2, the default; 0 e4m3 with
+// enable_fp8(grad_fmt="e4m3")): one wave-uniform branch per store, both conversions compiled in.
+PVR_DEV uint32_t pack4_fp8_rt(int fmt, float a, float b, float c, float d) {
+  return fmt ? (uint32_t)pack2_fp8<1, true>(c, d, pack2_fp8<1, false>(a, b, 0))
+             : (uint32_t)pack2_fp8<0, true>(c, d, pack2_fp8<0, false>(a, b, 0));
+}
+PVR_DEV uint8_t pack1_fp8_rt(int fmt, float a) {
+  return (uint8_t)((fmt ? pack2_fp8<1, false>(a, 0.f, 0) : pack2_fp8<0, false>(a, 0.f, 0)) & 0xFF);
+}
+PVR_DEV uint2 pack8_fp8_fast_rt(int fmt, const float (&v)[8], float qs, float vmax) {
+  return fmt ? pack8_fp8_fast<1>(v, qs, vmax) : pack8_fp8_fast<0>(v, qs, vmax);
+}
+
 }  // namespace pvr

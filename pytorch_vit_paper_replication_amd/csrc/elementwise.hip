@@ -25,14 +25,14 @@ __global__ void __launch_bounds__(256) cast_f32_bf16_kernel(const float* __restr
 
 // dY [rows][N] (row stride ld) -> db[N] += column sums of (mask * dY); if dz != null also writes
 // the masked gradient dz (= dropout backward) with row stride ld_dz.
-// Q8: also the e5m2 copy of the (masked) gradient, q[r][n] = fp8(v * *qscale), and its amax record
+// Q8: also the fp8 copy (qfmt 1 e5m2, 0 e4m3) of the (masked) gradient, q[r][n] = fp8(v * *qscale), and its amax record
 // (the fp8 dgrad operand of the same tensor whose column sums are the bias gradient: one read, two uses)
 template <bool Q8>
 __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict__ dy, int64_t ld, int rows, int N,
                                                       float* __restrict__ db, uint16_t* __restrict__ dz, int64_t ld_dz,
                                                       const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale,
                                                       uint8_t* __restrict__ qout, int64_t ld_q, const float* __restrict__ qscale,
-                                                      unsigned* __restrict__ amax, float* __restrict__ part) {
+                                                      unsigned* __restrict__ amax, int qfmt, float* __restrict__ part) {
   __shared__ float red[4][64 * 8];
   const float qs = Q8 ? *qscale : 1.f;
   float qam = 0.f;
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict_
 #pragma unroll
           for (int j = 0; j < 8; ++j) vm = nan_max(vm, fabsf(v[j]));
           qam = nan_max(qam, vm);
-          *(uint2*)(qout + (int64_t)r * ld_q + c * 8) = pack8_fp8_fast<1>(v, qs, vm);
+          *(uint2*)(qout + (int64_t)r * ld_q + c * 8) = pack8_fp8_fast_rt(qfmt, v, qs, vm);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += v[j];
@@ -470,16 +470,16 @@ extern "C" hipError_t pvr_rows_reduce(const float* part, int R, int C, int seg, 
 
 extern "C" hipError_t pvr_colsum(const uint16_t* dy, int64_t ld, int rows, int N, float* db, uint16_t* dz, int64_t ld_dz,
                                  const uint64_t* seed_ptr, uint64_t seed_off, uint32_t thr, float scale, uint8_t* q, int64_t ld_q,
-                                 const float* qscale, unsigned* amax, float* part, hipStream_t s) {
+                                 const float* qscale, unsigned* amax, int qfmt, float* part, hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
-  if (N % 8 != 0) return hipErrorInvalidValue;
+  if (N % 8 != 0 || (qfmt != 0 && qfmt != 1)) return hipErrorInvalidValue;
   if (q && (!qscale || !amax || ld_q % 8 != 0 || reinterpret_cast<uintptr_t>(q) % 8 != 0)) return hipErrorInvalidValue;
   const int gx = (N / 8 + 63) / 64;
   const int gy = pvr_colsum_part_rows(rows);
   if (!db) part = nullptr;
   hipLaunchKernelGGL(q ? colsum_kernel<true> : colsum_kernel<false>, dim3(gx, gy), dim3(256), 0, s, dy, ld, rows, N, db, dz, ld_dz,
-                     seed_ptr, seed_off, thr, scale, q, ld_q, qscale, amax, part);
+                     seed_ptr, seed_off, thr, scale, q, ld_q, qscale, amax, qfmt, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !part) return e;
   return pvr_rows_reduce(part, gy, N, N, db, nullptr, nullptr, s);

@@ -2100,21 +2100,23 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
     return pvr_gemm(&q, s);
   }
   const bool ak = p.a_kcontig, bk = p.b_kcontig;
-  if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad / wgrad e5m2 x e4m3)
+  if (p.elem8) {  // fp8 operands: k-contiguous ping-pong only (forward e4m3 x e4m3, dgrad / wgrad e5m2 or e4m3 x e4m3)
     const int f = p.fmt_a * 2 + p.fmt_b;
     if ((p.N & 3) || !p.scale_a || !p.scale_b) return hipErrorInvalidValue;
     if (!ak && !bk) {
       // weight gradient straight from the row-major fp8 copies ([tokens][features], mn-contiguous,
       // transposed LDS reads): split-K over the tokens, per-split partials (tile 14); 16-B rows
-      if (p.epi != EPI_F32_STORE || p.tile_cfg != 14 || p.k_split_len % 128 != 0 || f != 2 || (p.M & 15) || (p.N & 15) ||
-          (p.lda & 15) || (p.ldb & 15))
+      if (p.epi != EPI_F32_STORE || p.tile_cfg != 14 || p.k_split_len % 128 != 0 || (f != 2 && f != 0) || (p.M & 15) ||
+          (p.N & 15) || (p.lda & 15) || (p.ldb & 15))
         return hipErrorInvalidValue;
+      if (f == 0) return launch_pp<false, false, true, EPI_F32_STORE, 1, 0, 0>(p, s);  // e4m3 gradients
       return launch_pp<false, false, true, EPI_F32_STORE, 1, 1, 0>(p, s);
     }
     if (!ak || !bk || p.K % 128 != 0) return hipErrorInvalidValue;
     if (p.epi == EPI_F32_STORE) {
       // weight gradient: split-K over the (128-padded) token dim, per-split partials (tile 14)
-      if (p.tile_cfg != 14 || p.k_split_len % 128 != 0 || f != 2) return hipErrorInvalidValue;
+      if (p.tile_cfg != 14 || p.k_split_len % 128 != 0 || (f != 2 && f != 0)) return hipErrorInvalidValue;
+      if (f == 0) return launch_pp<true, true, true, EPI_F32_STORE, 1, 0, 0>(p, s);
       return launch_pp<true, true, true, EPI_F32_STORE, 1, 1, 0>(p, s);
     }
     if (p.k_split_len < p.K) return hipErrorInvalidValue;
@@ -2139,6 +2141,7 @@ extern "C" hipError_t pvr_gemm(const pvr::GemmParams* pp, hipStream_t s) {
         if (f == 0) return launch_pp<true, true, true, EPI_GELU, 1, 0, 0>(p, s);
         break;
       case EPI_DGELU:
+        if (f == 0) return launch_pp<true, true, true, EPI_DGELU, 1, 0, 0>(p, s);  // e4m3 gradients
         if (f == 2) return launch_pp<true, true, true, EPI_DGELU, 1, 1, 0>(p, s);
         break;
     }

@@ -215,8 +215,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
                                                       uint16_t* __restrict__ dz, int64_t dz_stride,
                                                       const uint64_t* __restrict__ seed_ptr, uint64_t seed_off, uint32_t thr,
                                                       float dscale, int dz_nostore, uint8_t* __restrict__ qout, int64_t q_stride,
-                                                      const float* __restrict__ qscale, unsigned* __restrict__ amax, int rows,
-                                                      int D) {
+                                                      const float* __restrict__ qscale, unsigned* __restrict__ amax, int qfmt,
+                                                      int rows, int D) {
   __shared__ float red[4][MAXCH * 64 * W > 1280 ? 1280 : MAXCH * 64 * W];  // one partial at a time
   __shared__ float qred[4];
   const float qs = Q8 ? *qscale : 1.f;
@@ -319,19 +319,20 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const uint16_t* __restrict_
             q.store(dz + (int64_t)row * dz_stride + c * W);
           }
         }
-        if constexpr (Q8) {  // e5m2 copy of the gradient written last (dz, else dx) for the next fp8 dgrad GEMM
+        if constexpr (Q8) {  // fp8 copy (qfmt 1 e5m2, 0 e4m3) of the gradient written last (dz, else dx) for the next fp8 dgrad GEMM
           uint32_t b4[W / 4];
           float vm = 0.f;
 #pragma unroll
           for (int j = 0; j < W; ++j) vm = nan_max(vm, fabsf(o[j]));
           qam = nan_max(qam, vm);
-          if (fp8_direct_ok<1>(vm, qs)) {  // no saturation / NaN handling needed in this wave
-#pragma unroll
-            for (int j = 0; j < W; j += 4) b4[j >> 2] = pack4_fp8_direct<1>(o[j] * qs, o[j + 1] * qs, o[j + 2] * qs, o[j + 3] * qs);
-          } else {
+          if (qfmt ? fp8_direct_ok<1>(vm, qs) : fp8_direct_ok<0>(vm, qs)) {  // no saturation / NaN handling needed in this wave
 #pragma unroll
             for (int j = 0; j < W; j += 4)
-              b4[j >> 2] = (uint32_t)pack2_fp8<1, true>(o[j + 2] * qs, o[j + 3] * qs, pack2_fp8<1, false>(o[j] * qs, o[j + 1] * qs, 0));
+              b4[j >> 2] = qfmt ? pack4_fp8_direct<1>(o[j] * qs, o[j + 1] * qs, o[j + 2] * qs, o[j + 3] * qs)
+                                : pack4_fp8_direct<0>(o[j] * qs, o[j + 1] * qs, o[j + 2] * qs, o[j + 3] * qs);
+          } else {
+#pragma unroll
+            for (int j = 0; j < W; j += 4) b4[j >> 2] = pack4_fp8_rt(qfmt, o[j] * qs, o[j + 1] * qs, o[j + 2] * qs, o[j + 3] * qs);
           }
           uint8_t* qp = qout + (int64_t)row * q_stride + c * W;
           if constexpr (W == 8)
@@ -456,9 +457,11 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
                                         int64_t dres_stride, uint16_t* dx, int64_t dx_stride, float* dw, float* db,
                                         float* dsum, uint16_t* dz, int64_t dz_stride, const uint64_t* seed_ptr,
                                         uint64_t seed_off, uint32_t thr, float dscale, int dz_nostore, uint8_t* q, int64_t q_stride,
-                                        const float* qscale, unsigned* amax, int rows, int D, float* part, hipStream_t s) {
+                                        const float* qscale, unsigned* amax, int qfmt, int rows, int D, float* part,
+                                        hipStream_t s) {
   using namespace pvr;
   if (rows <= 0) return hipSuccess;
+  if (qfmt != 0 && qfmt != 1) return hipErrorInvalidValue;
   if (D % 8 != 0 || D > 1280 || (dz && (!seed_ptr || !thr))) return hipErrorInvalidValue;
   if (q && (!qscale || !amax || q_stride % 8 != 0 || reinterpret_cast<uintptr_t>(q) % 8 != 0)) return hipErrorInvalidValue;
   if (dz_nostore && (!dz || !q)) return hipErrorInvalidValue;  // skipping dz needs dz's fp8 copy
@@ -475,7 +478,7 @@ extern "C" hipError_t pvr_layernorm_bwd(const uint16_t* dy, int64_t dy_stride, c
 #define PVR_LN_BWD(MC, W)                                                                                                   \
   hipLaunchKernelGGL(q ? (ln_bwd_kernel<MC, W, true>) : (ln_bwd_kernel<MC, W, false>), grid, block, 0, s, dy, dy_stride, x, x_stride, mean, rstd, w, dres, dres_stride, dx, \
                      dx_stride, dw, db, dsum, part, dz, dz_stride, seed_ptr, seed_off, thr, dscale, dz_nostore, q, q_stride, qscale, amax, \
-                     rows, D)
+                     qfmt, rows, D)
   if (use_w4) {
     switch (D / 256) {
       case 3: PVR_LN_BWD(3, 4); break;  // D = 768

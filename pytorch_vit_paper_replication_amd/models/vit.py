@@ -298,7 +298,7 @@ class ViT(nn.Module):
 
     # ------------------------------------------------------------------ fp8
     def enable_fp8(self, enabled: bool = True, history: int = 16, margin: int = 0, dgrad: bool = True,
-                   wgrad: bool = True) -> "ViT":
+                   wgrad: bool = True, grad_fmt: str = "e5m2") -> "ViT":
         """Run the encoder's GEMMs in fp8 on the fused MI355X path (ops/fp8.py), per-tensor delayed
         scaling with an amax history of ``history`` steps:
 
@@ -316,13 +316,22 @@ class ViT(nn.Module):
           deviation at every checkpoint and no significant paired difference (p 0.08-0.33), with the
           fp8 means 6-29 % above bf16's at steps 400 / 600: a trend more seeds would be needed to
           confirm or rule out;
+        * ``grad_fmt``: the gradients' fp8 format in the dgrad / wgrad GEMMs, ``"e5m2"`` (default)
+          or ``"e4m3"``. Round 6 measured the weight-gradient GEMM error on captured ViT-B/16
+          operands (``profiles/r6/mx_study``): the error comes from e5m2's 2-bit mantissa, and e4m3
+          gradients with the same per-tensor delayed scaling cut it by ~40 %; per-32-element MX block
+          scales change nothing. The format is a runtime argument of every kernel that writes a
+          gradient copy (the dgrad epilogues, LayerNorm backward, attention backward, column sums), so
+          both formats run the same kernels at the same speed;
         * attention, LayerNorm, the patch embedding / head GEMMs and the optimizer stay bf16 / fp32.
 
         The constructor signature stays the reference's; fp8 is opt-in."""
         old = getattr(self, "_fp8_cfg", None)
-        cfg = (history, margin, bool(dgrad), bool(wgrad)) if enabled else None
+        if grad_fmt not in ("e5m2", "e4m3"):
+            raise ValueError(f"enable_fp8: grad_fmt must be 'e5m2' or 'e4m3', got {grad_fmt!r}")
+        cfg = (history, margin, bool(dgrad), bool(wgrad), grad_fmt) if enabled else None
         object.__setattr__(self, "_fp8_cfg", cfg)
-        if cfg is None or old is None or old[:2] != cfg[:2]:
+        if cfg is None or old is None or old[:2] != cfg[:2] or old[4:] != cfg[4:]:
             object.__setattr__(self, "_fp8", None)  # new scaling state; only a dgrad switch keeps the histories
         return self
 
@@ -338,7 +347,8 @@ class ViT(nn.Module):
         st = getattr(self, "_fp8", None)
         if st is None or st.device != device:
             old_sd = st.state_dict() if st is not None else getattr(self, "_fp8_pending", None)
-            st = F8.Fp8State(c["num_transformer_layer"], device, history=cfg[0], margin=cfg[1], dgrad=cfg[2], wgrad=cfg[3])
+            st = F8.Fp8State(c["num_transformer_layer"], device, history=cfg[0], margin=cfg[1], dgrad=cfg[2], wgrad=cfg[3],
+                             grad_fmt=F8.E4M3 if cfg[4] == "e4m3" else F8.E5M2)
             if old_sd is not None:  # restored (or built) on another device: carry the scaling state over
                 st.load_state_dict(old_sd)
             object.__setattr__(self, "_fp8", st)
@@ -386,7 +396,7 @@ class ViT(nn.Module):
             st = getattr(self, "_fp8", None)
             if st is None or st.device != dev:
                 st = F8.Fp8State(self.config["num_transformer_layer"], dev, history=cfg[0], margin=cfg[1],
-                                 dgrad=cfg[2], wgrad=cfg[3])
+                                 dgrad=cfg[2], wgrad=cfg[3], grad_fmt=F8.E4M3 if cfg[4] == "e4m3" else F8.E5M2)
                 object.__setattr__(self, "_fp8", st)
             st.load_state_dict(sd["fp8"])
 

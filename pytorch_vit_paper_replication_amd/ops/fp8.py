@@ -111,10 +111,14 @@ class Fp8State:
 
     ACT_PER_BLOCK = 4  # xn1 (qkv input), o (out-proj input), xn2 (fc1 input), h (fc2 input)
 
-    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0, dgrad: bool = True, wgrad: bool = True):
+    def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0, dgrad: bool = True, wgrad: bool = True,
+                 grad_fmt: int = E5M2):
         self.act = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E4M3)
-        # e5m2 gradient slots for the fp8 dgrad GEMMs (dgrad=True): dz2, dU, dx1, dQKV per block
-        self.grad = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E5M2)
+        # gradient slots for the fp8 dgrad GEMMs (dgrad=True): dz2, dU, dx1, dQKV per block; e5m2 by
+        # default, e4m3 with grad_fmt=E4M3 (every producer of a gradient copy takes the slot's format)
+        if grad_fmt not in (E4M3, E5M2):
+            raise ValueError(f"Fp8State: grad_fmt {grad_fmt}")
+        self.grad = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, grad_fmt)
         self.dgrad = bool(dgrad)
         self.wgrad = bool(wgrad) and bool(dgrad)  # fp8 weight gradients reuse the dgrad gradient slots
         self.n_blocks = n_blocks
@@ -129,9 +133,12 @@ class Fp8State:
 
     def state_dict(self) -> Dict[str, Dict[str, torch.Tensor]]:
         """Activation / gradient slot state (weights use current scaling: nothing to keep)."""
-        return {"act": self.act.state_dict(), "grad": self.grad.state_dict()}
+        return {"act": self.act.state_dict(), "grad": self.grad.state_dict(), "grad_fmt": torch.tensor(self.grad.fmt)}
 
     def load_state_dict(self, sd) -> None:
+        fmt = sd.get("grad_fmt")
+        if fmt is not None and int(fmt) != self.grad.fmt:
+            raise ValueError(f"fp8 state: saved gradient format {int(fmt)} != this model's {self.grad.fmt}")
         self.act.load_state_dict(sd["act"])
         self.grad.load_state_dict(sd["grad"])
 
@@ -280,23 +287,24 @@ def linear_fwd_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: tor
 
 def linear_dgrad_fp8(gq: torch.Tensor, gs: torch.Tensor, wtq: torch.Tensor, wts: torch.Tensor, *,
                      dgelu_aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
-                     out: Optional[torch.Tensor] = None, quant=None, skip_out: bool = False):
-    """dx = dequant(gq (e5m2) . wtq^T (e4m3, W^T rows)) [* dgelu_aux]; ``quant`` as in linear_fwd_fp8
-    (dGELU variant: the e5m2 copy of dx for the next dgrad GEMM)."""
+                     out: Optional[torch.Tensor] = None, quant=None, skip_out: bool = False, g_fmt: int = E5M2):
+    """dx = dequant(gq (e5m2, or e4m3: ``g_fmt``) . wtq^T (e4m3, W^T rows)) [* dgelu_aux]; ``quant`` as in
+    linear_fwd_fp8 (dGELU variant: the gradient-format copy of dx for the next dgrad GEMM)."""
     T, N = gq.shape
     K = wtq.shape[0]
     if out is None:
         out = torch.empty(T, K, dtype=torch.bfloat16, device=gq.device)
     epi = gemm.EPI_DGELU if dgelu_aux is not None else gemm.EPI_BF16
     kw, q = _quant_args(quant, T, K, gq.device)
-    _ext.ext().gemm_fp8(gq, E5M2, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum,
+    _ext.ext().gemm_fp8(gq, g_fmt, wtq, E4M3, out, T, K, N, epi, gs, wts, None, None, dgelu_aux, None, 0, 0.0, colsum,
                         c_skip=bool(skip_out and quant is not None), tail_limit=gemm.DGRAD_TAIL_UNITS, **kw)
     return out if quant is None else (out, q)
 
 
 def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torch.Tensor, x_meta: "Fp8Meta", x_slot: int,
                      out: torch.Tensor, dy8: Optional[torch.Tensor] = None, x8: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[N, K] += dequant(dy^T (e5m2) . x (e4m3)) over the tokens: the weight gradient in fp8.
+    """out[N, K] += dequant(dy^T (the gradient slot's format, e5m2 or e4m3) . x (e4m3)) over the tokens:
+    the weight gradient in fp8.
 
     Both operands are needed TRANSPOSED ([features][tokens], the token dim padded to 128 with zeros)
     with their slots' current delayed scales. ``dy8`` / ``x8``: the row-major fp8 copies the dgrad /
@@ -313,7 +321,8 @@ def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torc
         ksplit = max(128, (T // splits + 127) // 128 * 128)
         nsplit = (T + ksplit - 1) // ksplit
         ws = gemm._workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
-        ext.gemm_fp8_wgrad_mn(dy8, x8, ws, N, K, T, dy_meta.dscale[dy_slot:dy_slot + 1], x_meta.dscale[x_slot:x_slot + 1], ksplit)
+        ext.gemm_fp8_wgrad_mn(dy8, x8, ws, N, K, T, dy_meta.dscale[dy_slot:dy_slot + 1], x_meta.dscale[x_slot:x_slot + 1], ksplit,
+                              dy_meta.fmt)
         ext.splitk_reduce(ws, nsplit, out, True)
         return out
     Tp = (T + 127) // 128 * 128
@@ -322,7 +331,7 @@ def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torc
     if dy8 is not None:
         ext.fp8_transpose(dy8, dyt)
     else:
-        ext.fp8_quant_t(dy, dyt, dy_meta.qscale[dy_slot:dy_slot + 1], E5M2)
+        ext.fp8_quant_t(dy, dyt, dy_meta.qscale[dy_slot:dy_slot + 1], dy_meta.fmt)
     if x8 is not None:
         ext.fp8_transpose(x8, xt)
     else:
@@ -331,7 +340,8 @@ def linear_wgrad_fp8(dy: torch.Tensor, dy_meta: "Fp8Meta", dy_slot: int, x: torc
     ksplit = max(128, (Tp // splits + 127) // 128 * 128)
     nsplit = (Tp + ksplit - 1) // ksplit
     ws = gemm._workspace(nsplit * N * K, dy.device)[:nsplit * N * K].view(nsplit, N, K)
-    ext.gemm_fp8_wgrad(dyt, xt, ws, N, K, Tp, dy_meta.dscale[dy_slot:dy_slot + 1], x_meta.dscale[x_slot:x_slot + 1], ksplit)
+    ext.gemm_fp8_wgrad(dyt, xt, ws, N, K, Tp, dy_meta.dscale[dy_slot:dy_slot + 1], x_meta.dscale[x_slot:x_slot + 1], ksplit,
+                       dy_meta.fmt)
     ext.splitk_reduce(ws, nsplit, out, True)
     return out
 

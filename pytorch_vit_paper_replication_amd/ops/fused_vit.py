@@ -100,7 +100,7 @@ def _poison(t: torch.Tensor, skipped: bool) -> None:
 
 
 def _ln_grad_quant(f8d, which: int, shape, device):
-    """Producer-side e5m2 copy of a LayerNorm-backward output for gradient slot ``which`` of the fp8
+    """Producer-side fp8 copy (the gradient slot's format) of a LayerNorm-backward output for gradient slot ``which`` of the fp8
     block ``f8d = (Fp8State, block)``: (layernorm_bwd kwargs, (copy, dequant scale)) once the slot is
     calibrated, else ({}, None) (the first step calibrates it through the quantize pass)."""
     if f8d is None:
@@ -110,7 +110,7 @@ def _ln_grad_quant(f8d, which: int, shape, device):
         return {}, None
     meta, slot = prod
     q = torch.empty(shape, dtype=torch.uint8, device=device)
-    kw = dict(q_out=q, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1])
+    kw = dict(q_out=q, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1], q_fmt=meta.fmt)
     return kw, (q, meta.dscale[slot:slot + 1])
 
 
@@ -244,6 +244,7 @@ class EncoderBlockFn(torch.autograd.Function):
         own, prev = ctx.links
         f8d = ctx.f8d
 
+        # (the gradient copies below are e5m2, or e4m3 with enable_fp8(grad_fmt="e4m3"): Fp8State.grad.fmt)
         pre_q = {}  # grad slot -> (e5m2 copy, dequant scale) written by the producing dgrad epilogue
         grads8 = {}  # grad slot -> the e5m2 copy a dgrad GEMM consumed (reused by the fp8 weight gradients)
         acts8 = ctx.acts8
@@ -269,7 +270,8 @@ class EncoderBlockFn(torch.autograd.Function):
                 # the dGELU dgrad (fc2) also writes dU's e5m2 copy for the fc1 dgrad (grad slot 1)
                 nq = st.grad_producer(blk, 1) if dgelu_aux is not None else None
                 skip = skip_out and DGRAD_TAP is None and nq is not None
-                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq, skip_out=skip)
+                out = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=dgelu_aux, colsum=colsum, quant=nq, skip_out=skip,
+                                          g_fmt=st.grad.fmt)
                 if nq is not None:
                     out, pre_q[1] = out
                     _poison(out, skip)
@@ -362,7 +364,8 @@ class EncoderBlockFn(torch.autograd.Function):
                 # dQKV's bf16 copy is not stored when every reader takes the e5m2 copy: the qkv dgrad
                 # and weight gradient (both fp8) and the bias gradient (kernel partials, prow > 0)
                 q8_only = wgrad8_qkv and prow > 0 and DGRAD_TAP is None and T >= 256
-                q8kw = dict(q_out=q8, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1], q_only=q8_only)
+                q8kw = dict(q_out=q8, q_scale=meta.qscale[slot:slot + 1], q_amax=meta.amax[slot:slot + 1], q_only=q8_only,
+                            q_fmt=meta.fmt)
                 q8res = (q8, meta.dscale[slot:slot + 1])
         if prow > 0:
             # the attention backward emits per-(image, head, query block) column sums of dQ and dO

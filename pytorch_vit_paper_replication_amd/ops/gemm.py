@@ -284,8 +284,8 @@ def bias_grad(dy: torch.Tensor, db: Optional[torch.Tensor], *, drop: Drop = None
               dz: Optional[torch.Tensor] = None, quant=None):
     """db += column sums of (mask * dy); writes the masked gradient to dz when given.
 
-    ``quant=(meta, slot)`` (a calibrated e5m2 slot, ``Fp8Meta.producer``): the same pass writes the
-    (masked) gradient's e5m2 copy with the slot's delayed scale and records its amax; returns
+    ``quant=(meta, slot)`` (a calibrated gradient slot, ``Fp8Meta.producer``): the same pass writes the
+    (masked) gradient's fp8 copy in the slot's format with the slot's delayed scale and records its amax; returns
     ``(copy, dequant scale)`` then."""
     T, N = dy.shape
     seed, soff, p = _drop_args(drop)
@@ -295,5 +295,5 @@ def bias_grad(dy: torch.Tensor, db: Optional[torch.Tensor], *, drop: Drop = None
     meta, slot = quant
     q = torch.empty(T, N, dtype=torch.uint8, device=dy.device)
     _ext.ext().colsum(dy, T, N, db, dz, seed, soff, p, q_out=q, q_scale=meta.qscale[slot:slot + 1],
-                      q_amax=meta.amax[slot:slot + 1])
+                      q_amax=meta.amax[slot:slot + 1], q_fmt=meta.fmt)
     return q, meta.dscale[slot:slot + 1]

@@ -48,6 +48,8 @@ def run(path, args, init_sd, data):
         model.enable_fp8(wgrad=False)  # e4m3 forward, e5m2-gradient dgrad GEMMs, delayed scaling (wgrad bf16)
     elif path == "fused_fp8w":
         model.enable_fp8(dgrad=True, wgrad=True)  # + e5m2 x e4m3 weight-gradient GEMMs
+    elif path == "fused_fp8w4":
+        model.enable_fp8(dgrad=True, wgrad=True, grad_fmt="e4m3")  # the same with e4m3 gradients
     groups = param_groups_weight_decay(model, 0.03)
     opt = FusedAdam(groups, lr=args.lr) if fused else torch.optim.Adam(groups, lr=args.lr)
     sched = warmup_linear_decay(opt, args.steps, 0.05)
@@ -127,6 +129,9 @@ def main():
     p.add_argument("--fp8-study", type=int, default=0, metavar="SEEDS",
                    help="seed study: SEEDS inits x {fused bf16, fp8 fwd+dgrad, fp8 fwd+dgrad+wgrad}; prints the "
                         "per-variant mean / spread of the final loss and held-out accuracy")
+    p.add_argument("--variants", default="fused,fused_fp8,fused_fp8w",
+                   help="seed study: paths to train per seed (fused = bf16; fused_fp8 = fp8 fwd+dgrad; fused_fp8w = "
+                        "+ fp8 weight gradients; fused_fp8w4 = the same with e4m3 gradients)")
     p.add_argument("--seed-start", type=int, default=0, help="seed study: first seed (studies split over runs)")
     p.add_argument("--stop-at", type=int, default=0, help="train only this many steps of the --steps schedule")
     p.add_argument("--checkpoints", default="", help="seed study: comma-separated steps whose windowed mean loss "
@@ -186,7 +191,7 @@ def fp8_study(args):
     tr = make_data(args.train_size, args.classes, args.image_size, gen, dev, templates)
     te = make_data(args.test_size, args.classes, args.image_size, gen, dev, templates)
     k = max(1, args.steps // 10)
-    res = {v: [] for v in ("fused", "fused_fp8", "fused_fp8w")}
+    res = {v: [] for v in args.variants.split(",")}
     ckpts = [int(c) for c in args.checkpoints.split(",") if c]
     for seed in range(args.seed_start, args.seed_start + args.fp8_study):
         torch.manual_seed(seed)

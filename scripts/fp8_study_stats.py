@@ -31,7 +31,8 @@ def main():
     for st in steps:
         b = [base[s][st] for s in seeds]
         bm, bs = sum(b) / len(b), stats.tstd(b) if len(b) > 1 else 0.0
-        for v in ("fused_fp8", "fused_fp8w"):
+        for v in [v for v in ("fused_fp8", "fused_fp8w", "fused_fp8w4") if v in runs] + sorted(
+                v for v in runs if v not in ("fused", "fused_fp8", "fused_fp8w", "fused_fp8w4")):
             if v not in runs:
                 continue
             sv = [s for s in seeds if s in runs[v] and st in runs[v][s]]
@@ -45,6 +46,21 @@ def main():
             out["rows"].append({"step": st, "variant": v, "mean": m, "std": sd, "bf16_mean": bm, "bf16_std": bs,
                                 "diff_mean": dm, "diff_std": dsd, "p_paired": p, "within_1sd": bool(within)})
             print(f"| {st} | {v} | {m:.4f} +- {sd:.4f} | {bm:.4f} +- {bs:.4f} | {dm:+.4f} +- {dsd:.4f} | {p:.3f} | {'yes' if within else 'no'} |")
+    if "fused_fp8w" in runs and "fused_fp8w4" in runs:  # e4m3 vs e5m2 gradients, paired by seed
+        print("\n| step | e4m3 grads | e5m2 grads | paired diff (e4m3 - e5m2) | paired t-test p |")
+        print("|---:|---:|---:|---:|---:|")
+        for st in steps:
+            sv = [s for s in seeds if st in runs["fused_fp8w"].get(s, {}) and st in runs["fused_fp8w4"].get(s, {})]
+            if len(sv) < 2:
+                continue
+            a4 = [runs["fused_fp8w4"][s][st] for s in sv]
+            a5 = [runs["fused_fp8w"][s][st] for s in sv]
+            d = [x - y for x, y in zip(a4, a5)]
+            p = float(stats.ttest_rel(a4, a5).pvalue)
+            out.setdefault("e4m3_vs_e5m2", []).append({"step": st, "e4m3": sum(a4) / len(a4), "e5m2": sum(a5) / len(a5),
+                                                       "diff_mean": sum(d) / len(d), "diff_std": stats.tstd(d), "p_paired": p})
+            print(f"| {st} | {sum(a4) / len(a4):.4f} +- {stats.tstd(a4):.4f} | {sum(a5) / len(a5):.4f} +- {stats.tstd(a5):.4f} | "
+                  f"{sum(d) / len(d):+.4f} +- {stats.tstd(d):.4f} | {p:.3f} |")
     print(json.dumps(out))
 
 

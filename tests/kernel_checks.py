@@ -643,10 +643,11 @@ def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
             lim(5e-3, 1e-2, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
 
 
-def check_attn_bwd_q8(B, N, H, dh=64, p=0.0):
-    """The attention backward's own e5m2 copy of dQKV (fp8 recipe, grad slot 3) vs quantizing its bf16
-    dQKV: same bytes up to the double rounding bf16 -> e5m2 (the kernel rounds the fp32 value once),
-    i.e. at most one e5m2 step apart on a tiny fraction of elements; the amax record is max |dQKV|."""
+def check_attn_bwd_q8(B, N, H, dh=64, p=0.0, fmt=1):
+    """The attention backward's own fp8 copy of dQKV (fp8 recipe, grad slot 3; fmt 1 e5m2, 0 e4m3) vs
+    quantizing its bf16 dQKV: same bytes up to the double rounding bf16 -> fp8 (the kernel rounds the
+    fp32 value once), i.e. at most one fp8 step apart on a tiny fraction of elements; the amax record
+    is max |dQKV|."""
     ext = _ext.ext()
     D = H * dh
     sc = 1.0 / math.sqrt(dh)
@@ -654,13 +655,16 @@ def check_attn_bwd_q8(B, N, H, dh=64, p=0.0):
     seed = torch.tensor([4321], dtype=torch.int64, device=DEV) if p > 0 else None
     o, lse = ext.attn_fwd(qkv, B, N, H, sc, seed, 5 << 32, p)
     do = bf(rnd(B * N, D))
-    qs = torch.tensor([3000.0], device=DEV)
+    qs = torch.tensor([3000.0 if fmt else 20.0], device=DEV)
     amax = torch.zeros(1, dtype=torch.int32, device=DEV)
     q8 = torch.full((B * N, 3 * D), 0xAB, dtype=torch.uint8, device=DEV)
-    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, sc, None, None, seed, 5 << 32, p, q_out=q8, q_scale=qs, q_amax=amax)
-    got = q8.view(torch.float8_e5m2).float()
-    ref = (dqkv.float() * qs).clamp(-57344, 57344).to(torch.float8_e5m2).float()
-    step = ref.abs() * 0.25 + 1e-30  # one e5m2 step (2 mantissa bits) at the reference magnitude
+    dqkv = ext.attn_bwd(do, qkv, o, lse, B, N, H, sc, None, None, seed, 5 << 32, p, q_out=q8, q_scale=qs, q_amax=amax,
+                        q_fmt=fmt)
+    f8t, fmax = (torch.float8_e5m2, 57344) if fmt else (torch.float8_e4m3fn, 448)
+    got = q8.view(f8t).float()
+    ref = (dqkv.float() * qs).clamp(-fmax, fmax).to(f8t).float()
+    # one fp8 step at the reference magnitude: 2 / 3 mantissa bits, the subnormal spacing (2^-16 / 2^-9) below
+    step = torch.clamp(ref.abs() * (0.25 if fmt else 0.125), min=2.0 ** -16 if fmt else 2.0 ** -9)
     far = ((got - ref).abs() > step * 1.01).float().mean().item()
     diff = (got != ref).float().mean().item()
     am = amax.view(torch.float32).item()
@@ -668,7 +672,9 @@ def check_attn_bwd_q8(B, N, H, dh=64, p=0.0):
     m = {"beyond_one_step": far, "differ_frac": diff, "amax_rel": abs(am - am_ref) / am_ref}
     # differ_frac: bf16 keeps 6 bits past e5m2's 2, so ~1/64 of the bf16 values sit exactly on an e5m2
     # rounding midpoint and about half of those round the other way than the fp32 value (1.0e-2 measured)
-    return (f"attn_bwd e5m2 dQKV copy B{B} N{N} H{H} dh{dh} p{p}", m, {"beyond_one_step": 0, "differ_frac": 2.5e-2, "amax_rel": 8e-3})
+    # (e4m3 keeps 5 bits fewer than bf16: ~1/32 of the values on a midpoint, differ_frac ~2x e5m2's)
+    return (f"attn_bwd {'e5m2' if fmt else 'e4m3'} dQKV copy B{B} N{N} H{H} dh{dh} p{p}", m,
+            {"beyond_one_step": 0, "differ_frac": 2.5e-2 if fmt else 4.5e-2, "amax_rel": 8e-3})
 
 
 def check_attn_dropout(B, N, H, dh=64, p=0.1):
@@ -904,7 +910,7 @@ def check_layernorm_fwd_q8(T=3000, D=1280):
     return (f"layernorm_fwd_q8 T{T} D{D}", m, {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 4e-3, "ln_not_identical": 0})
 
 
-def check_layernorm_bwd_q8(T=3000, D=1280, linked=False, p=0.1):
+def check_layernorm_bwd_q8(T=3000, D=1280, linked=False, p=0.1, fmt=1):
     """LayerNorm backward with the fused e5m2 copy of the gradient it writes last (dz with the linked
     dropout backward, else dx): dx / dz / dgamma / dbeta / dsum bit-identical to the plain backward
     (f32 atomics aside: the same kernel order), the copy within one fp8 step of quantizing the bf16
@@ -916,7 +922,7 @@ def check_layernorm_bwd_q8(T=3000, D=1280, linked=False, p=0.1):
     w, b = rnd(D) * 0.5 + 1, rnd(D) * 0.1
     _, mean, rstd = ext.layernorm_fwd(x, w, b, 1e-5, T, D)
     dy, dres = bf(rnd(T, D)), bf(rnd(T, D))
-    meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2)
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=fmt)
     meta.calibrated[0] = True
     meta.qscale.fill_(2.0)
     meta.dscale.copy_(1.0 / meta.qscale)
@@ -929,24 +935,24 @@ def check_layernorm_bwd_q8(T=3000, D=1280, linked=False, p=0.1):
         q = None
         if quant:
             q = torch.empty(T, D, dtype=torch.uint8, device=DEV)
-            kw.update(q_out=q, q_scale=meta.qscale[0:1], q_amax=meta.amax[0:1])
+            kw.update(q_out=q, q_scale=meta.qscale[0:1], q_amax=meta.amax[0:1], q_fmt=fmt)
         ext.layernorm_bwd(dy, D, x, D, mean, rstd, w, dres, D, dx, D, dw, db, T, **kw)
         outs.append((dx, dz, dw, db, ds, q))
     (dx0, dz0, dw0, db0, ds0, _), (dx1, dz1, dw1, db1, ds1, q) = outs
     y = dz1 if linked else dx1
     ref = torch.empty(T, D, dtype=torch.uint8, device=DEV)
-    ext.fp8_quant(y, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), F8.E5M2)
+    ext.fp8_quant(y, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), fmt)
     amax = meta.amax.view(torch.float32)[0].item()
     same = torch.equal(dx0, dx1) and (not linked or torch.equal(dz0, dz1))
     sums = max(errs(dw1, dw0)[0], errs(db1, db0)[0], errs(ds1, ds0)[0])
     m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
          "amax_rel": abs(amax - y.float().abs().max().item()) / y.float().abs().max().item(),
          "grad_not_identical": float(not same), "sums_l2": sums}
-    return (f"layernorm_bwd_q8 e5m2 T{T} D{D} linked{int(linked)}", m,
+    return (f"layernorm_bwd_q8 {'e5m2' if fmt else 'e4m3'} T{T} D{D} linked{int(linked)}", m,
             {"fp8_steps": 1, "mismatch_frac": 0.05, "amax_rel": 8e-3, "grad_not_identical": 0, "sums_l2": 1e-6})  # amax: bf16 rounding <= 2^-8
 
 
-def check_colsum_q8(T=4000, N=3840):
+def check_colsum_q8(T=4000, N=3840, fmt=1):
     """Column sums (the in_proj bias gradient over all of dQKV) fused with dQKV's e5m2 copy: the sums
     as the plain column-sum pass, the copy as the quantize pass with the same scale (the inputs are
     the bf16 values themselves, so the bytes should agree), amax = max|dy|."""
@@ -954,7 +960,7 @@ def check_colsum_q8(T=4000, N=3840):
 
     ext = _ext.ext()
     dy = bf(rnd(T, N) * 0.3)
-    meta = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2)
+    meta = F8.Fp8Meta(1, DEV, history=1, fmt=fmt)
     meta.calibrated[0] = True
     meta.qscale.fill_(8.0)
     meta.dscale.copy_(1.0 / meta.qscale)
@@ -962,12 +968,12 @@ def check_colsum_q8(T=4000, N=3840):
     G.bias_grad(dy, db0)
     q, ds = G.bias_grad(dy, db1, quant=meta.producer(0))
     ref = torch.empty(T, N, dtype=torch.uint8, device=DEV)
-    ext.fp8_quant(dy, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), F8.E5M2)
+    ext.fp8_quant(dy, ref, meta.qscale[0:1], torch.zeros(1, dtype=torch.int32, device=DEV), fmt)
     amax = meta.amax.view(torch.float32)[0].item()
     m = {"fp8_steps": _fp8_code_dist(q, ref), "mismatch_frac": (q != ref).float().mean().item(),
          "amax_rel": abs(amax - dy.float().abs().max().item()) / dy.float().abs().max().item(),
          "colsum_l2": errs(db1, db0)[0], "colsum_vs_fp32_l2": errs(db1, dy.float().sum(0))[0]}
-    return (f"colsum + e5m2 copy T{T} N{N}", m,
+    return (f"colsum + {'e5m2' if fmt else 'e4m3'} copy T{T} N{N}", m,
             {"fp8_steps": 1, "mismatch_frac": 1e-3, "amax_rel": 1e-6, "colsum_l2": 1e-6, "colsum_vs_fp32_l2": 1e-5})
 
 
@@ -1019,7 +1025,7 @@ def check_fp8_transpose(T=1000, C=1280, fmt=1):
     return (f"fp8_transpose T{T} C{C} fmt{fmt}", {"bytes_differ": float((a != b).sum().item())}, {"bytes_differ": 0})
 
 
-def check_wgrad_fp8_mn(T, N, K):
+def check_wgrad_fp8_mn(T, N, K, gfmt=1):
     """fp8 weight gradient read straight from the row-major fp8 copies (mn-contiguous operands,
     ds_read_b64_tr_b8 fragments) vs the byte-transposed copies through the k-contiguous GEMM (the same
     fp8 operands: equal up to fp32 summation order) and vs the exact product of the dequantized
@@ -1028,7 +1034,7 @@ def check_wgrad_fp8_mn(T, N, K):
 
     ext = _ext.ext()
     dy, x = bf(rnd(T, N)), bf(rnd(T, K))
-    gm, am = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2), F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+    gm, am = F8.Fp8Meta(1, DEV, history=1, fmt=gfmt), F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
     dy8, _ = gm.quantize(dy, 0)
     x8, _ = am.quantize(x, 0)
     out_mn = torch.zeros(N, K, device=DEV)
@@ -1039,20 +1045,20 @@ def check_wgrad_fp8_mn(T, N, K):
         F8.linear_wgrad_fp8(dy, gm, 0, x, am, 0, out_t, dy8, x8)
     finally:
         F8.WGRAD_MN = True
-    dyd = ext.fp8_dequant(dy8.contiguous(), gm.dscale[0:1], 1)
+    dyd = ext.fp8_dequant(dy8.contiguous(), gm.dscale[0:1], gfmt)
     xd = ext.fp8_dequant(x8.contiguous(), am.dscale[0:1], 0)
     m = worst((out_mn, dyd.t() @ xd))
     m["vs_transposed_l2"] = errs(out_mn, out_t)[0]
-    return (f"wgrad fp8 mn-contiguous T{T} N{N} K{K}", m, lim(2.5e-5, 5e-5, vs_transposed_l2=1e-6))
+    return (f"wgrad fp8 mn-contiguous {'e5m2' if gfmt else 'e4m3'} T{T} N{N} K{K}", m, lim(2.5e-5, 5e-5, vs_transposed_l2=1e-6))
 
 
-def check_wgrad_fp8(T, N, K):
+def check_wgrad_fp8(T, N, K, gfmt=1):
     """dW = dequant(dy^T (e5m2) . x (e4m3)) from the transposed quantize passes + split-K fp8 GEMM,
     against the exact product of the same quantized operands and against bf16."""
     from pytorch_vit_paper_replication_amd.ops import fp8 as F8
 
     dy, x = bf(rnd(T, N)), bf(rnd(T, K))
-    gm, am = F8.Fp8Meta(1, DEV, history=1, fmt=F8.E5M2), F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
+    gm, am = F8.Fp8Meta(1, DEV, history=1, fmt=gfmt), F8.Fp8Meta(1, DEV, history=1, fmt=F8.E4M3)
     _, gs = gm.quantize(dy, 0, current=True)
     _, xs = am.quantize(x, 0, current=True)
     out = torch.zeros(N, K, device=DEV)
@@ -1060,29 +1066,29 @@ def check_wgrad_fp8(T, N, K):
     ext = _ext.ext()  # reference from the same fp8 values (non-transposed quantize, dequantized)
     q1 = torch.empty(T, N, dtype=torch.uint8, device=DEV)
     q2 = torch.empty(T, K, dtype=torch.uint8, device=DEV)
-    ext.fp8_quant(dy, q1, gm.qscale[0:1], gm.amax[0:1], F8.E5M2)
+    ext.fp8_quant(dy, q1, gm.qscale[0:1], gm.amax[0:1], gfmt)
     ext.fp8_quant(x, q2, am.qscale[0:1], am.amax[0:1], F8.E4M3)
-    dyd = ext.fp8_dequant(q1, gs, F8.E5M2).view(T, N)
+    dyd = ext.fp8_dequant(q1, gs, gfmt).view(T, N)
     xd = ext.fp8_dequant(q2, xs, F8.E4M3).view(T, K)
     m = worst((out, dyd.t() @ xd))
     m["bf16_l2"] = errs(out, dy.float().t() @ x.float())[0]
-    return (f"wgrad_fp8 e5m2^T x e4m3 T{T} N{N} K{K}", m, lim(2.5e-5, 4e-5, bf16_l2=1.2e-1))
+    return (f"wgrad_fp8 {'e5m2' if gfmt else 'e4m3'}^T x e4m3 T{T} N{N} K{K}", m, lim(2.5e-5, 4e-5, bf16_l2=1.2e-1))
 
 
-def check_dgrad_fp8(M, N, K):
+def check_dgrad_fp8(M, N, K, gfmt=1):
     """dX = dequant(g (e5m2) . W (e4m3)) with the dGELU epilogue and the fused bias-grad column sum."""
     from pytorch_vit_paper_replication_amd.ops import fp8 as F8
 
     g, wt = bf(rnd(M, N)), bf(rnd(K, N, scale=0.05))
     aux = bf(rnd(M, K))
-    gq, gs, gd = _fp8_operand(g, 1)
+    gq, gs, gd = _fp8_operand(g, gfmt)
     wq, ws, wd = _fp8_operand(wt, 0)
     cs = torch.zeros(K, device=DEV)
-    y = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=aux, colsum=cs)
+    y = F8.linear_dgrad_fp8(gq, gs, wq, ws, dgelu_aux=aux, colsum=cs, g_fmt=gfmt)
     ref = (gd @ wd.t()) * aux.float()
     m = worst((y, ref))
     m["colsum_l2"], m["colsum_max"] = errs(cs, ref.sum(0))
-    return (f"dgrad_fp8 e5m2 x e4m3 dGELU M{M} N{N} K{K}", m, lim(3.5e-3, 5e-3, colsum_l2=2.5e-5, colsum_max=3e-5))
+    return (f"dgrad_fp8 {'e5m2' if gfmt else 'e4m3'} x e4m3 dGELU M{M} N{N} K{K}", m, lim(3.5e-3, 5e-3, colsum_l2=2.5e-5, colsum_max=3e-5))
 
 
 _FP8_CFG = dict(image_size=64, patch_size=16, num_transformer_layer=2, num_heads=2, embedding_dim=256, mlp_size=512,
@@ -1286,6 +1292,45 @@ def check_vit_fp8_wgrad(B=4):
     met = {"l2": max(e for _, e in per), "loss_not_falling": float(not ok or len(per) != 4 * _FP8_CFG["num_transformer_layer"])}
     return (f"vit fp8 wgrad per-tensor vs bf16 wgrad, loss {losses[0]:.3f}->{losses[-1]:.3f}", met,
             {"l2": 1.6e-1, "loss_not_falling": 0})
+
+
+def check_vit_fp8_grad_formats(B=4):
+    """e4m3 vs e5m2 gradients in the fp8 dgrad / wgrad GEMMs (enable_fp8(grad_fmt=...)): every encoder
+    parameter gradient of the fully fp8 backward against the bf16-backward gradients of the same
+    fp8-forward model (identical calibrated passes). e4m3's extra mantissa bit must lower the mean
+    per-tensor error (the captured-operand study, profiles/r6/mx_study, measured -40 % on the weight
+    gradients), and training with e4m3 gradients must decrease the loss."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops.fused_vit import cross_entropy
+
+    torch.manual_seed(0)
+    m = ViT(**_FP8_CFG).to(DEV)
+    x = torch.rand(B * 64, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (B * 64,), device=DEV)
+    names = [n for n, p in m.named_parameters() if "encoder" in n]
+
+    def grads(dgrad: bool, fmt: str):
+        m.enable_fp8(dgrad=dgrad, wgrad=dgrad, grad_fmt=fmt)  # a new format: fresh scaling state
+        for _ in range(2):  # the first pass calibrates every slot (its weight gradients are bf16)
+            m.zero_grad(set_to_none=False)
+            cross_entropy(m(x), y).backward()
+        torch.cuda.synchronize()
+        assert m._fp8 is not None and m._fp8.grad.fmt == (0 if fmt == "e4m3" else 1)
+        return {n: p.grad.float().clone() for n, p in m.named_parameters() if n in names}
+
+    ref = grads(False, "e5m2")
+    e5 = grads(True, "e5m2")
+    e4 = grads(True, "e4m3")
+    err5 = [errs(e5[n], ref[n])[0] for n in names]
+    err4 = [errs(e4[n], ref[n])[0] for n in names]
+    mean5, mean4 = sum(err5) / len(err5), sum(err4) / len(err4)
+    print(f"fp8 gradient formats, mean per-tensor rel-L2 vs bf16 backward: e5m2 {mean5:.3e}, e4m3 {mean4:.3e} "
+          f"(ratio {mean4 / mean5:.2f})")
+    m.enable_fp8(dgrad=True, wgrad=True, grad_fmt="e4m3")
+    losses, ok = _train_losses(m, x, y)
+    met = {"e4m3_over_e5m2": mean4 / mean5, "e4m3_max_l2": max(err4), "loss_not_falling": float(not ok)}
+    return (f"vit fp8 e4m3 vs e5m2 gradients: mean rel-L2 {mean4:.2e} vs {mean5:.2e}, e4m3 loss {losses[0]:.3f}->{losses[-1]:.3f}",
+            met, {"e4m3_over_e5m2": 0.9, "e4m3_max_l2": 1.6e-1, "loss_not_falling": 0})
 
 
 def check_fp8_nonfinite_recovery(B=2):
@@ -1759,6 +1804,18 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_fwd_head_qf(4, 197, 12),
         lambda: check_attn_fwd_head_qf(3, 17, 2),
         lambda: check_attn_fwd_head_qf(2, 256, 4),
+        # e4m3 gradients (enable_fp8(grad_fmt="e4m3")): every kernel that writes or reads a gradient copy
+        lambda: check_attn_bwd_q8(2, 257, 3, 80, fmt=0),
+        lambda: check_attn_bwd_q8(2, 577, 2, 64, fmt=0),
+        lambda: check_attn_bwd_q8(3, 197, 2, 80, 0.1, fmt=0),
+        lambda: check_layernorm_bwd_q8(fmt=0),
+        lambda: check_layernorm_bwd_q8(2000, 768, linked=True, fmt=0),
+        lambda: check_colsum_q8(1001, 2304, fmt=0),
+        lambda: check_wgrad_fp8_mn(1000, 1280, 512, gfmt=0),
+        lambda: check_wgrad_fp8_mn(300, 768, 256, gfmt=0),
+        lambda: check_wgrad_fp8(1000, 1280, 512, gfmt=0),
+        lambda: check_dgrad_fp8(1030, 1280, 768, gfmt=0),
+        check_vit_fp8_grad_formats,
     ]
     return c
 
