@@ -97,10 +97,10 @@ def deterministic() -> bool:
     weight gradients are reduced in a fixed order, so a training step produces the same bits on every
     run. Off by default: the float-atomic reductions are order-dependent in the last bits.
 
-    Not covered: the attention backward at sequence lengths with several 256-key blocks that take
-    neither its last-key nor its tail-split slab path (e.g. N = 677) still sums dQ with float atomics
-    (the extension warns once when deterministic mode meets such a shape). Every shape of the
-    BASELINE models (N = 197, 257, 577) is covered.
+    The attention backward at sequence lengths with several 256-key blocks that take neither its
+    last-key nor its tail-split slab path (e.g. N = 400, 677) sums dQ with float atomics by default;
+    in deterministic mode each key block stores an f32 dQ slab and one pass sums the slabs in key-block
+    order (``dq_slab_sum_kernel``; ``tests/kernel_checks.py::check_attn_bwd_det``).
 
     Each fused backward entry point calls this, so the native flag follows
     ``torch.use_deterministic_algorithms`` from the first backward kernel of a step on."""

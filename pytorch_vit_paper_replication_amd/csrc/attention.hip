@@ -1613,6 +1613,18 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_pipe8_kernel(const uint16_t* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
 }
 
+// Deterministic dQ of a multi-key-block head without the tail-split slab path: dQ = the key blocks'
+// f32 partial slabs (mode-3 launch, slab s = key block s) summed in slab order, as bf16.
+__global__ void __launch_bounds__(256) dq_slab_sum_kernel(const float* __restrict__ slab, int nslab, int64_t sstride,
+                                                           uint16_t* __restrict__ dqkv, int64_t ld_dq, int64_t rows, int D) {
+  const int64_t n = rows * D;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float v = slab[i];
+    for (int k = 1; k < nslab; ++k) v += slab[k * sstride + i];
+    dqkv[(i / D) * ld_dq + i % D] = f2bf(v);
+  }
+}
+
 __global__ void __launch_bounds__(256) dq_convert_kernel(float* __restrict__ acc, uint16_t* __restrict__ dqkv, int64_t ld_dq,
                                                           int64_t rows, int D, int rezero) {
   const int64_t n = rows * D;
@@ -1867,9 +1879,10 @@ static bool attn_bwd_bpart_ok(int N, int DH) {
   return (N + KB - 1) / KB == 1 && NE <= pvr_attn_bwd_waves(N);
 }
 
-// 1 if pvr_attn_bwd needs the zero-initialised f32 dQ workspace for this shape
-extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias, int drop) {
-  if (pvr_attn_bwd_key_blocks(N) <= 1) return 0;
+// 1 if pvr_attn_bwd needs the zero-initialised f32 dQ workspace for this shape (det: deterministic
+// mode, where such shapes sum per-key-block dQ slabs in a fixed order instead: no workspace)
+extern "C" int pvr_attn_bwd_needs_dq_acc(int N, int dh, int dbias, int drop, int det) {
+  if (pvr_attn_bwd_key_blocks(N) <= 1 || det) return 0;
   return attn_bwd_lastkey_path(N, dbias != 0, drop != 0) || attn_bwd_slab_path(N, dbias != 0, drop != 0) ? 0 : 1;
 }
 
@@ -1916,7 +1929,9 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
   const int rem_ = N % KB;
   const bool tail_split = !lastkey && nkb > 1 && rem_ >= 16 && rem_ <= 128 && !dbias;
   const bool slab_path = tail_split;
-  if (nkb > 1 && !dq_acc && !lastkey && !slab_path) return hipErrorInvalidValue;
+  // no dQ accumulator for a shape that would need one: deterministic mode (pvr_attn_bwd_needs_dq_acc),
+  // per-key-block slabs in the scratch past the pre-pass outputs, summed in a fixed order
+  const bool det_slab = nkb > 1 && !dq_acc && !lastkey && !slab_path;
   if (dbias && 2 * Hd<DH>::NE > 2 * NW) return hipErrorInvalidValue;  // q-bias sums: <= 2 fragments per wave
   if (!ws) return hipErrorInvalidValue;
   const int RB = 128 * Hd<DH>::NH;
@@ -1932,7 +1947,7 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
   // pre-pass: delta (and, on the lastkey path, key N - 1's dS / dK / dV)
   float* dlt = ws;
   float* dsl = lastkey ? ws + (int64_t)B * H * N : nullptr;
-  float* slab = slab_path ? ws + 2 * (int64_t)B * H * N : nullptr;  // [N / KB + 1][B*N][D] f32 partial dQ
+  float* slab = slab_path || det_slab ? ws + 2 * (int64_t)B * H * N : nullptr;  // [N / KB + 1][B*N][D] f32 partial dQ
   if (lastkey)
     hipLaunchKernelGGL((attn_bwd_prep_kernel<DH, true>), dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dlt, dsl,
                        bpart, dqkv, ld_dq, N, H, D, scale, q8);
@@ -1967,6 +1982,14 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
     launch(pvr_attn_bwd_waves(rem), N - rem, N, 4, slab, sstride, nslab, bpart);
     return hipGetLastError();
   }
+  if (det_slab) {
+    const int64_t rows = (int64_t)B * N, sstride = rows * D;
+    launch(NW, 0, N, 3, slab, sstride, 0, nullptr);
+    int64_t blocks = (rows * D + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(dq_slab_sum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, nkb, sstride, dqkv, ld_dq, rows, D);
+    return hipGetLastError();
+  }
   launch(NW, 0, N, 0, nkb > 1 ? dq_acc : nullptr, 0, 0, nkb > 1 ? nullptr : bpart);
   if (nkb > 1) {
     const int64_t rows = (int64_t)B * N;
@@ -1991,10 +2014,15 @@ static hipError_t attn_bwd_launch(const uint16_t* qkv, int64_t ld, const uint16_
                                      drop, q8, s);
 }
 
-// floats of the f32 scratch pvr_attn_bwd needs (per-query delta and, on the lastkey path, ds_last)
-extern "C" int64_t pvr_attn_bwd_ws_floats(int B, int N, int H, int D, int dbias, int drop) {
+// floats of the f32 scratch pvr_attn_bwd needs (per-query delta and, on the lastkey path, ds_last;
+// dQ slabs on the tail-split path, and in deterministic mode (det) on multi-key-block shapes without it)
+extern "C" int64_t pvr_attn_bwd_ws_floats(int B, int N, int H, int D, int dbias, int drop, int det) {
   int64_t n = 2 * (int64_t)B * H * N;
-  if (attn_bwd_slab_path(N, dbias != 0, drop != 0)) n += (int64_t)(N / (32 * pvr_attn_bwd_waves(N)) + 1) * B * N * D;
+  const int KB = 32 * pvr_attn_bwd_waves(N);
+  if (attn_bwd_slab_path(N, dbias != 0, drop != 0))
+    n += (int64_t)(N / KB + 1) * B * N * D;
+  else if (det && pvr_attn_bwd_key_blocks(N) > 1 && !attn_bwd_lastkey_path(N, dbias != 0, drop != 0))
+    n += (int64_t)((N + KB - 1) / KB) * B * N * D;
   return n;
 }
 

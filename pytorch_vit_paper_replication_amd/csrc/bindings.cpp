@@ -68,7 +68,7 @@ hipError_t pvr_fp8_quant_t(const uint16_t*, int64_t, uint8_t*, int64_t, int, int
 hipError_t pvr_fp8_transpose(const uint8_t*, int64_t, uint8_t*, int64_t, int, int, hipStream_t);
 hipError_t pvr_fp8_quant_multi(const int64_t*, int, int64_t, const float*, unsigned*, int, int, hipStream_t);
 int pvr_attn_bwd_key_blocks(int);
-int pvr_attn_bwd_needs_dq_acc(int, int, int, int);
+int pvr_attn_bwd_needs_dq_acc(int, int, int, int, int);
 int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
 int pvr_attn_bwd_part_rows(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
@@ -81,7 +81,7 @@ hipError_t pvr_attn_dbias_reduce(const float*, float*, float*, int, int, int, in
 hipError_t pvr_attn_bwd(const uint16_t*, int64_t, const uint16_t*, int64_t, const uint16_t*, int64_t, const float*, uint16_t*, int64_t, float*, int, float*, float*, float*, int, int, int, int, float,
                         const uint64_t*, uint64_t, uint32_t, float, uint8_t*, int64_t, const float*, unsigned*,
                         int, int, hipStream_t);
-int64_t pvr_attn_bwd_ws_floats(int, int, int, int, int, int);
+int64_t pvr_attn_bwd_ws_floats(int, int, int, int, int, int, int);
 int pvr_attn_bwd_q8_ok(int, int);
 }
 
@@ -1041,12 +1041,9 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
       old_part = torch::empty({B * pvr_attn_bwd_key_blocks((int)N), 3 * D}, qkv.options().dtype(torch::kFloat32));
   }
   const int old_db = old_part.defined() ? 1 : 0;
-  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)dh, old_db, has_drop)) {
+  if (pvr_attn_bwd_needs_dq_acc((int)N, (int)dh, old_db, has_drop, g_deterministic ? 1 : 0)) {
     // several key blocks per head and neither the lastkey nor the tail-split slab path (e.g. N = 677):
-    // dQ is summed with f32 atomics, which deterministic mode does not replace for this shape
-    if (g_deterministic)
-      TORCH_WARN_ONCE("deterministic mode: the attention backward at N = ", N,
-                      " accumulates dQ with float atomics (several key blocks, no slab path); dQ is not bitwise repeatable");
+    // dQ is summed with f32 atomics (deterministic mode: per-key-block slabs summed in order instead)
     dq_acc = dq_workspace(B * N * D, qkv.options());
     dq_rezero = dq_acc.defined() ? 1 : 0;
     if (!dq_acc.defined()) dq_acc = torch::zeros({B * N, D}, qkv.options().dtype(torch::kFloat32));
@@ -1075,7 +1072,7 @@ torch::Tensor attn_bwd(torch::Tensor dout, torch::Tensor qkv, torch::Tensor out,
   // pre-pass outputs of the generic backward (per-query delta, lastkey path: ds_last; slab path: dQ
   // slabs): a persistent per-(device, stream) scratch, so the slab path (~0.9 GB per ViT-L/16@384
   // b128 layer) is not allocated on every backward
-  auto ws = attn_scratch(pvr_attn_bwd_ws_floats((int)B, (int)N, (int)H, (int)D, old_db, has_drop), qkv.options());
+  auto ws = attn_scratch(pvr_attn_bwd_ws_floats((int)B, (int)N, (int)H, (int)D, old_db, has_drop, g_deterministic ? 1 : 0), qkv.options());
   const hipError_t err = pvr_attn_bwd(bf(qkv, "qkv"), lds[0], bf(out, "out"), lds[2], bf(dout, "dout"), lds[1], f32(lse, "lse"),
                                       bf_mut(dqkv, "dqkv"), lds[3], dq_acc.defined() ? dq_acc.data_ptr<float>() : nullptr, dq_rezero,
                                       dbias_arg, bpart_arg, ws.data_ptr<float>(), (int)B, (int)N, (int)H, (int)D, (float)scale,

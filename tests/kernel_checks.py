@@ -643,6 +643,38 @@ def check_attn_bwd(B, N, H, dh=64, fused_bias=False):
             lim(5e-3, 1e-2, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
 
 
+def check_attn_bwd_det(B, N, H, dh=64, fused_bias=False):
+    """Deterministic mode on a multi-key-block shape with neither the lastkey nor the tail-split slab
+    path (N = 677 = 2 x 256 + 165): per-key-block f32 dQ slabs summed in a fixed order instead of f32
+    atomics. Two backward calls are bitwise equal, and dQ|dK|dV (and the bias gradient) match the fp32
+    reference as in check_attn_bwd."""
+    ext = _ext.ext()
+    D = H * dh
+    sc = 1.0 / math.sqrt(dh)
+    qkv = bf(rnd(B * N, 3 * D))
+    o, lse = ext.attn_fwd(qkv, B, N, H, sc)
+    do = bf(rnd(B * N, D))
+    was = ext.deterministic()
+    ext.set_deterministic(True)
+    try:
+        outs = []
+        for _ in range(2):
+            dbias = torch.zeros(3 * D, device=DEV) if fused_bias else None
+            outs.append((ext.attn_bwd(do, qkv, o, lse, B, N, H, sc, dbias), dbias))
+    finally:
+        ext.set_deterministic(was)
+    (d0, b0), (d1, b1) = outs
+    qr = qkv.float().requires_grad_(True)
+    oref, _ = _attn_ref(qr, B, N, H)
+    oref.backward(do.float())
+    m = worst((d0, qr.grad))
+    m["not_bitwise_repeatable"] = float(not (torch.equal(d0, d1) and (not fused_bias or torch.equal(b0, b1))))
+    if fused_bias:
+        m["dbias_l2"], m["dbias_max"] = errs(b0, qr.grad.sum(0))
+    return (f"attn_bwd deterministic ordered dQ slabs B{B} N{N} H{H} dh{dh} dbias{int(fused_bias)}", m,
+            lim(5e-3, 1e-2, not_bitwise_repeatable=0, **({"dbias_l2": 1.6e-3, "dbias_max": 1e-3} if fused_bias else {})))
+
+
 def check_attn_bwd_q8(B, N, H, dh=64, p=0.0, fmt=1):
     """The attention backward's own fp8 copy of dQKV (fp8 recipe, grad slot 3; fmt 1 e5m2, 0 e4m3) vs
     quantizing its bf16 dQKV: same bytes up to the double rounding bf16 -> fp8 (the kernel rounds the
@@ -1816,6 +1848,10 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_wgrad_fp8(1000, 1280, 512, gfmt=0),
         lambda: check_dgrad_fp8(1030, 1280, 768, gfmt=0),
         check_vit_fp8_grad_formats,
+        # deterministic mode, multi-key-block shapes without the slab / lastkey paths: ordered dQ slabs
+        lambda: check_attn_bwd_det(2, 677, 2),
+        lambda: check_attn_bwd_det(2, 677, 3, 64, True),
+        lambda: check_attn_bwd_det(1, 400, 2, 80),
     ]
     return c
 
