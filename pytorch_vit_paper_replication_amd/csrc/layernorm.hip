@@ -420,6 +420,10 @@ extern "C" hipError_t pvr_layernorm_fwd(const uint16_t* x, int64_t x_stride, con
   return hipGetLastError();
 }
 
+// grid cap of ln_fwd_q8_kernel, in workgroups per CU (A/B: pvr_set_ln_fwd_q8_grid)
+static int g_ln_q8_blocks_per_cu = 4;
+extern "C" void pvr_set_ln_fwd_q8_grid(int per_cu) { g_ln_q8_blocks_per_cu = per_cu < 1 ? 1 : per_cu > 64 ? 64 : per_cu; }
+
 // pvr_layernorm_fwd plus the e4m3 copy yq (row stride q_stride bytes) with scale *qscale and the
 // amax record (see ln_fwd_q8_kernel)
 extern "C" hipError_t pvr_layernorm_fwd_q8(const uint16_t* x, int64_t x_stride, const float* w, const float* b, uint16_t* y,
@@ -429,7 +433,8 @@ extern "C" hipError_t pvr_layernorm_fwd_q8(const uint16_t* x, int64_t x_stride, 
   if (rows <= 0) return hipSuccess;
   if (D % 8 != 0 || D > 2048 || q_stride % 8 != 0) return hipErrorInvalidValue;
   int nblk = (rows + 3) / 4;
-  if (nblk > 1024) nblk = 1024;
+  const int cap = g_ln_q8_blocks_per_cu * device_cus();
+  if (nblk > cap) nblk = cap;
   const dim3 grid(nblk), block(256);
   switch ((D / 8 + 63) / 64) {
     case 1: hipLaunchKernelGGL(ln_fwd_q8_kernel<1>, grid, block, 0, s, x, x_stride, w, b, y, y_stride, yq, q_stride, qscale, amax, mean, rstd, rows, D, eps); break;
