@@ -112,10 +112,10 @@ class Fp8State:
     ACT_PER_BLOCK = 4  # xn1 (qkv input), o (out-proj input), xn2 (fc1 input), h (fc2 input)
 
     def __init__(self, n_blocks: int, device, history: int = 16, margin: int = 0, dgrad: bool = True, wgrad: bool = True,
-                 grad_fmt: int = E5M2):
+                 grad_fmt: int = E4M3):
         self.act = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, E4M3)
-        # gradient slots for the fp8 dgrad GEMMs (dgrad=True): dz2, dU, dx1, dQKV per block; e5m2 by
-        # default, e4m3 with grad_fmt=E4M3 (every producer of a gradient copy takes the slot's format)
+        # gradient slots for the fp8 dgrad GEMMs (dgrad=True): dz2, dU, dx1, dQKV per block; e4m3 by
+        # default, e5m2 with grad_fmt=E5M2 (every producer of a gradient copy takes the slot's format)
         if grad_fmt not in (E4M3, E5M2):
             raise ValueError(f"Fp8State: grad_fmt {grad_fmt}")
         self.grad = Fp8Meta(n_blocks * self.ACT_PER_BLOCK, device, history, margin, grad_fmt)
@@ -136,9 +136,14 @@ class Fp8State:
         return {"act": self.act.state_dict(), "grad": self.grad.state_dict(), "grad_fmt": torch.tensor(self.grad.fmt)}
 
     def load_state_dict(self, sd) -> None:
+        # the amax histories do not depend on the format (the scales are re-derived from them with the
+        # slot's fmax at every step start), so a state from before the format field loads into either;
+        # a recorded format must match for the resumed run to quantize like the original
         fmt = sd.get("grad_fmt")
         if fmt is not None and int(fmt) != self.grad.fmt:
-            raise ValueError(f"fp8 state: saved gradient format {int(fmt)} != this model's {self.grad.fmt}")
+            names = {E4M3: "e4m3", E5M2: "e5m2"}
+            raise ValueError(f"fp8 state: saved with {names.get(int(fmt), fmt)} gradients, this model uses "
+                             f"{names[self.grad.fmt]}: enable_fp8(grad_fmt='{names.get(int(fmt), fmt)}') to resume it")
         self.act.load_state_dict(sd["act"])
         self.grad.load_state_dict(sd["grad"])
 

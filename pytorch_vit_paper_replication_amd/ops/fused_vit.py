@@ -244,7 +244,7 @@ class EncoderBlockFn(torch.autograd.Function):
         own, prev = ctx.links
         f8d = ctx.f8d
 
-        # (the gradient copies below are e5m2, or e4m3 with enable_fp8(grad_fmt="e4m3"): Fp8State.grad.fmt)
+        # (the "e5m2" gradient copies below are e4m3 by default since round 6: Fp8State.grad.fmt)
         pre_q = {}  # grad slot -> (e5m2 copy, dequant scale) written by the producing dgrad epilogue
         grads8 = {}  # grad slot -> the e5m2 copy a dgrad GEMM consumed (reused by the fp8 weight gradients)
         acts8 = ctx.acts8

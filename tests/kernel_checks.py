@@ -1254,7 +1254,7 @@ def check_vit_fp8_default_producers(images=64, steps=8):
 
 
 def check_vit_fp8_dgrad(B=4):
-    """fp8 dgrad GEMMs (enable_fp8(dgrad=True): e5m2 gradients x e4m3 W^T) against the bf16 dgrads of the
+    """fp8 dgrad GEMMs (enable_fp8(dgrad=True): fp8 gradients, e4m3 by default, x e4m3 W^T) against the bf16 dgrads of the
     same fp8-forward model, PER dgrad output tensor (fc2 / fc1 / out-proj / qkv of every block, tapped
     straight from the backward) on identical calibrated forward passes; then training with them must
     decrease the loss. Per-tensor errors are printed into the test log."""
@@ -1295,7 +1295,7 @@ def check_vit_fp8_dgrad(B=4):
 
 
 def check_vit_fp8_wgrad(B=4):
-    """fp8 weight-gradient GEMMs (enable_fp8(wgrad=True): e5m2 dy^T x e4m3 x^T) against the bf16 weight
+    """fp8 weight-gradient GEMMs (enable_fp8(wgrad=True): fp8 dy^T, e4m3 by default, x e4m3 x^T) against the bf16 weight
     gradients of the same fp8 model (identical calibrated passes, fp8 dgrads in both), per encoder
     GEMM weight; then training with them must decrease the loss. Errors printed into the test log."""
     from pytorch_vit_paper_replication_amd.models import ViT
