@@ -1068,13 +1068,15 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_kernel(const uint16_t* __re
                                                              const float* __restrict__ lse, float* __restrict__ dlt,
                                                              float* __restrict__ dsl, float* __restrict__ bpart,
                                                              uint16_t* __restrict__ dqkv, int64_t ld_dq, int N, int H, int D,
-                                                             float scale, AttnQ8 q8) {
+                                                             float scale, AttnQ8 q8, int xcd) {
   constexpr int E = DH / 8;   // elements per lane (8 / 10 / 12 / 16)
   constexpr int W = E / 2;    // dwords per lane and row
   constexpr int RS = 32;      // row slots (8 per wave)
   static_assert(DH % 16 == 0 && DH <= 128, "head dim");
   __shared__ float red[3][4][DH];  // per-wave partial column sums
-  const int pr = blockIdx.x;
+  // xcd: consecutive (batch, head) pairs on one XCD, so the heads of a token row share its L2 (a dh 80
+  // head slice is 160 B: its 128-B lines straddle the neighbouring heads' slices)
+  const int pr = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int b = pr / H, h = pr % H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = lane & 7, rs = tid >> 3;  // this lane's eighth of the row, row slot
@@ -1811,6 +1813,10 @@ extern "C" void pvr_set_attn_dbg(void* p) {
 
 extern "C" void pvr_set_attn_fwd_qg(int qg) { g_attn_fwd_qg = qg == 1 || qg == 2 ? qg : 0; }
 extern "C" void pvr_set_attn_fwd_head_qf(int qf) { g_attn_fwd_head_qf = qf == 2 ? 2 : 1; }
+// backward pre-pass: (batch, head) pairs dealt XCD-contiguously (1) or round-robin (0, default: the
+// two measured equal, profiles/r6/prep/attn_ab.log); A/B
+static int g_attn_prep_xcd = 0;
+extern "C" void pvr_set_attn_prep_xcd(int on) { g_attn_prep_xcd = on ? 1 : 0; }
 
 // seed (optional): attention-probability dropout with keep threshold thr16 (see AttnDrop); the
 // backward must get the same seed / seed_off / thr16
@@ -1950,10 +1956,10 @@ static hipError_t attn_bwd_generic(const uint16_t* qkv, int64_t ld, const uint16
   float* slab = slab_path || det_slab ? ws + 2 * (int64_t)B * H * N : nullptr;  // [N / KB + 1][B*N][D] f32 partial dQ
   if (lastkey)
     hipLaunchKernelGGL((attn_bwd_prep_kernel<DH, true>), dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dlt, dsl,
-                       bpart, dqkv, ld_dq, N, H, D, scale, q8);
+                       bpart, dqkv, ld_dq, N, H, D, scale, q8, g_attn_prep_xcd);
   else
     hipLaunchKernelGGL((attn_bwd_prep_kernel<DH, false>), dim3(B * H), dim3(256), 0, s, qkv, ld, dout, ld_do, out, ld_o, lse, dlt,
-                       nullptr, bpart, dqkv, ld_dq, N, H, D, scale, q8);
+                       nullptr, bpart, dqkv, ld_dq, N, H, D, scale, q8, g_attn_prep_xcd);
   // bp: q-bias partials, passed only to the launch that writes the final dQ
   auto launch = [&](int nw, int k0, int k1, int dq_mode, float* dqa, int64_t sstride, int nslab, float* bp) {
     const int kb = nw * 32;

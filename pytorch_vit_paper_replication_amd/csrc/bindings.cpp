@@ -26,6 +26,7 @@ int pvr_gemm_tail_split(int M, int N, int K, int elem_bytes, int max_units);
 void pvr_set_attn_fwd_qg(int qg);
 void pvr_set_attn_fwd_head_qf(int qf);
 void pvr_set_ln_fwd_q8_grid(int per_cu);
+void pvr_set_attn_prep_xcd(int on);
 void pvr_set_attn_dbg(void* p);
 void pvr_set_fp8_persistent(int mode);
 hipError_t pvr_layernorm_fwd(const uint16_t*, int64_t, const float*, const float*, uint16_t*, int64_t, float*, float*, int, int, float, hipStream_t);
@@ -1109,6 +1110,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_attn_dbg", [](torch::Tensor t) { pvr_set_attn_dbg(t.defined() && t.numel() ? t.data_ptr() : nullptr); },
         "diagnostic builds (-DPVR_ATTN_STAMPS): int64 buffer for the attention backward's phase stamps "
         "[workgroup * waves + wave][8] (scripts/attn_stamps.py); a no-op otherwise");
+  m.def("set_attn_prep_xcd", &pvr_set_attn_prep_xcd, "attention backward pre-pass: XCD-contiguous (batch, head) pairs (1) or round-robin (0, default); A/B");
   m.def("set_ln_fwd_q8_grid", &pvr_set_ln_fwd_q8_grid, "LayerNorm forward with the e4m3 copy: grid cap in workgroups per CU (A/B)");
   m.def("set_attn_fwd_head_qf", &pvr_set_attn_fwd_head_qf, "whole-head attention forward (dh 64, N <= 256): 16-query fragments per wave (1 = default, 2 = half the LDS reads with 7 waves; A/B)");
   m.def("set_attn_fwd_qg", &pvr_set_attn_fwd_qg, "tiled attention forward: 16-query groups per wave (0 = auto by query padding, 1 = round-3 form, 2 = forced; A/B)");

@@ -47,6 +47,8 @@ def main():
         variants = [("qg2", lambda: ext.set_attn_fwd_qg(2)), ("qg1", lambda: ext.set_attn_fwd_qg(1))]
     elif a.ab == "hqf":
         variants = [("hqf2", lambda: ext.set_attn_fwd_head_qf(2)), ("hqf1", lambda: ext.set_attn_fwd_head_qf(1))]
+    elif a.ab == "prepxcd":  # backward pre-pass: XCD-contiguous vs round-robin (batch, head) pairs
+        variants = [("prep_xcd", lambda: ext.set_attn_prep_xcd(1)), ("prep_rr", lambda: ext.set_attn_prep_xcd(0))]
     res = {}
     data = {}
     for name in a.shapes.split(","):
@@ -62,10 +64,11 @@ def main():
             for vn, setv in order:
                 setv()
                 res.setdefault((name, "fwd", vn), []).append(timeit(lambda: ext.attn_fwd(qkv, B, N, H, dh ** -0.5)))
-            if a.bwd:
-                res.setdefault((name, "bwd", ""), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
+                if a.bwd:
+                    res.setdefault((name, "bwd", vn), []).append(timeit(lambda: ext.attn_bwd(do, qkv, o, lse, B, N, H, dh ** -0.5)))
     ext.set_attn_fwd_qg(0)
     ext.set_attn_fwd_head_qf(1)
+    ext.set_attn_prep_xcd(0)
     for name in a.shapes.split(","):
         B, N, H, dh = SHAPES[name]
         fl = 4.0 * B * H * N * N * dh
