@@ -6,10 +6,12 @@ Examples::
     python -m pytorch_vit_paper_replication_amd.cli.train --model tinyvgg --train-dir data/pizza_steak_sushi/train \
         --test-dir data/pizza_steak_sushi/test --image-size 64
     torchrun --nproc-per-node 8 -m pytorch_vit_paper_replication_amd.cli.train --synthetic ...   # RCCL DP
+    python -m pytorch_vit_paper_replication_amd.cli.train --model vit_h14 --synthetic --dtype fp8   # BASELINE config 5
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 
 import torch
 
@@ -44,6 +46,16 @@ def build_parser():
     p.add_argument("--metrics", default=None, help="append per-epoch JSONL metrics here")
     p.add_argument("--torch-optimizer", action="store_true", help="use torch.optim.Adam instead of FusedAdam")
     p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                   help="fp8: the encoder GEMMs in fp8 with delayed scaling (ViT.enable_fp8; GPU fused path only)")
+    p.add_argument("--fp8-grad", choices=["e4m3", "e5m2"], default="e4m3", help="fp8: the gradients' format")
+    p.add_argument("--fp8-bf16-wgrad", action="store_true", help="fp8: keep the weight-gradient GEMMs bf16")
+    p.add_argument("--dropout", type=float, default=None,
+                   help="override the MLP and embedding dropout of the ViT preset (0.1 = the reference's)")
+    p.add_argument("--deterministic", action="store_true",
+                   help="fixed-order reductions instead of float atomics: bitwise-repeatable gradients")
+    p.add_argument("--bucket-mb", type=float, default=28.0, help="DDP gradient bucket size (MiB)")
+    p.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32", help="DDP all-reduce wire format")
     return p
 
 
@@ -54,9 +66,12 @@ def main(argv=None) -> int:
     from ..models import TinyVGG, vit
     from ..optim import FusedAdam, param_groups_weight_decay, warmup_linear_decay
     from ..parallel import DistributedDataParallel, init_distributed, is_dist
+    from .. import _ext
     from ..utils import load_checkpoint, save_model, set_seeds
 
     args = build_parser().parse_args(argv)
+    if args.dtype == "fp8" and args.model == "tinyvgg":
+        raise SystemExit("--dtype fp8 applies to the ViT models")
     rank, world, device = init_distributed()
     set_seeds(args.seed)
     if args.synthetic or not args.train_dir:
@@ -72,7 +87,10 @@ def main(argv=None) -> int:
     if args.model == "tinyvgg":
         model = TinyVGG(input_shape=3, hidden_units=args.hidden_units, output_shape=ncls)
     else:
-        model = vit(args.model, image_size=args.image_size, num_classes=ncls)
+        drop = {} if args.dropout is None else dict(mlp_dropout=args.dropout, embedding_dropout=args.dropout)
+        model = vit(args.model, image_size=args.image_size, num_classes=ncls, **drop)
+        if args.dtype == "fp8":  # before a resume: the checkpoint's fp8 scaling state needs it
+            model.enable_fp8(wgrad=not args.fp8_bf16_wgrad, grad_fmt=args.fp8_grad)
     model.to(device)
     groups = param_groups_weight_decay(model, args.weight_decay)
     if args.torch_optimizer:
@@ -88,11 +106,14 @@ def main(argv=None) -> int:
         start_epoch, results = int(info["epoch"]), info["results"]
         if _is_rank0():
             print(f"[INFO] Resumed {args.resume} at epoch {start_epoch} of {args.epochs}")
-    net = DistributedDataParallel(model) if is_dist() else model
-    engine.train(model=net, train_dataloader=train_dl, test_dataloader=test_dl, optimizer=opt,
-                 loss_fn=torch.nn.CrossEntropyLoss(), lr_scheduler=sched, epochs=args.epochs, device=device,
-                 max_grad_norm=args.max_grad_norm, checkpoint_dir=args.checkpoint_dir, metrics_path=args.metrics,
-                 start_epoch=start_epoch, results=results)
+    net = (DistributedDataParallel(model, bucket_cap_mb=args.bucket_mb,
+                                   comm_dtype=torch.bfloat16 if args.comm_dtype == "bf16" else None)
+           if is_dist() else model)
+    with _ext.deterministic_mode() if args.deterministic else contextlib.nullcontext():
+        engine.train(model=net, train_dataloader=train_dl, test_dataloader=test_dl, optimizer=opt,
+                     loss_fn=torch.nn.CrossEntropyLoss(), lr_scheduler=sched, epochs=args.epochs, device=device,
+                     max_grad_norm=args.max_grad_norm, checkpoint_dir=args.checkpoint_dir, metrics_path=args.metrics,
+                     start_epoch=start_epoch, results=results)
     save_model(model, args.save_dir, args.save_name or f"{args.model}_{args.epochs}_epochs.pth")
     return 0
 

@@ -43,3 +43,29 @@ def test_cli_imagefolder_tinyvgg(tmp_path):
                "--num-workers", "0", "--save-dir", str(tmp_path), "--save-name", "t.pth"])
     assert rc == 0
     assert (tmp_path / "t.pth").exists()
+
+
+def test_cli_fp8_and_options(tmp_path, monkeypatch):
+    """--dtype fp8 / --fp8-grad / --dropout / --deterministic reach the model and the run (on the CPU the
+    fused fp8 path does not engage: the reference math runs, the configuration is still recorded)."""
+    from pytorch_vit_paper_replication_amd.cli import train as T
+    from pytorch_vit_paper_replication_amd.models import presets
+
+    made = []
+    orig = presets.vit
+
+    def spy(*a, **kw):
+        m = orig(*a, **kw)
+        made.append(m)
+        return m
+
+    monkeypatch.setattr("pytorch_vit_paper_replication_amd.models.vit", spy)
+    rc = T.main(["--model", "vit_tiny_test", "--synthetic", "--epochs", "1", "--batch-size", "4", "--image-size", "32",
+                 "--num-classes", "3", "--synthetic-train-len", "8", "--synthetic-test-len", "4", "--save-dir", str(tmp_path),
+                 "--dtype", "fp8", "--fp8-grad", "e5m2", "--dropout", "0.0", "--deterministic"])
+    assert rc == 0 and made
+    m = made[0]
+    assert m._fp8_cfg is not None and m._fp8_cfg[3] is True and m._fp8_cfg[4] == "e5m2"
+    assert all(mod.p == 0.0 for mod in m.modules() if isinstance(mod, torch.nn.Dropout))
+    a = T.build_parser().parse_args([])
+    assert a.dtype == "bf16" and a.fp8_grad == "e4m3" and a.comm_dtype == "fp32" and not a.deterministic
