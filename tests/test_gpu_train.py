@@ -632,6 +632,25 @@ def test_deterministic_mode_gradients_bitwise_repeatable():
         assert torch.equal(a, b), n
 
 
+def test_deterministic_mode_long_sequence_attention_slabs():
+    """Deterministic mode through the model at N = 401 (320 px / 16 + CLS = 256 + 145: two key blocks,
+    neither the last-key nor the tail-split path), where the attention backward's dQ goes through
+    per-key-block slabs summed in order: two backward passes give bit-identical gradients."""
+    from pytorch_vit_paper_replication_amd import _ext
+    from pytorch_vit_paper_replication_amd.models import ViT
+
+    torch.manual_seed(0)
+    m = ViT(**dict(CFG, image_size=320, embedding_dim=128, num_heads=2, mlp_size=256, mlp_dropout=0.0,
+                   embedding_dropout=0.0)).cuda()
+    x = torch.rand(4, 3, 320, 320, device="cuda")
+    y = torch.randint(0, 10, (4,), device="cuda")
+    with _ext.deterministic_mode():
+        g1, g2 = _grads(m, x, y), _grads(m, x, y)
+    for (n, _), a, b in zip(m.named_parameters(), g1, g2):
+        assert torch.equal(a, b), n
+        assert torch.isfinite(a).all(), n
+
+
 def _det_model_and_batch():
     from pytorch_vit_paper_replication_amd.models import ViT
 
