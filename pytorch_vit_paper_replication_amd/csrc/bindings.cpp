@@ -733,7 +733,8 @@ void gemm_fp8(torch::Tensor A, int64_t fmt_a, torch::Tensor B, int64_t fmt_b, to
   if (bias.has_value() && bias->defined()) { TORCH_CHECK(bias->numel() >= N && bias->is_contiguous(), "bias"); p.bias = f32(*bias, "bias"); }
   if (resid.has_value() && resid->defined()) { p.resid = bf(*resid, "resid"); p.ld_resid = ld_of(*resid, "resid"); }
   if (aux.has_value() && aux->defined()) { p.aux = const_cast<uint16_t*>(bf(*aux, "aux")); p.ld_aux = ld_of(*aux, "aux"); }
-  if (epi == 1 || epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm_fp8: GELU epilogues need aux");
+  // GELU without aux: the inference epilogue (no derivative stored; its stores go to a 0-byte range)
+  if (epi == 2) TORCH_CHECK(p.aux != nullptr, "gemm_fp8: the dGELU epilogue needs aux");
   if (colsum.has_value() && colsum->defined()) p.colsum = f32_mut(*colsum, "colsum");
   if (q_out.has_value() && q_out->defined()) {
     // fp8 copy of the GELU / dGELU output from the register-direct epilogue (its preconditions:

@@ -271,19 +271,20 @@ def layernorm_fwd_q8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: flo
 def linear_fwd_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
                    bias: Optional[torch.Tensor] = None, *, resid: Optional[torch.Tensor] = None, drop=None,
                    gelu_aux: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, quant=None,
-                   skip_out: bool = False):
+                   skip_out: bool = False, gelu: bool = False):
     """y = resid + dropout(dequant(xq . wq^T) + bias), or the GELU variant (see gemm.linear_fwd).
 
     ``quant=(meta, slot)`` (GELU variant, a calibrated slot: ``Fp8Meta.producer``): the epilogue also
     writes y's fp8 copy with the slot's delayed scale and records y's amax, so the next GEMM needs no
     quantize pass; returns ``(y, (y_fp8, dequant scale))`` then. ``skip_out`` (with ``quant``): the bf16
-    y is not stored (allocated, unwritten) - for when every consumer reads the fp8 copy."""
+    y is not stored (allocated, unwritten) - for when every consumer reads the fp8 copy. ``gelu=True``
+    without ``gelu_aux``: the GELU epilogue for inference (no derivative stored)."""
     T, K = xq.shape
     N = wq.shape[0]
     if out is None:
         out = torch.empty(T, N, dtype=torch.bfloat16, device=xq.device)
     seed, soff, p = gemm._drop_args(drop)
-    epi = gemm.EPI_GELU if gelu_aux is not None else gemm.EPI_BF16
+    epi = gemm.EPI_GELU if (gelu or gelu_aux is not None) else gemm.EPI_BF16
     kw, q = _quant_args(quant, T, N, xq.device)
     _ext.ext().gemm_fp8(xq, E4M3, wq, E4M3, out, T, N, K, epi, xs, ws, bias, resid, gelu_aux, seed, soff, p,
                         c_skip=bool(skip_out and quant is not None), **kw)

@@ -153,14 +153,17 @@ class EncoderBlockFn(torch.autograd.Function):
         # mode): the fc1 epilogue stores no GELU derivative and nothing is saved for a backward
         need_bwd = getattr(store, "grad_enabled", True) and any(ctx.needs_input_grad)
         u = (torch.empty(T, M, dtype=torch.bfloat16, device=x.device)  # receives mask*scale*gelu'(pre-act)
-             if need_bwd or f8 is not None else None)
+             if need_bwd else None)
         q1 = f8[0].act_producer(f8[1], 0) if f8 is not None else None
 
         def fp8_only(which_grad: int, which_act: int) -> bool:
             # the bf16 activation is read by nothing but the weight gradient of (gradient slot, activation
             # slot), and that one is certain to run in fp8 from the activation's e4m3 copy (both slots
-            # calibrated, so they stay so): the producer then stores only the fp8 copy (HBM writes saved)
-            return (need_bwd and ctx.f8d is not None and T >= 256 and DGRAD_TAP is None
+            # calibrated, so they stay so): the producer then stores only the fp8 copy (HBM writes saved).
+            # Inference: the next GEMM reads the e4m3 copy and nothing is saved, so no bf16 copy either
+            if not need_bwd:
+                return T >= 256 and DGRAD_TAP is None
+            return (ctx.f8d is not None and T >= 256 and DGRAD_TAP is None
                     and f8[0].wgrad_ready(f8[1], which_grad, which_act))
 
         if q1 is not None:  # fp8 forward, calibrated: xn1's e4m3 copy from the LayerNorm itself
@@ -213,7 +216,7 @@ class EncoderBlockFn(torch.autograd.Function):
             acts8.append(a)
             hq = st.act_producer(blk, 3)  # h's e4m3 copy from the fc1 epilogue (calibrated slot)
             skip_h = hq is not None and fp8_only(0, 3)
-            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq, skip_out=skip_h)
+            h = F8.linear_fwd_fp8(a, s_, *wq[2], b1, gelu_aux=u, drop=drop1, quant=hq, skip_out=skip_h, gelu=True)
             if hq is not None:
                 h, (a, s_) = h
                 _poison(h, skip_h)

@@ -1589,6 +1589,44 @@ def check_vit_inference(B=5):
             lim(2.1e-2, 2.8e-2, not_bit_identical=0, no_grad_after=0))
 
 
+def check_vit_fp8_inference(B=8):
+    """fp8 inference (eval under inference_mode / no_grad): the fc1 GELU epilogue stores no derivative
+    and the LayerNorm / fc1 producers write only the e4m3 copies the next GEMM reads (no bf16 xn1 /
+    xn2 / h: filled with NaN here, POISON_SKIPPED). Once the slots are calibrated, the logits equal
+    the grad-mode fp8 forward (which writes every copy) bit for bit and stay within the fp8 forward
+    error of the fp32 reference; a training step afterwards still gets finite gradients."""
+    from pytorch_vit_paper_replication_amd.models import ViT
+    from pytorch_vit_paper_replication_amd.ops import fused_vit
+
+    torch.manual_seed(0)
+    m = ViT(**_FP8_CFG).to(DEV).eval().enable_fp8()
+    mr = ViT(**_FP8_CFG).to(DEV).eval()
+    mr.load_state_dict(m.state_dict())
+    x = torch.rand(B * 4, 3, 64, 64, device=DEV)  # 544 tokens: the fp8 path (>= 256)
+    m(x)  # calibrates the activation slots (eval: the scales stay put afterwards)
+    assert m._fp8 is not None and all(m._fp8.act.calibrated), "fp8 path did not engage / calibrate"
+    lg = m(x)
+    fused_vit.POISON_SKIPPED = True
+    try:
+        with torch.inference_mode():
+            li = m(x)
+        with torch.no_grad():
+            ln = m(x)
+    finally:
+        fused_vit.POISON_SKIPPED = False
+    with torch.no_grad():
+        lr = _reference_logits(mr, x)
+    same = torch.equal(lg.detach(), li) and torch.equal(li, ln)
+    m.train()
+    F.cross_entropy(m(x), torch.randint(0, 10, (B * 4,), device=DEV)).backward()
+    has_grad = all(p.grad is not None and torch.isfinite(p.grad).all().item() for p in m.parameters())
+    met = worst((li, lr))
+    met.update(not_bit_identical=float(not same), nonfinite=float(not torch.isfinite(li).all().item()),
+               no_grad_after=float(not has_grad))
+    return ("vit fp8 inference (no derivative, e4m3 copies only) == grad-mode fp8 logits, vs fp32 ref", met,
+            lim(8.5e-2, 1e-1, not_bit_identical=0, nonfinite=0, no_grad_after=0))
+
+
 def check_vit_dropout_fused(B=4):
     """Training with every dropout on (embedding, MLP, attention probabilities p = 0.1) stays on the
     HIP path (fused forward engaged; the attention kernels draw the mask in-register): replaying the
@@ -1852,6 +1890,7 @@ def all_checks() -> List[Callable[[], Result]]:
         lambda: check_attn_bwd_det(2, 677, 2),
         lambda: check_attn_bwd_det(2, 677, 3, 64, True),
         lambda: check_attn_bwd_det(1, 400, 2, 80),
+        check_vit_fp8_inference,
     ]
     return c
 
