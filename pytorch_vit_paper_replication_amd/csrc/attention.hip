@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
         uint2 w;
         w.x = pack2bf(o[gi][e][0] * inv, o[gi][e][1] * inv);
         w.y = pack2bf(o[gi][e][2] * inv, o[gi][e][3] * inv);
-        *(uint2*)(orow + 16 * e + 4 * g) = w;
+        if (!q8.only) *(uint2*)(orow + 16 * e + 4 * g) = w;  // only: inference reads the e4m3 copy alone
       }
       if (q8.out) {  // e4m3 copy for the fp8 out-proj GEMM
         uint8_t* qrow = q8.out + ((int64_t)b * N + q) * q8.ld + h * DH;
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) a
 #pragma unroll
       for (int k = 0; k < (16 * OC + 63) / 64; ++k) {
         const int ch = lane + 64 * k, row = ch / OC, cc = ch % OC;
-        if (ch < 16 * OC && row < nrow)
+        if (ch < 16 * OC && row < nrow && !q8.only)
           *(uint4*)((char*)(out + ((int64_t)b * N + r0 + row) * ld_o + h * DH) + cc * 16) = *(const uint4*)(st + row * OB + cc * 16);
       }
       if (qon) {
@@ -1822,12 +1822,14 @@ extern "C" void pvr_set_attn_prep_xcd(int on) { g_attn_prep_xcd = on ? 1 : 0; }
 // backward must get the same seed / seed_off / thr16
 extern "C" hipError_t pvr_attn_fwd(const uint16_t* qkv, int64_t ld, uint16_t* out, int64_t ld_o, float* lse, int B, int N,
                                    int H, int D, float scale, const uint64_t* seed, uint64_t seed_off, uint32_t thr16, float keep_scale,
-                                   uint8_t* q8_out, int64_t q8_ld, const float* q8_qs, unsigned* q8_amax, hipStream_t s) {
+                                   uint8_t* q8_out, int64_t q8_ld, const float* q8_qs, unsigned* q8_amax, int q8_only, hipStream_t s) {
   using namespace pvr;
   if (H <= 0 || D % H != 0 || B <= 0 || N <= 0 || N > 65536) return hipErrorInvalidValue;
   if (q8_out && (!q8_qs || !q8_amax || q8_ld % 4 != 0 || (uintptr_t)q8_out % 4 != 0)) return hipErrorInvalidValue;
+  if (q8_only && !q8_out) return hipErrorInvalidValue;
   const AttnDrop drop{seed, seed_off, thr16, keep_scale};
-  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, 0};
+  // only (inference): O's e4m3 copy alone is stored (bf16 O unwritten); the copy's path is the generic kernel
+  const AttnQ8 q8{q8_out, q8_ld, q8_qs, q8_amax, q8_only ? 1 : 0};
   switch (D / H) {
     case 64: return attn_fwd_launch<64>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);
     case 80: return attn_fwd_launch<80>(qkv, ld, out, ld_o, lse, B, N, H, D, scale, drop, q8, s);

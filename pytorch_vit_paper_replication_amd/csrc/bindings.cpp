@@ -75,7 +75,7 @@ int pvr_attn_bwd_waves(int);
 int pvr_attn_bwd_uses_pipe(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
 int pvr_attn_bwd_part_rows(int, int, int, int, int64_t, int64_t, int64_t, int64_t, int);
 hipError_t pvr_attn_fwd(const uint16_t*, int64_t, uint16_t*, int64_t, float*, int, int, int, int, float, const uint64_t*, uint64_t,
-                        uint32_t, float, uint8_t*, int64_t, const float*, unsigned*, hipStream_t);
+                        uint32_t, float, uint8_t*, int64_t, const float*, unsigned*, int, hipStream_t);
 int pvr_attn_dbias_splits(int, int);
 hipError_t pvr_splitk_epilogue(const float*, int, int64_t, int, int, const float*, const uint16_t*, int64_t, int, uint16_t*, int64_t,
                                hipStream_t);
@@ -912,10 +912,11 @@ void fp8_scale_update(torch::Tensor hist, torch::Tensor amax, torch::Tensor qsca
 // seed / seed_offset / drop_p: attention-probability dropout (the backward gets the same three)
 std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int64_t H, double scale, c10::optional<torch::Tensor> seed,
                                     int64_t seed_offset, double drop_p, c10::optional<torch::Tensor> q_out,
-                                    c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax) {
+                                    c10::optional<torch::Tensor> q_scale, c10::optional<torch::Tensor> q_amax, bool q_only) {
   const int64_t D = qkv.size(1) / 3;
   auto out = torch::empty({B * N, D}, qkv.options());
   auto lse = torch::empty({B * H, N}, qkv.options().dtype(torch::kFloat32));
+  TORCH_CHECK(!q_only || (q_out.has_value() && q_out->defined()), "attn_fwd: q_only needs q_out");
   TORCH_CHECK(qkv.size(0) == B * N, "attn_fwd: qkv rows != B*N");
   const DropArgs d = drop_args(seed, drop_p, "attn_fwd");
   uint8_t* q8 = nullptr;
@@ -936,7 +937,8 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t B, int64_t N, int
     q8_amax = reinterpret_cast<unsigned*>(q_amax->data_ptr<int32_t>());
   }
   check(pvr_attn_fwd(bf(qkv, "qkv"), ld_of(qkv, "qkv"), bf_mut(out, "out"), D, f32_mut(lse, "lse"), (int)B, (int)N, (int)H, (int)D,
-                     (float)scale, d.seed, (uint64_t)seed_offset, d.thr, d.scale, q8, q8_ld, q8_qs, q8_amax, stream()),
+                     (float)scale, d.seed, (uint64_t)seed_offset, d.thr, d.scale, q8, q8_ld, q8_qs, q8_amax, q_only ? 1 : 0,
+                     stream()),
         "attn_fwd");
   return {out, lse};
 }
@@ -1182,7 +1184,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("amax_only"));
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("B"), py::arg("N"), py::arg("H"), py::arg("scale"),
         py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0, py::arg("q_out") = py::none(),
-        py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none());
+        py::arg("q_scale") = py::none(), py::arg("q_amax") = py::none(), py::arg("q_only") = false);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("B"), py::arg("N"),
         py::arg("H"), py::arg("scale"), py::arg("dbias") = py::none(), py::arg("dbias_part") = py::none(),
         py::arg("seed") = py::none(), py::arg("seed_offset") = 0, py::arg("drop_p") = 0.0, py::arg("q_out") = py::none(),

@@ -197,8 +197,11 @@ class EncoderBlockFn(torch.autograd.Function):
             qo = st.act_producer(blk, 1)  # o's e4m3 copy from the attention forward (calibrated slot)
             if qo is not None:
                 a = torch.empty(T, D, dtype=torch.uint8, device=x.device)
+                # inference: only o's e4m3 copy is read (the out-proj GEMM); the bf16 o is not stored
+                o_only = not need_bwd and T >= 256 and DGRAD_TAP is None
                 o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap, a, qo[0].qscale[qo[1]:qo[1] + 1],
-                                      qo[0].amax[qo[1]:qo[1] + 1])
+                                      qo[0].amax[qo[1]:qo[1] + 1], q_only=o_only)
+                _poison(o, o_only)
                 s_ = qo[0].dscale[qo[1]:qo[1] + 1]
             else:
                 o, lse = ext.attn_fwd(qkv, B, N, H, scale, aseed, aoff, ap)
